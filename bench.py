@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""bench.py -- headline benchmark of the MI355X DiPs difference-series path.
+
+Metric (BASELINE.json): frames/s + achieved HBM GB/s (% of roofline), 4K RGB8,
+1/2/4/8 GPUs.  Workload at N GPUs: BASELINE.json configs[2] per GPU --
+3840x2160 RGB8 synthetic frames, 5000 per GPU, 'per-frame' mode -- weakly
+scaled: rank k owns global frames [k*F, (k+1)*F), receives the halo frame
+k*F-1 from rank k-1 (RCCL send/recv) and rank 0 gathers the per-frame series
+(one RCCL gather).  `--mode overall` runs configs[3]'s mode instead (the
+reference frame is broadcast once at setup).
+
+A step = one pass of the hot path over the rank's resident frame batch:
+series kernel + reduction (+ halo exchange + series gather when N > 1).
+Frames are generated into HBM by the shared integer generator before timing.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE).
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/s + achieved HBM GB/s (% of roofline), 4K RGB8, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0   # MI355X spec (MI355X_MICROARCH.md "Chip-level parameters")
+SEED = 0xD1B5
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames-per-gpu", type=int, default=5000)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--mode", choices=["per-frame", "overall"], default="per-frame")
+    ap.add_argument("--tau", type=float, default=8.0 / 255.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target CPU work of the cpu_baseline sample")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="HBM traffic per launch measured by profiles/collect_pmc.sh")
+    return ap.parse_args()
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_baseline(frames_dev, mode: int, tau: float, target_s: float):
+    """The oracle ('port' of the reference semantics) timed on this host's
+    cores on a bounded prefix of the same frames (per-frame cost is constant)."""
+    from oracle import oracle
+    try:
+        path = oracle.build(native=True)
+        lib = oracle.load(path)
+        build = "gcc -O3 -march=native -ffp-contract=off"
+    except Exception:  # pragma: no cover - no compiler on the box
+        lib = oracle.load()
+        build = "gcc -O3 -ffp-contract=off (prebuilt)"
+    threads = max(1, min(16, os.cpu_count() or 1))
+    probe = frames_dev[:threads].cpu().numpy()
+    t = time.perf_counter()
+    oracle.series(probe, mode=mode, tau=tau, nthreads=threads, lib=lib)
+    per_round = time.perf_counter() - t  # `threads` frames in parallel
+    rounds = int(max(1, min(12, target_s / max(per_round, 1e-3))))
+    n = min(frames_dev.shape[0], threads * rounds)
+    sample = frames_dev[:n].cpu().numpy()
+    t = time.perf_counter()
+    oracle.series(sample, mode=mode, tau=tau, nthreads=threads, lib=lib)
+    dt = time.perf_counter() - t
+    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} frames of the same synthetic 4K RGB8 batch, series only "
+                      f"(oracle/dips_oracle.c, {build}, {threads} threads over frame ranges), "
+                      f"{dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+
+    W, H, F = args.width, args.height, args.frames_per_gpu
+    C = 3
+    fb = W * H * C
+    mode = Mode.PerFrame if args.mode == "per-frame" else Mode.Overall
+    op = DiffSeriesOperator(PixelFormat.RGB8, mode, args.tau, time_kernel=True, device=local)
+
+    t0 = rank * F  # global frame index of this rank's first frame
+    frames = torch.empty((F, H, W, C), dtype=torch.uint8, device=dev)
+    op.synth_device(frames, W, H, SEED, t0)
+    series = torch.zeros((F, 4), dtype=torch.int64, device=dev)
+    ref = torch.empty((H, W, C), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    log(f"rank {rank}: {F} frames {W}x{H} RGB8 = {F * fb / 1e9:.1f} GB generated in HBM")
+
+    # Reference frame of the rank's first frame.
+    if mode == Mode.Overall:
+        if rank == 0:
+            ref.copy_(frames[0])
+        if world > 1:
+            dist.broadcast(ref, src=0)   # once per job: the reference is fixed
+    gathered = torch.zeros((world * F, 4), dtype=torch.int64, device=dev) if rank == 0 else None
+
+    def step():
+        r = None
+        if mode == Mode.Overall:
+            r = ref
+        elif world > 1:
+            ops = []
+            if rank + 1 < world:
+                ops.append(dist.P2POp(dist.isend, frames[F - 1], rank + 1))
+            if rank > 0:
+                ops.append(dist.P2POp(dist.irecv, ref, rank - 1))
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            r = ref if rank > 0 else None
+        op.run_device(frames, series, ref=r)
+        if world > 1:
+            dist.gather(series, [gathered[k * F:(k + 1) * F] for k in range(world)] if rank == 0 else None, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    op.kernel_time(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t
+    kms, launches = op.kernel_time()
+    tt = torch.tensor([elapsed, kms / max(launches, 1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed_max, kernel_ms = float(tt[0]), float(tt[1])
+
+    if rank == 0:
+        # validity: the gathered series must be the series of frames 0..N*F-1
+        final = (gathered if world > 1 else series).cpu().numpy().view(np.uint64)
+        assert final.shape == (world * F, 4)
+        if mode == Mode.PerFrame:
+            assert final[0].sum() == 0  # frame 0 against itself
+        waves, tiles, pbytes = op.geometry(W, H, F)
+        algo_bytes = F * fb  # each frame read once per launch
+        achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
+        traffic = None
+        pmc_note = None
+        if os.path.exists(args.pmc_json):
+            try:
+                with open(args.pmc_json) as f:
+                    pmc = json.load(f)
+                if (pmc.get("width"), pmc.get("height"), pmc.get("frames"), pmc.get("mode")) == (W, H, F, args.mode):
+                    traffic = pmc.get("hbm_bytes_per_launch")
+                    pmc_note = pmc.get("source")
+            except Exception:
+                traffic = None
+        value = world * F * args.steps / elapsed_max
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(frames, int(mode), args.tau, args.cpu_seconds)
+            except Exception as e:  # report, never hide
+                cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port",
+                       "sample": f"failed: {e}"}
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (shared integer-hash generator, frames generated in HBM)",
+            "config": {
+                "workload": f"{W}x{H} RGB8, {F} frames per GPU, '{args.mode}' mode, tau={args.tau:.6g} "
+                            f"(BASELINE.json configs[{2 if mode == Mode.PerFrame else 3}] per-GPU slice)",
+                "frames_per_gpu": F, "width": W, "height": H, "mode": args.mode,
+                "parallelism": f"frame-range x{world}" + (" + RCCL halo send/recv + gather" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "series_fast_kernel<3,0,4,PF,false>",
+                "kernel_ms": round(kernel_ms, 4),
+                "algorithmic_bytes_per_launch": algo_bytes,
+                "partial_bytes_per_launch": int(pbytes) * F,
+                "waves": int(waves),
+                **({"traffic_source": pmc_note} if pmc_note else {}),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    op.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+"""ctypes binding of the C ABI in include/dips_hip.h (libdips_hip.so).
+
+The product path always runs through this library: if the shared object is
+missing or fails to load, every entry point raises ``DipsLibraryError`` --
+there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+from typing import List, Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdips_hip.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dips_hip.h")
+
+DIPS_OK = 0
+DIPS_ERR_INVALID = -1
+DIPS_ERR_HIP = -2
+DIPS_ERR_STATE = -3
+DIPS_ERR_NOMEM = -4
+DIPS_ERR_CAPACITY = -5
+DIPS_ERR_NODEVICE = -6
+
+FLAG_DEVICE_PTRS = 0x1
+FLAG_TIME_KERNEL = 0x2
+FLAG_FORCE_GENERIC = 0x4
+
+FMT_GRAY8 = 1
+FMT_RGB8 = 3
+FMT_RGBA8 = 4
+MODE_OVERALL = 0
+MODE_PER_FRAME = 1
+
+
+class DipsLibraryError(RuntimeError):
+    """libdips_hip.so is missing or unusable."""
+
+
+class DipsError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"dips status {status}: {message}")
+        self.status = status
+
+
+class DipsParams(ctypes.Structure):
+    _fields_ = [
+        ("colorize", ctypes.c_uint8),
+        ("spatial_window_size", ctypes.c_int32),
+        ("sensitivity", ctypes.c_float),
+        ("filter_type", ctypes.c_uint32),
+        ("chroma_filter", ctypes.c_uint32),
+        ("mode", ctypes.c_uint32),
+        ("format", ctypes.c_uint32),
+        ("tau", ctypes.c_float),
+        ("flags", ctypes.c_uint32),
+    ]
+
+
+class SeriesEntry(ctypes.Structure):
+    _fields_ = [
+        ("sad", ctypes.c_uint64),
+        ("sj", ctypes.c_uint64),
+        ("count", ctypes.c_uint64),
+        ("si_fixed", ctypes.c_uint64),
+    ]
+
+
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+_vp = ctypes.c_void_p
+_u8p = ctypes.c_void_p  # raw pointers (host or device) are passed as integers
+
+
+def header_functions() -> List[str]:
+    """Names of every function declared in include/dips_hip.h."""
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(dips_[a-z_0-9]+)\s*\(", text, flags=re.M)
+
+
+def _share_torch_hip_runtime() -> None:
+    """Make the process use ONE HIP runtime.
+
+    torch ships its own libamdhip64 (soname libamdhip64.so.7, NEEDED by torch
+    as "libamdhip64.so").  Loaded after libdips_hip.so, torch would map a
+    second HIP runtime next to /opt/rocm's and fail to initialise; loaded
+    first, its runtime satisfies libdips_hip.so's NEEDED entry by soname and
+    device pointers / streams are shared.  So: import torch and initialise
+    its HIP context before loading the library (no-op without torch/GPU)."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        _share_torch_hip_runtime()
+        if not os.path.exists(LIB_PATH):
+            raise DipsLibraryError(
+                f"{LIB_PATH} not found: build it with `make -C dips_amd/csrc` "
+                "or __graft_entry__.build() (the HIP path has no fallback)")
+        try:
+            lib = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the box
+            raise DipsLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        P = ctypes.POINTER
+        i32, u32, u64, f32 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_float
+        st = ctypes.c_int
+        sig = {
+            "dips_abi_version": ([], st),
+            "dips_params_default": ([P(DipsParams)], st),
+            "dips_create": ([P(DipsParams), st, P(_vp)], st),
+            "dips_destroy": ([_vp], None),
+            "dips_last_error": ([_vp], ctypes.c_char_p),
+            "dips_set_stream": ([_vp, _vp], st),
+            "dips_synchronize": ([_vp], st),
+            "dips_add_texture": ([_vp, u32, u32, _u8p, ctypes.c_size_t], st),
+            "dips_dispatch": ([_vp, _u8p, ctypes.c_size_t], st),
+            "dips_frame_callback": ([_vp, u32, u32, _u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t], st),
+            "dips_start_texture": ([_vp, _u8p, ctypes.c_size_t], st),
+            "dips_diff_series": ([_vp, u32, u32, _u8p, u32, _u8p, _vp, _u8p], st),
+            "dips_series_si": ([P(SeriesEntry)], ctypes.c_double),
+            "dips_diff_series_streamed": ([_vp, u32, u32, _u8p, u32, _u8p, _vp, u32], st),
+            "dips_synth_frames": ([_vp, u32, u32, u64, u64, u32, _u8p], st),
+            "dips_kernel_time": ([_vp, P(ctypes.c_double), P(u64)], st),
+            "dips_kernel_time_reset": ([_vp], st),
+            "dips_series_geometry": ([_vp, u32, u32, u32, P(u64), P(u64), P(u64)], st),
+        }
+        del i32, f32
+        for name, (args, res) in sig.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = lib
+        return lib
+
+
+def check(status: int, handle=None) -> int:
+    if status < 0:
+        lib = load()
+        msg = lib.dips_last_error(handle)
+        raise DipsError(status, msg.decode() if msg else "")
+    return status

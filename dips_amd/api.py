@@ -1,0 +1,405 @@
+"""Host-side mirror of the reference operator surface, over the C ABI.
+
+Reference surface (RubenMovsesyan/DiPs, crate ``dips``):
+  DiPsFilter / ChromaFilter        dips/src/lib.rs:25-61
+  DiPsProperties (builder)         dips/src/lib.rs:63-170
+  ComputeState::new/add_texture/dispatch   dips/src/gpu/mod.rs:59, :170, :306
+  frame_callback                   dips/src/lib.rs:233-246
+plus the north-star batch path (per-frame difference series), which has no
+reference counterpart beyond the per-pixel math of dips_shader.wgsl:64-82.
+Every call goes to libdips_hip.so; there is no Python compute path.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from dataclasses import dataclass
+from typing import Callable, Iterable, Iterator, Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import DipsError, DipsParams, SeriesEntry, check
+
+
+class DiPsFilter(enum.IntEnum):
+    """dips/src/lib.rs:25-41; the value is the WGSL override id 3 code."""
+    Unfiltered = 255
+    Sigmoid = 0
+    InverseSigmoid = 1
+
+
+class ChromaFilter(enum.IntEnum):
+    """dips/src/lib.rs:43-61; the value is the WGSL override id 4 code."""
+    None_ = 0
+    Red = 1
+    Green = 2
+    Blue = 3
+
+
+class PixelFormat(enum.IntEnum):
+    Gray8 = _lib.FMT_GRAY8
+    RGB8 = _lib.FMT_RGB8
+    RGBA8 = _lib.FMT_RGBA8
+
+
+class Mode(enum.IntEnum):
+    Overall = _lib.MODE_OVERALL     # against frame 0 (README.md:7)
+    PerFrame = _lib.MODE_PER_FRAME  # against the previous frame (README.md:8-10)
+
+
+class VideoPathNotSpecifiedError(Exception):
+    """dips/src/lib.rs:173-186"""
+
+
+class FrameCallbackNotSpecifiedError(Exception):
+    """dips/src/lib.rs:188-201"""
+
+
+class DiPsProperties:
+    """Builder mirroring dips/src/lib.rs:63-170 (defaults :74-86)."""
+
+    def __init__(self) -> None:
+        self._video_path: Optional[str] = None
+        self._frame_callback: Optional[Callable] = None
+        self._output_path: Optional[str] = None
+        self.colorize_: bool = False
+        self.spatial_window_size_: int = 1
+        self.sensitivity_: float = 5.0
+        self.filter_type_: DiPsFilter = DiPsFilter.Unfiltered
+        self.chroma_filter_: ChromaFilter = ChromaFilter.None_
+
+    @classmethod
+    def new(cls) -> "DiPsProperties":
+        return cls()
+
+    def video_path(self, p: str) -> "DiPsProperties":
+        self._video_path = str(p)
+        return self
+
+    def frame_callback(self, cb: Callable) -> "DiPsProperties":
+        self._frame_callback = cb
+        return self
+
+    def output_path(self, p: str) -> "DiPsProperties":
+        self._output_path = str(p)
+        return self
+
+    def colorize(self, v: bool) -> "DiPsProperties":
+        self.colorize_ = bool(v)
+        return self
+
+    def spatial_window_size(self, v: int) -> "DiPsProperties":
+        self.spatial_window_size_ = int(v)
+        return self
+
+    def sensitivity(self, v: float) -> "DiPsProperties":
+        self.sensitivity_ = float(v)
+        return self
+
+    def filter_type(self, v: DiPsFilter) -> "DiPsProperties":
+        self.filter_type_ = DiPsFilter(v)
+        return self
+
+    def chroma_filter(self, v: ChromaFilter) -> "DiPsProperties":
+        self.chroma_filter_ = ChromaFilter(v)
+        return self
+
+    def get_video_path(self) -> Optional[str]:
+        return self._video_path
+
+    def get_output_path(self) -> Optional[str]:
+        return self._output_path
+
+    def get_frame_callback(self) -> Optional[Callable]:
+        return self._frame_callback
+
+    def build(self) -> "DiPsProperties":
+        out = DiPsProperties()
+        out.__dict__.update(self.__dict__)
+        return out
+
+
+def _params(colorize=False, spatial_window_size=1, sensitivity=5.0,
+            filter_type=DiPsFilter.Unfiltered, chroma_filter=ChromaFilter.None_,
+            mode=Mode.Overall, fmt=PixelFormat.RGB8, tau=0.0, flags=0) -> DipsParams:
+    p = DipsParams()
+    check(_lib.load().dips_params_default(ctypes.byref(p)))
+    p.colorize = 1 if colorize else 0
+    p.spatial_window_size = int(spatial_window_size)
+    p.sensitivity = float(sensitivity)
+    p.filter_type = int(filter_type)
+    p.chroma_filter = int(chroma_filter)
+    p.mode = int(mode)
+    p.format = int(fmt)
+    p.tau = float(tau)
+    p.flags = int(flags)
+    return p
+
+
+class _Handle:
+    def __init__(self, params: DipsParams, device: int = 0):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        st = self._lib.dips_create(ctypes.byref(params), int(device), ctypes.byref(h))
+        check(st, None)
+        self._h = h
+        self.params = params
+        self.device = device
+
+    @property
+    def ptr(self) -> ctypes.c_void_p:
+        if self._h is None:
+            raise DipsError(_lib.DIPS_ERR_STATE, "handle destroyed")
+        return self._h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None:
+            self._lib.dips_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, st: int) -> int:
+        return check(st, self._h)
+
+
+def _as_u8(frame) -> np.ndarray:
+    a = np.ascontiguousarray(frame)
+    if a.dtype != np.uint8:
+        a = a.astype(np.uint8)
+    return a
+
+
+class ComputeState:
+    """Drop-in for dips/src/gpu/mod.rs ComputeState on a HIP device."""
+
+    def __init__(self, colorize: bool, spatial_window_size: int, sensitivity: float,
+                 filter_type: DiPsFilter, chroma_filter: ChromaFilter, device: int = 0):
+        self._hd = _Handle(_params(colorize, spatial_window_size, sensitivity, filter_type,
+                                   chroma_filter, fmt=PixelFormat.RGBA8), device)
+        self._w = 0
+        self._h = 0
+
+    @classmethod
+    def new(cls, colorize, spatial_window_size, sensitivity, filter_type, chroma_filter,
+            device: int = 0) -> "ComputeState":
+        return cls(colorize, spatial_window_size, sensitivity, filter_type, chroma_filter, device)
+
+    def add_texture(self, width: int, height: int, frame_data) -> None:
+        a = _as_u8(frame_data)
+        self._hd.check(self._hd._lib.dips_add_texture(self._hd.ptr, width, height,
+                                                      a.ctypes.data, a.nbytes))
+        self._w, self._h = width, height
+
+    def dispatch(self) -> Optional[np.ndarray]:
+        out = np.empty((self._h, self._w, 4), dtype=np.uint8)
+        r = self._hd.check(self._hd._lib.dips_dispatch(self._hd.ptr, out.ctypes.data, out.nbytes))
+        return out if r == 1 else None
+
+    def start_texture(self) -> Optional[np.ndarray]:
+        out = np.empty((self._h, self._w, 4), dtype=np.uint8)
+        r = self._hd.check(self._hd._lib.dips_start_texture(self._hd.ptr, out.ctypes.data, out.nbytes))
+        return out if r == 1 else None
+
+    def close(self) -> None:
+        self._hd.close()
+
+
+def frame_callback(width: int, height: int, frame_data, compute: ComputeState) -> np.ndarray:
+    """dips/src/lib.rs:233-246 through the C ABI's dips_frame_callback."""
+    a = _as_u8(frame_data)
+    out = np.empty((height, width, 4), dtype=np.uint8)
+    compute._hd.check(compute._hd._lib.dips_frame_callback(
+        compute._hd.ptr, width, height, a.ctypes.data, a.nbytes, out.ctypes.data, out.nbytes))
+    compute._w, compute._h = width, height
+    return out
+
+
+def perform_dips_frames(properties: DiPsProperties, frames: Iterable, width: int, height: int,
+                        device: int = 0) -> Iterator[np.ndarray]:
+    """perform_dips (dips/src/lib.rs:252-257) minus the GStreamer decode
+    front-end (out of scope): runs the frame callback over an iterable of
+    RGBA8 frames and yields the callback's outputs in order."""
+    cs = ComputeState(properties.colorize_, properties.spatial_window_size_,
+                      properties.sensitivity_, properties.filter_type_,
+                      properties.chroma_filter_, device)
+    cb = properties.get_frame_callback() or frame_callback
+    for f in frames:
+        yield cb(width, height, f, cs)
+
+
+# ---------------------------------------------------------------------------
+# Batch difference series (north-star path)
+# ---------------------------------------------------------------------------
+
+@dataclass
+class Series:
+    """Per-frame difference series (see dips_series_entry in dips_hip.h)."""
+    sad: np.ndarray       # uint64 [N]
+    sj: np.ndarray        # uint64 [N]
+    count: np.ndarray     # uint64 [N]
+    si_fixed: np.ndarray  # uint64 [N]
+
+    @property
+    def si(self) -> np.ndarray:
+        return np.ldexp(self.si_fixed.astype(np.float64), -32)
+
+    @property
+    def sj_norm(self) -> np.ndarray:
+        return self.sj.astype(np.float64) / 510.0
+
+    def as_array(self) -> np.ndarray:
+        return np.stack([self.sad, self.sj, self.count, self.si_fixed], axis=1)
+
+    @classmethod
+    def from_array(cls, a: np.ndarray) -> "Series":
+        a = np.asarray(a, dtype=np.uint64).reshape(-1, 4)
+        return cls(a[:, 0].copy(), a[:, 1].copy(), a[:, 2].copy(), a[:, 3].copy())
+
+
+def _frame_geometry(frames, fmt: PixelFormat) -> Tuple[int, int, int]:
+    shape = tuple(frames.shape)
+    c = int(fmt)
+    if c == 1:
+        if len(shape) == 4 and shape[3] == 1:
+            shape = shape[:3]
+        if len(shape) != 3:
+            raise ValueError("gray8 frames must be [N, H, W]")
+        return shape[0], shape[1], shape[2]
+    if len(shape) != 4 or shape[3] != c:
+        raise ValueError(f"frames must be [N, H, W, {c}]")
+    return shape[0], shape[1], shape[2]
+
+
+class DiffSeriesOperator:
+    """The batch operator: per-frame difference series of a frame stack.
+
+    Inputs are numpy arrays (host; the call stages them through HBM) or
+    torch tensors on a HIP device (zero-copy, asynchronous on the tensor's
+    current stream)."""
+
+    def __init__(self, fmt: PixelFormat = PixelFormat.RGB8, mode: Mode = Mode.Overall,
+                 tau: float = 0.0, chroma_filter: ChromaFilter = ChromaFilter.None_,
+                 device: int = 0, time_kernel: bool = False, force_generic: bool = False):
+        flags = (_lib.FLAG_TIME_KERNEL if time_kernel else 0) | (_lib.FLAG_FORCE_GENERIC if force_generic else 0)
+        self.fmt = PixelFormat(fmt)
+        self.mode = Mode(mode)
+        self.tau = float(tau)
+        self._host = _Handle(_params(fmt=self.fmt, mode=self.mode, tau=tau,
+                                     chroma_filter=chroma_filter, flags=flags), device)
+        self._dev = _Handle(_params(fmt=self.fmt, mode=self.mode, tau=tau,
+                                    chroma_filter=chroma_filter,
+                                    flags=flags | _lib.FLAG_DEVICE_PTRS), device)
+
+    def close(self) -> None:
+        self._host.close()
+        self._dev.close()
+
+    # -- host arrays -------------------------------------------------------
+    def __call__(self, frames: np.ndarray, ref: Optional[np.ndarray] = None,
+                 want_map: bool = False) -> Tuple[Series, Optional[np.ndarray]]:
+        frames = _as_u8(frames)
+        n, h, w = _frame_geometry(frames, self.fmt)
+        out = np.zeros((n, 4), dtype=np.uint64)
+        dmap = np.empty_like(frames) if want_map else None
+        rp = None
+        if ref is not None:
+            ref = _as_u8(ref)
+            if ref.size != frames[0].size:
+                raise ValueError("ref must have the shape of one frame")
+            rp = ref.ctypes.data
+        self._host.check(self._host._lib.dips_diff_series(
+            self._host.ptr, w, h, frames.ctypes.data, n, rp, out.ctypes.data,
+            dmap.ctypes.data if dmap is not None else None))
+        return Series.from_array(out), dmap
+
+    def streamed(self, frames: np.ndarray, ref: Optional[np.ndarray] = None,
+                 chunk_frames: int = 0) -> Series:
+        """Pinned-staging + side-stream DMA feed (dips_diff_series_streamed)."""
+        frames = _as_u8(frames)
+        n, h, w = _frame_geometry(frames, self.fmt)
+        out = np.zeros((n, 4), dtype=np.uint64)
+        rp = None
+        if ref is not None:
+            ref = _as_u8(ref)
+            rp = ref.ctypes.data
+        self._host.check(self._host._lib.dips_diff_series_streamed(
+            self._host.ptr, w, h, frames.ctypes.data, n, rp, out.ctypes.data, int(chunk_frames)))
+        return Series.from_array(out)
+
+    # -- device tensors (torch, HIP) ----------------------------------------
+    def run_device(self, frames, series_out, ref=None, map_out=None, stream=None) -> None:
+        """Asynchronous: frames / ref / map_out uint8 device tensors,
+        series_out an int64 device tensor of shape [N, 4]."""
+        n, h, w = _frame_geometry(frames, self.fmt)
+        if tuple(series_out.shape) != (n, 4) or series_out.element_size() != 8:
+            raise ValueError("series_out must be an 8-byte tensor of shape [N, 4]")
+        for t in (frames, series_out, ref, map_out):
+            if t is not None and (not t.is_cuda or not t.is_contiguous()):
+                raise ValueError("device path needs contiguous HIP tensors")
+        lib = self._dev._lib
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device).cuda_stream
+        self._dev.check(lib.dips_set_stream(self._dev.ptr, ctypes.c_void_p(int(stream))))
+        self._dev.check(lib.dips_diff_series(
+            self._dev.ptr, w, h, frames.data_ptr(), n,
+            ref.data_ptr() if ref is not None else None, series_out.data_ptr(),
+            map_out.data_ptr() if map_out is not None else None))
+
+    def synth_device(self, dst, width: int, height: int, seed: int, t0: int, stream=None) -> None:
+        """Fill a uint8 device tensor [N, H, W(, C)] with synthetic frames t0..t0+N-1."""
+        n = dst.shape[0]
+        lib = self._dev._lib
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(dst.device).cuda_stream
+        self._dev.check(lib.dips_set_stream(self._dev.ptr, ctypes.c_void_p(int(stream))))
+        self._dev.check(lib.dips_synth_frames(self._dev.ptr, width, height, int(seed), int(t0), n,
+                                              dst.data_ptr()))
+
+    def kernel_time(self, reset: bool = False) -> Tuple[float, int]:
+        ms = ctypes.c_double()
+        cnt = ctypes.c_uint64()
+        self._dev.check(self._dev._lib.dips_kernel_time(self._dev.ptr, ctypes.byref(ms), ctypes.byref(cnt)))
+        out = (ms.value, cnt.value)
+        if reset:
+            self._dev.check(self._dev._lib.dips_kernel_time_reset(self._dev.ptr))
+        return out
+
+    def geometry(self, width: int, height: int, n_frames: int) -> Tuple[int, int, int]:
+        waves, tiles, pbytes = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._dev.check(self._dev._lib.dips_series_geometry(
+            self._dev.ptr, width, height, n_frames, ctypes.byref(waves), ctypes.byref(tiles),
+            ctypes.byref(pbytes)))
+        return waves.value, tiles.value, pbytes.value
+
+
+def diff_series(frames: np.ndarray, *, fmt: Optional[PixelFormat] = None, mode: Mode = Mode.Overall,
+                tau: float = 0.0, chroma_filter: ChromaFilter = ChromaFilter.None_,
+                ref: Optional[np.ndarray] = None, want_map: bool = False, device: int = 0,
+                force_generic: bool = False) -> Tuple[Series, Optional[np.ndarray]]:
+    """One-shot helper over DiffSeriesOperator for host arrays."""
+    if fmt is None:
+        fmt = PixelFormat.Gray8 if frames.ndim == 3 else PixelFormat(frames.shape[-1])
+    op = DiffSeriesOperator(fmt, mode, tau, chroma_filter, device, force_generic=force_generic)
+    try:
+        return op(frames, ref=ref, want_map=want_map)
+    finally:
+        op.close()
+
+
+def si_from_fixed(si_fixed) -> np.ndarray:
+    return np.ldexp(np.asarray(si_fixed, dtype=np.float64), -32)
+
+
+__all__ = [
+    "DiPsFilter", "ChromaFilter", "PixelFormat", "Mode", "DiPsProperties", "ComputeState",
+    "frame_callback", "perform_dips_frames", "Series", "DiffSeriesOperator", "diff_series",
+    "si_from_fixed", "VideoPathNotSpecifiedError", "FrameCallbackNotSpecifiedError", "DipsError",
+]

@@ -1,0 +1,144 @@
+// compat_kernels.hip -- the dips-compat ComputeState kernels on gfx950.
+//
+//   compat_precompute: pre_compute_main (pre_compute_shader.wgsl:92-132),
+//                      the start texture S = q(upper median of the four
+//                      spatially filtered first frames), run once.
+//   compat_main:       compute_main (dips_shader.wgsl:172-240) for one frame:
+//                      filter the newest ring slot (quantised on store, A4),
+//                      upper median of the four slots, diff against S,
+//                      filter / sensitivity / colour epilogue, RGBA8 out.
+//
+// Both run one thread per pixel on 16x16 workgroups.  For a spatial window
+// W > 1 the workgroup first stages the intensity of its (16 + 2h - 1)^2
+// neighbourhood in LDS (out-of-frame texels are 0.0, dips_shader.wgsl:135-136)
+// and each thread selects the window's order statistic from LDS.  The
+// reference filters the newest slot in place while neighbours read it (a
+// data race); here the filter reads a separate copy (`raw`).
+#include "dips_math.h"
+#include "dips_kernels.h"
+
+namespace dips {
+
+constexpr int kTile = 16;
+constexpr int kMaxHalo = 5;                       // window <= 11
+constexpr int kLds = kTile + 2 * kMaxHalo;        // 26
+
+__device__ __forceinline__ float texel_intensity(const uint8_t* img, uint64_t p, uint32_t chroma) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(img + 4 * p);
+    return intensity_rgb(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, chroma);
+}
+
+// Stage the intensity neighbourhood of this workgroup's tile.
+__device__ void stage_tile(float (*tile)[kLds], const uint8_t* img, uint32_t w, uint32_t h, int halo,
+                           uint32_t chroma) {
+    const int ox = (int)(blockIdx.x * kTile) - halo;
+    const int oy = (int)(blockIdx.y * kTile) - halo;
+    const int span = kTile + 2 * halo;
+    for (int idx = threadIdx.y * kTile + threadIdx.x; idx < span * span; idx += kTile * kTile) {
+        const int ty = idx / span, tx = idx - ty * span;
+        const int gx = ox + tx, gy = oy + ty;
+        float v = 0.0f;
+        if (gx >= 0 && gy >= 0 && gx < (int)w && gy < (int)h) v = texel_intensity(img, (uint64_t)gy * w + gx, chroma);
+        tile[ty][tx] = v;
+    }
+}
+
+// spatial_median_filter for W > 1 (dips_shader.wgsl:120-170): the sorted
+// 121-entry array holds the (2h)^2 window values and zeros elsewhere; the
+// bubble sort (j+1 clamped to 120 by naga's Restrict policy) sorts indices
+// 0..min(W^2,120); the result is element min(W^2/2 + 1, 120).  All values are
+// >= 0, so that element is 0 while it falls among the zeros, otherwise the
+// (k - zeros)-th smallest window value.
+__device__ float window_select(float (*tile)[kLds], int window) {
+    const int hw = window / 2;
+    const int side = 2 * hw;
+    const int n = side * side;
+    const int ws2 = window * window;
+    const int region = (ws2 < 120 ? ws2 : 120) + 1;
+    const int zeros = region - n;
+    int k = ws2 / 2 + 1;
+    if (k > 120) k = 120;
+    if (k < zeros) return 0.0f;
+    const int kk = k - zeros;
+    // tile[ty + j + hw][tx + i + hw] for i, j in [-hw, hw) -> rows/cols [ty, ty + side)
+    const int tx = threadIdx.x, ty = threadIdx.y;
+    for (int c = 0; c < n; ++c) {
+        const float vc = tile[ty + c / side][tx + c % side];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) {
+            const float vj = tile[ty + j / side][tx + j % side];
+            rank += (vj < vc || (vj == vc && j < c)) ? 1 : 0;
+        }
+        if (rank == kk) return vc;
+    }
+    return 0.0f;  // unreachable
+}
+
+__global__ __launch_bounds__(256) void compat_precompute_kernel(CompatArgs a) {
+    __shared__ float tile[kLds][kLds];
+    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
+    const uint32_t y = blockIdx.y * kTile + threadIdx.y;
+    const bool inside = x < a.width && y < a.height;
+    const uint64_t p = (uint64_t)y * a.width + x;
+    float m[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (a.window == 1) {
+            m[k] = inside ? texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
+        } else {
+            __syncthreads();
+            stage_tile(tile, a.slots[k], a.width, a.height, a.window / 2, a.chroma);
+            __syncthreads();
+            m[k] = inside ? window_select(tile, a.window) : 0.0f;
+        }
+        // get_intensity(vec4(f, f, f, 1)) = f (pre_compute_shader.wgsl:105-108)
+    }
+    if (!inside) return;
+    const uint32_t s = unorm_store(upper_median4(m[0], m[1], m[2], m[3]));
+    // start texture is gray RGBA8 (pre_compute_shader.wgsl:128-131)
+    *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(a.start) + 4 * p) = s | (s << 8) | (s << 16) | (255u << 24);
+}
+
+__global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
+    __shared__ float tile[kLds][kLds];
+    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
+    const uint32_t y = blockIdx.y * kTile + threadIdx.y;
+    const bool inside = x < a.width && y < a.height;
+    const uint64_t p = (uint64_t)y * a.width + x;
+    float fi;
+    if (a.window == 1) {
+        if (!inside) return;
+        fi = texel_intensity(a.raw, p, a.chroma);
+    } else {
+        stage_tile(tile, a.raw, a.width, a.height, a.window / 2, a.chroma);
+        __syncthreads();
+        if (!inside) return;
+        fi = window_select(tile, a.window);
+    }
+    // in-place store of the filtered newest slot, quantised (dips_shader.wgsl:187)
+    const uint32_t qi = unorm_store(fi);
+    *reinterpret_cast<uint32_t*>(a.slots[a.newest] + 4 * p) = qi | (qi << 8) | (qi << 16) | (255u << 24);
+    float m[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        // the newest slot re-reads its own quantised gray texel (:192)
+        m[i] = (uint32_t)i == a.newest ? intensity_rgb(qi, qi, qi, a.chroma) : texel_intensity(a.slots[i], p, a.chroma);
+    }
+    const float original = unorm_load(a.start[4 * p]);  // textureLoad(start_texture).r (:213)
+    const float diff = original - upper_median4(m[0], m[1], m[2], m[3]);
+    *reinterpret_cast<uint32_t*>(a.out + 4 * p) = visual_epilogue(diff, a.filter, a.sensitivity, a.colorize != 0u);
+}
+
+hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s) {
+    dim3 grid((a.width + kTile - 1) / kTile, (a.height + kTile - 1) / kTile);
+    hipLaunchKernelGGL(compat_precompute_kernel, grid, dim3(kTile, kTile), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s) {
+    dim3 grid((a.width + kTile - 1) / kTile, (a.height + kTile - 1) / kTile);
+    hipLaunchKernelGGL(compat_main_kernel, grid, dim3(kTile, kTile), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace dips

@@ -1,0 +1,664 @@
+// dips_abi.hip -- host side of the C ABI declared in include/dips_hip.h.
+//
+// The handle plays the role of the reference's ComputeState
+// (dips/src/gpu/mod.rs:39-56): it owns the HIP device binding, the stream,
+// the temporal ring of the dips-compat path and the workspace of the batch
+// series path.  No C++ exception leaves this file: every entry point returns
+// a dips_status (or the documented int) and records a message for
+// dips_last_error().
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/dips_hip.h"
+#include "dips_kernels.h"
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            p = nullptr;
+            cap = 0;
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct HostPinned {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) {
+            (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
+};
+
+std::mutex g_err_mu;
+std::string g_create_err;
+
+}  // namespace
+
+struct dips_handle {
+    dips_params p{};
+    int device = 0;
+    int cu_count = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    hipStream_t copy_stream = nullptr;
+    std::string err;
+
+    // batch series workspace
+    DevBuf partials, stage_frames, stage_ref, stage_series, stage_map;
+    std::map<const void*, int> occupancy;
+
+    // streamed feed
+    DevBuf ring[3];
+    DevBuf ring_ref;
+    HostPinned pinned[2];
+    hipEvent_t copy_done[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t kernel_done[3] = {nullptr, nullptr, nullptr};
+
+    // kernel timing
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    std::vector<hipEvent_t> ev_free;
+    double t_ms = 0.0;
+    uint64_t t_launches = 0;
+
+    // dips-compat ComputeState
+    uint32_t width = 0, height = 0;
+    int n_queued = 0;
+    bool main_init = false;
+    uint32_t ring_idx = 0;     // UCircularIndex (utils/indexing.rs:1-34)
+    uint32_t uniform_idx = 0;  // starting_index uniform (bind_groups.rs:317-321)
+    DevBuf slots[4], raw, start, out;
+    HostPinned io;
+};
+
+namespace {
+
+dips_status fail(dips_handle* h, dips_status st, const std::string& msg) {
+    if (h) h->err = msg;
+    return st;
+}
+
+dips_status hip_fail(dips_handle* h, hipError_t e, const char* what) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(e);
+    return fail(h, e == hipErrorOutOfMemory ? DIPS_ERR_NOMEM : DIPS_ERR_HIP, m);
+}
+
+#define DIPS_HIP(h, call)                                   \
+    do {                                                    \
+        hipError_t e_ = (call);                             \
+        if (e_ != hipSuccess) return hip_fail((h), e_, #call); \
+    } while (0)
+
+dips_status validate_params(const dips_params* p, std::string* why) {
+    if (p->spatial_window_size < 1 || p->spatial_window_size > 11) {
+        *why = "spatial_window_size must be in [1, 11] (dips_shader.wgsl:27 MAX_WIN_SIZE_SQUARE = 11*11)";
+        return DIPS_ERR_INVALID;
+    }
+    if (p->chroma_filter > 3u) {
+        *why = "chroma_filter must be 0..3 (dips/src/lib.rs:43-61)";
+        return DIPS_ERR_INVALID;
+    }
+    if (p->mode > 1u) {
+        *why = "mode must be DIPS_MODE_OVERALL or DIPS_MODE_PER_FRAME";
+        return DIPS_ERR_INVALID;
+    }
+    if (p->format != DIPS_FMT_GRAY8 && p->format != DIPS_FMT_RGB8 && p->format != DIPS_FMT_RGBA8) {
+        *why = "format must be DIPS_FMT_GRAY8, DIPS_FMT_RGB8 or DIPS_FMT_RGBA8";
+        return DIPS_ERR_INVALID;
+    }
+    if (!(p->tau >= 0.0f) || std::isinf(p->tau)) {
+        *why = "tau must be finite and >= 0";
+        return DIPS_ERR_INVALID;
+    }
+    if (!std::isfinite(p->sensitivity)) {
+        *why = "sensitivity must be finite";
+        return DIPS_ERR_INVALID;
+    }
+    return DIPS_OK;
+}
+
+hipEvent_t take_event(dips_handle* h) {
+    if (!h->ev_free.empty()) {
+        hipEvent_t e = h->ev_free.back();
+        h->ev_free.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int occupancy_blocks(dips_handle* h, const void* kernel) {
+    auto it = h->occupancy.find(kernel);
+    if (it != h->occupancy.end()) return it->second;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, 256, 0) != hipSuccess || nb < 1) nb = 1;
+    h->occupancy[kernel] = nb;
+    return nb;
+}
+
+struct FastGeom {
+    bool ok = false;
+    uint64_t n_tiles = 0, items = 0, n_waves = 0, blocks = 0;
+};
+
+FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, int C, bool pf,
+                       bool map) {
+    FastGeom g;
+    const uint64_t npx = (uint64_t)width * height;
+    const uint64_t fb = npx * (uint64_t)C;
+    const int ppv = dips::pixels_per_vec(C);
+    if (npx % (uint64_t)ppv != 0 || fb >= (1ull << 31) || n_frames == 0) return g;
+    const uint64_t U = (uint64_t)dips::fast_unroll(C);
+    const uint64_t nvec = npx / (uint64_t)ppv;
+    g.n_tiles = (nvec + 64 * U - 1) / (64 * U);
+    g.items = g.n_tiles * n_frames;
+    const void* k = dips::series_fast_kernel_ptr(C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map);
+    if (!k) return g;
+    const uint64_t resident = (uint64_t)occupancy_blocks(h, k) * (uint64_t)h->cu_count * 4u;
+    g.n_waves = g.items < resident ? g.items : resident;
+    g.blocks = (g.n_waves + 3) / 4;
+    g.ok = g.n_tiles < (1ull << 32) && g.blocks < (1ull << 31);
+    return g;
+}
+
+// Run the series on device pointers, asynchronously on `s`.
+dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
+                              uint32_t n_frames, const uint8_t* ref0, dips_series_entry* series, uint8_t* map,
+                              hipStream_t s) {
+    const int C = (int)h->p.format;
+    const bool pf = h->p.mode == DIPS_MODE_PER_FRAME;
+    const uint64_t npx = (uint64_t)width * height;
+    const uint64_t fb = npx * (uint64_t)C;
+    DIPS_HIP(h, hipMemsetAsync(series, 0, sizeof(dips_series_entry) * (size_t)n_frames, s));
+
+    auto aligned4 = [](const void* q) { return ((uintptr_t)q & 3u) == 0; };
+    FastGeom g;
+    if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC) && aligned4(frames) && aligned4(ref0) && (!map || aligned4(map)))
+        g = fast_geometry(h, width, height, n_frames, C, pf, map != nullptr);
+
+    const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
+        DIPS_HIP(h, hipEventRecord(e0, s));
+    }
+    if (g.ok) {
+        DIPS_HIP(h, h->partials.ensure((size_t)g.items * 16u));
+        dips::SeriesArgs a{};
+        a.frames = frames;
+        a.ref0 = ref0;
+        a.dmap = map;
+        a.partials = h->partials.as<uint64_t>();
+        a.items = g.items;
+        a.frame_bytes = (uint32_t)fb;
+        a.n_frames = n_frames;
+        a.n_tiles = (uint32_t)g.n_tiles;
+        a.n_waves = (uint32_t)g.n_waves;
+        a.thr = C == 1 ? h->p.tau : 2.0f * h->p.tau;
+        DIPS_HIP(h, dips::launch_series_fast(a, C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map != nullptr,
+                                             (uint32_t)g.blocks, s));
+    } else {
+        const uint64_t bpf = (npx + 255u) / 256u;
+        if (bpf * (uint64_t)n_frames >= (1ull << 31))
+            return fail(h, DIPS_ERR_INVALID, "frame batch too large for the generic kernel; split the batch");
+        dips::GenericArgs a{};
+        a.frames = frames;
+        a.ref0 = ref0;
+        a.dmap = map;
+        a.series = series;
+        a.frame_bytes = fb;
+        a.n_px = npx;
+        a.n_frames = n_frames;
+        a.blocks_per_frame = (uint32_t)bpf;
+        a.mode = h->p.mode;
+        a.chroma = C == 1 ? 0u : h->p.chroma_filter;
+        a.tau = h->p.tau;
+        DIPS_HIP(h, dips::launch_series_generic(a, C, s));
+    }
+    if (timing) {
+        DIPS_HIP(h, hipEventRecord(e1, s));
+        h->ev_pending.emplace_back(e0, e1);
+    }
+    if (g.ok) DIPS_HIP(h, dips::launch_series_reduce(h->partials.as<uint64_t>(), n_frames, (uint32_t)g.n_tiles, series, s));
+    return DIPS_OK;
+}
+
+dips_status bind(dips_handle* h) {
+    if (!h) return DIPS_ERR_INVALID;
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
+    return DIPS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dips_abi_version(void) { return DIPS_ABI_VERSION; }
+
+dips_status dips_params_default(dips_params* p) {
+    if (!p) return DIPS_ERR_INVALID;
+    std::memset(p, 0, sizeof(*p));
+    p->colorize = 0;
+    p->spatial_window_size = 1;
+    p->sensitivity = 5.0f;
+    p->filter_type = DIPS_FILTER_UNFILTERED;
+    p->chroma_filter = DIPS_CHROMA_NONE;
+    p->mode = DIPS_MODE_OVERALL;
+    p->format = DIPS_FMT_RGB8;
+    p->tau = 0.0f;
+    p->flags = 0;
+    return DIPS_OK;
+}
+
+dips_status dips_create(const dips_params* params, int device, dips_handle** out) {
+    if (!out) return DIPS_ERR_INVALID;
+    *out = nullptr;
+    dips_params p;
+    if (params) p = *params;
+    else dips_params_default(&p);
+    std::string why;
+    if (validate_params(&p, &why) != DIPS_OK) {
+        std::lock_guard<std::mutex> lk(g_err_mu);
+        g_create_err = why;
+        return DIPS_ERR_INVALID;
+    }
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0 || device < 0 || device >= count) {
+        std::lock_guard<std::mutex> lk(g_err_mu);
+        g_create_err = std::string("no HIP device ") + std::to_string(device) + " (" +
+                       (e == hipSuccess ? std::to_string(count) + " visible" : hipGetErrorString(e)) + ")";
+        return DIPS_ERR_NODEVICE;
+    }
+    dips_handle* h = new (std::nothrow) dips_handle();
+    if (!h) return DIPS_ERR_NOMEM;
+    h->p = p;
+    h->device = device;
+    e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&h->cu_count, hipDeviceAttributeMultiprocessorCount, device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking);
+    for (int i = 0; i < 3 && e == hipSuccess; ++i) {
+        e = hipEventCreateWithFlags(&h->copy_done[i], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->kernel_done[i], hipEventDisableTiming);
+    }
+    if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_err_mu);
+        g_create_err = std::string("HIP initialisation failed: ") + hipGetErrorString(e);
+        dips_destroy(h);
+        return DIPS_ERR_HIP;
+    }
+    h->stream = h->own_stream;
+    *out = h;
+    return DIPS_OK;
+}
+
+void dips_destroy(dips_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
+    for (auto& pr : h->ev_pending) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    for (auto e : h->ev_free) (void)hipEventDestroy(e);
+    for (int i = 0; i < 3; ++i) {
+        if (h->copy_done[i]) (void)hipEventDestroy(h->copy_done[i]);
+        if (h->kernel_done[i]) (void)hipEventDestroy(h->kernel_done[i]);
+        h->ring[i].release();
+    }
+    h->ring_ref.release();
+    h->pinned[0].release();
+    h->pinned[1].release();
+    h->partials.release();
+    h->stage_frames.release();
+    h->stage_ref.release();
+    h->stage_series.release();
+    h->stage_map.release();
+    for (auto& s : h->slots) s.release();
+    h->raw.release();
+    h->start.release();
+    h->out.release();
+    h->io.release();
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
+    delete h;
+}
+
+const char* dips_last_error(const dips_handle* h) {
+    if (h) return h->err.c_str();
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    return g_create_err.c_str();
+}
+
+dips_status dips_set_stream(dips_handle* h, void* stream) {
+    if (!h) return DIPS_ERR_INVALID;
+    h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+    return DIPS_OK;
+}
+
+dips_status dips_synchronize(dips_handle* h) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    return DIPS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// dips-compat ComputeState
+// ---------------------------------------------------------------------------
+
+dips_status dips_add_texture(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frame, size_t len) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!frame || width == 0 || height == 0) return fail(h, DIPS_ERR_INVALID, "add_texture: empty frame");
+    const size_t fb = (size_t)width * height * 4u;
+    if (len != fb) return fail(h, DIPS_ERR_INVALID, "add_texture: len != width*height*4 (RGBA8, stride width*4)");
+    if (h->n_queued > 0 && (width != h->width || height != h->height))
+        return fail(h, DIPS_ERR_INVALID, "add_texture: frame size changed after the first frame");
+    if (h->n_queued == 0) {
+        for (auto& s : h->slots) DIPS_HIP(h, s.ensure(fb));
+        DIPS_HIP(h, h->raw.ensure(fb));
+        DIPS_HIP(h, h->start.ensure(fb));
+        DIPS_HIP(h, h->out.ensure(fb));
+        DIPS_HIP(h, h->io.ensure(fb));
+        h->width = width;
+        h->height = height;
+    }
+    // upload through the pinned staging buffer (one PCIe transfer)
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    std::memcpy(h->io.p, frame, fb);
+    if (!h->main_init) {
+        // VecDeque phase (dips/src/gpu/mod.rs:171-177): frames 0..3 fill slots 0..3
+        DIPS_HIP(h, hipMemcpyAsync(h->slots[h->n_queued].p, h->io.p, fb, hipMemcpyHostToDevice, h->stream));
+        h->n_queued += 1;
+        if (h->n_queued == 4) {
+            // PreComputeBindGroups::initialize + run_precompute_pipeline (:178-188)
+            dips::CompatArgs a{};
+            for (int k = 0; k < 4; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
+            a.start = h->start.as<uint8_t>();
+            a.width = width;
+            a.height = height;
+            a.window = h->p.spatial_window_size;
+            a.chroma = h->p.chroma_filter;
+            DIPS_HIP(h, dips::launch_compat_precompute(a, h->stream));
+            // MainComputeBindGroups::initialize with starting index 0 (bind_groups.rs:73)
+            h->main_init = true;
+            h->ring_idx = 0;
+            h->uniform_idx = 0;
+        }
+    } else {
+        // update_temporal_texture (bind_groups.rs:407-427)
+        DIPS_HIP(h, hipMemcpyAsync(h->slots[h->ring_idx].p, h->io.p, fb, hipMemcpyHostToDevice, h->stream));
+        h->uniform_idx = h->ring_idx;
+        h->ring_idx = (h->ring_idx + 1u) % 4u;
+    }
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    return DIPS_OK;
+}
+
+int dips_dispatch(dips_handle* h, uint8_t* out, size_t cap) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!h->main_init) return 0;  // None (dips/src/gpu/mod.rs:394-396)
+    const size_t fb = (size_t)h->width * h->height * 4u;
+    if (!out) return fail(h, DIPS_ERR_INVALID, "dispatch: null output");
+    if (cap < fb) return fail(h, DIPS_ERR_CAPACITY, "dispatch: output buffer smaller than width*height*4");
+    dips::CompatArgs a{};
+    for (int k = 0; k < 4; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
+    a.start = h->start.as<uint8_t>();
+    a.out = h->out.as<uint8_t>();
+    a.width = h->width;
+    a.height = h->height;
+    a.newest = h->uniform_idx;
+    a.window = h->p.spatial_window_size;
+    a.chroma = h->p.chroma_filter;
+    a.filter = h->p.filter_type;
+    a.sensitivity = h->p.sensitivity;
+    a.colorize = h->p.colorize ? 1u : 0u;
+    if (a.window == 1) {
+        a.raw = a.slots[a.newest];  // per-pixel in-place filter is race free
+    } else {
+        DIPS_HIP(h, hipMemcpyAsync(h->raw.p, a.slots[a.newest], fb, hipMemcpyDeviceToDevice, h->stream));
+        a.raw = h->raw.as<uint8_t>();
+    }
+    DIPS_HIP(h, dips::launch_compat_main(a, h->stream));
+    DIPS_HIP(h, hipMemcpyAsync(h->io.p, h->out.p, fb, hipMemcpyDeviceToHost, h->stream));
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    std::memcpy(out, h->io.p, fb);
+    return 1;
+}
+
+int dips_frame_callback(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frame, size_t len,
+                        uint8_t* out, size_t cap) {
+    if (!h) return DIPS_ERR_INVALID;
+    if (!out || cap < len) return fail(h, DIPS_ERR_CAPACITY, "frame_callback: output buffer too small");
+    dips_status st = dips_add_texture(h, width, height, frame, len);
+    if (st != DIPS_OK) return st;
+    const int r = dips_dispatch(h, out, cap);
+    if (r == 0) std::memcpy(out, frame, len);  // frame_data.to_vec() (dips/src/lib.rs:244)
+    return r;
+}
+
+int dips_start_texture(dips_handle* h, uint8_t* out, size_t cap) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!h->main_init) return 0;
+    const size_t fb = (size_t)h->width * h->height * 4u;
+    if (!out || cap < fb) return fail(h, DIPS_ERR_CAPACITY, "start_texture: output buffer too small");
+    DIPS_HIP(h, hipMemcpyAsync(h->io.p, h->start.p, fb, hipMemcpyDeviceToHost, h->stream));
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    std::memcpy(out, h->io.p, fb);
+    return 1;
+}
+
+// ---------------------------------------------------------------------------
+// Batch series
+// ---------------------------------------------------------------------------
+
+double dips_series_si(const dips_series_entry* e) { return e ? std::ldexp((double)e->si_fixed, -32) : 0.0; }
+
+dips_status dips_diff_series(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
+                             uint32_t n_frames, const uint8_t* ref, dips_series_entry* series, uint8_t* map) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (n_frames == 0) return DIPS_OK;
+    if (!frames || !series || width == 0 || height == 0) return fail(h, DIPS_ERR_INVALID, "diff_series: null or empty argument");
+    const int C = (int)h->p.format;
+    const uint64_t fb = (uint64_t)width * height * (uint64_t)C;
+    if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) {
+        return run_series_device(h, width, height, frames, n_frames, ref ? ref : frames, series, map, h->stream);
+    }
+    // host pointers: stage through HBM (synchronous call)
+    const size_t total = (size_t)fb * n_frames;
+    DIPS_HIP(h, h->stage_frames.ensure(total));
+    DIPS_HIP(h, h->stage_series.ensure(sizeof(dips_series_entry) * (size_t)n_frames));
+    DIPS_HIP(h, hipMemcpyAsync(h->stage_frames.p, frames, total, hipMemcpyHostToDevice, h->stream));
+    const uint8_t* ref_dev = h->stage_frames.as<uint8_t>();
+    if (ref) {
+        DIPS_HIP(h, h->stage_ref.ensure(fb));
+        DIPS_HIP(h, hipMemcpyAsync(h->stage_ref.p, ref, fb, hipMemcpyHostToDevice, h->stream));
+        ref_dev = h->stage_ref.as<uint8_t>();
+    }
+    uint8_t* map_dev = nullptr;
+    if (map) {
+        DIPS_HIP(h, h->stage_map.ensure(total));
+        map_dev = h->stage_map.as<uint8_t>();
+    }
+    st = run_series_device(h, width, height, h->stage_frames.as<uint8_t>(), n_frames, ref_dev,
+                           h->stage_series.as<dips_series_entry>(), map_dev, h->stream);
+    if (st != DIPS_OK) return st;
+    DIPS_HIP(h, hipMemcpyAsync(series, h->stage_series.p, sizeof(dips_series_entry) * (size_t)n_frames,
+                               hipMemcpyDeviceToHost, h->stream));
+    if (map) DIPS_HIP(h, hipMemcpyAsync(map, map_dev, total, hipMemcpyDeviceToHost, h->stream));
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    return DIPS_OK;
+}
+
+dips_status dips_diff_series_streamed(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* host_frames,
+                                      uint32_t n_frames, const uint8_t* host_ref, dips_series_entry* series,
+                                      uint32_t chunk_frames) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (n_frames == 0) return DIPS_OK;
+    if (!host_frames || !series || width == 0 || height == 0)
+        return fail(h, DIPS_ERR_INVALID, "diff_series_streamed: null or empty argument");
+    const int C = (int)h->p.format;
+    const bool pf = h->p.mode == DIPS_MODE_PER_FRAME;
+    const size_t fb = (size_t)width * height * (size_t)C;
+    uint32_t chunk = chunk_frames;
+    if (chunk == 0) {
+        const size_t target = 256u << 20;  // ~256 MiB per DMA chunk
+        chunk = (uint32_t)(target / fb);
+        if (chunk < 1) chunk = 1;
+    }
+    if (chunk > n_frames) chunk = n_frames;
+    const size_t cbytes = fb * chunk;
+    for (auto& r : h->ring) DIPS_HIP(h, r.ensure(cbytes));
+    DIPS_HIP(h, h->ring_ref.ensure(fb));
+    for (auto& pn : h->pinned) DIPS_HIP(h, pn.ensure(cbytes));
+    DIPS_HIP(h, h->stage_series.ensure(sizeof(dips_series_entry) * (size_t)n_frames));
+    dips_series_entry* series_dev = h->stage_series.as<dips_series_entry>();
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
+    if (host_ref) {
+        std::memcpy(h->pinned[1].p, host_ref, fb);
+        DIPS_HIP(h, hipMemcpyAsync(h->ring_ref.p, h->pinned[1].p, fb, hipMemcpyHostToDevice, h->copy_stream));
+        DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
+    }
+    const uint32_t n_chunks = (n_frames + chunk - 1) / chunk;
+    for (uint32_t k = 0; k < n_chunks; ++k) {
+        const uint32_t b = k % 3u, hb = k % 2u;
+        const uint32_t f0 = k * chunk;
+        const uint32_t nk = (f0 + chunk <= n_frames) ? chunk : n_frames - f0;
+        // pinned[hb] was last read by the DMA of chunk k-2
+        if (k >= 2) DIPS_HIP(h, hipEventSynchronize(h->copy_done[(k - 2) % 3u]));
+        std::memcpy(h->pinned[hb].p, host_frames + (size_t)f0 * fb, (size_t)nk * fb);
+        // ring[b] was read by kernel k-3 (frames) and kernel k-2 (per-frame ref)
+        if (k >= 2) DIPS_HIP(h, hipStreamWaitEvent(h->copy_stream, h->kernel_done[(k - 2) % 3u], 0));
+        DIPS_HIP(h, hipMemcpyAsync(h->ring[b].p, h->pinned[hb].p, (size_t)nk * fb, hipMemcpyHostToDevice, h->copy_stream));
+        DIPS_HIP(h, hipEventRecord(h->copy_done[b], h->copy_stream));
+        DIPS_HIP(h, hipStreamWaitEvent(h->stream, h->copy_done[b], 0));
+        const uint8_t* frames_dev = h->ring[b].as<uint8_t>();
+        const uint8_t* ref_dev;
+        if (pf) {
+            if (k == 0) ref_dev = host_ref ? h->ring_ref.as<uint8_t>() : frames_dev;
+            else ref_dev = h->ring[(k - 1) % 3u].as<uint8_t>() + (size_t)(chunk - 1) * fb;
+        } else {
+            if (k == 0 && !host_ref) {
+                DIPS_HIP(h, hipMemcpyAsync(h->ring_ref.p, frames_dev, fb, hipMemcpyDeviceToDevice, h->stream));
+            }
+            ref_dev = h->ring_ref.as<uint8_t>();
+        }
+        st = run_series_device(h, width, height, frames_dev, nk, ref_dev, series_dev + f0, nullptr, h->stream);
+        if (st != DIPS_OK) return st;
+        DIPS_HIP(h, hipEventRecord(h->kernel_done[b], h->stream));
+    }
+    DIPS_HIP(h, hipMemcpyAsync(series, series_dev, sizeof(dips_series_entry) * (size_t)n_frames,
+                               hipMemcpyDeviceToHost, h->stream));
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    return DIPS_OK;
+}
+
+dips_status dips_synth_frames(dips_handle* h, uint32_t width, uint32_t height, uint64_t seed, uint64_t t0,
+                              uint32_t n_frames, uint8_t* dst) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (n_frames == 0) return DIPS_OK;
+    if (!dst || width == 0 || height == 0) return fail(h, DIPS_ERR_INVALID, "synth_frames: null or empty argument");
+    dips::SynthArgs a{};
+    a.dst = dst;
+    a.channels = h->p.format;
+    a.width = width;
+    a.height = height;
+    a.frame_bytes = (uint64_t)width * height * a.channels;
+    a.total_bytes = a.frame_bytes * n_frames;
+    a.seed = seed;
+    a.t0 = t0;
+    a.radius = height / 8u > 0 ? height / 8u : 1u;
+    DIPS_HIP(h, dips::launch_synth(a, h->stream));
+    return DIPS_OK;
+}
+
+dips_status dips_kernel_time(dips_handle* h, double* total_ms, uint64_t* launches) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    for (auto& pr : h->ev_pending) {
+        DIPS_HIP(h, hipEventSynchronize(pr.second));
+        float ms = 0.0f;
+        DIPS_HIP(h, hipEventElapsedTime(&ms, pr.first, pr.second));
+        h->t_ms += ms;
+        h->t_launches += 1;
+        h->ev_free.push_back(pr.first);
+        h->ev_free.push_back(pr.second);
+    }
+    h->ev_pending.clear();
+    if (total_ms) *total_ms = h->t_ms;
+    if (launches) *launches = h->t_launches;
+    return DIPS_OK;
+}
+
+dips_status dips_kernel_time_reset(dips_handle* h) {
+    dips_status st = dips_kernel_time(h, nullptr, nullptr);
+    if (st != DIPS_OK) return st;
+    h->t_ms = 0.0;
+    h->t_launches = 0;
+    return DIPS_OK;
+}
+
+dips_status dips_series_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames,
+                                 uint64_t* waves, uint64_t* tiles, uint64_t* partial_bytes) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    const int C = (int)h->p.format;
+    FastGeom g = fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false);
+    if (waves) *waves = g.ok ? g.n_waves : 0;
+    if (tiles) *tiles = g.ok ? g.n_tiles : 0;
+    if (partial_bytes) *partial_bytes = g.ok ? g.n_tiles * 16u : 0;
+    return g.ok ? DIPS_OK : fail(h, DIPS_ERR_INVALID, "shape not eligible for the fast kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+// dips_kernels.h -- kernel argument blocks and host launchers (internal).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dips_hip.h"
+
+namespace dips {
+
+// Unroll (vecs per lane) of the fast series kernel; a tile = 64 * U vecs.
+constexpr int kUnrollRGB = 4;   // 1024 px / wave / frame for RGB8 and RGBA8
+constexpr int kUnrollGray = 2;  // 2048 px / wave / frame for GRAY8
+
+struct SeriesArgs {
+    const uint8_t* frames;   // n_frames * frame_bytes, contiguous
+    const uint8_t* ref0;     // overall: reference; per-frame: predecessor of frame 0
+    uint8_t* dmap;           // optional |F - R| map (same layout as frames)
+    uint64_t* partials;      // [n_tiles][n_frames] x 16-byte records
+    uint64_t items;          // n_tiles * n_frames
+    uint32_t frame_bytes;
+    uint32_t n_frames;
+    uint32_t n_tiles;
+    uint32_t n_waves;
+    float thr;               // threshold in kernel units (2*tau for RGB(A), tau for gray)
+};
+
+struct GenericArgs {
+    const uint8_t* frames;
+    const uint8_t* ref0;
+    uint8_t* dmap;
+    dips_series_entry* series;
+    uint64_t frame_bytes;
+    uint64_t n_px;
+    uint32_t n_frames;
+    uint32_t blocks_per_frame;
+    uint32_t mode;
+    uint32_t chroma;
+    float tau;
+};
+
+struct SynthArgs {
+    uint8_t* dst;
+    uint64_t total_bytes;
+    uint64_t frame_bytes;
+    uint64_t seed;
+    uint64_t t0;
+    uint32_t channels;
+    uint32_t width;
+    uint32_t height;
+    uint32_t radius;
+};
+
+struct CompatArgs {
+    const uint8_t* raw;      // filter source (RGBA8) for the newest slot
+    uint8_t* slots[4];       // temporal ring (RGBA8)
+    const uint8_t* start;    // start texture (RGBA8 gray)
+    uint8_t* out;            // visualisation (RGBA8)
+    uint32_t width, height;
+    uint32_t newest;         // starting_index uniform
+    int32_t window;
+    uint32_t chroma;
+    uint32_t filter;
+    float sensitivity;
+    uint32_t colorize;
+};
+
+int pixels_per_vec(int channels);
+int fast_unroll(int channels);
+const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map);
+hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, bool per_frame, bool map,
+                              uint32_t blocks, hipStream_t s);
+hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles,
+                                dips_series_entry* series, hipStream_t s);
+hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);
+hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
+hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s);
+hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s);
+
+}  // namespace dips

@@ -1,0 +1,112 @@
+"""Frame-range sharding of the difference series over one process per GPU.
+
+The series path partitions by frames: once the reference is known, frames
+are independent.  Rank k owns the contiguous global frames
+[k*N/G, (k+1)*N/G).  The only exchanges are
+  * 'overall': the reference frame, broadcast once from rank 0;
+  * 'per-frame': the halo frame (global index start-1), sent by rank k-1 to
+    rank k (one point-to-point transfer per batch);
+  * the per-frame series (32 B per frame), reassembled on rank 0 by ONE
+    gather (RCCL over xGMI with the "nccl" backend; gloo in the CPU tests).
+No collective touches the frame data itself.
+
+The per-rank compute is a callable so that the CPU tests can drive the same
+protocol with the oracle over gloo; the product passes the HIP operator
+(DiffSeriesOperator.run_device) and never a CPU function.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+SERIES_COLS = 4  # sad, sj, count, si_fixed
+
+
+def frame_range(n_total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous frame range of `rank` (balanced to within one frame)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad world/rank")
+    return (n_total * rank) // world, (n_total * (rank + 1)) // world
+
+
+def frame_ranges(n_total: int, world: int) -> List[Tuple[int, int]]:
+    return [frame_range(n_total, world, r) for r in range(world)]
+
+
+def broadcast_reference(ref: torch.Tensor, src: int = 0, group=None) -> torch.Tensor:
+    """'overall' mode: the reference frame from rank `src` to every rank."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.broadcast(ref, src=src, group=group)
+    return ref
+
+
+def exchange_halo(local_frames: torch.Tensor, halo: torch.Tensor, group=None) -> Optional[torch.Tensor]:
+    """'per-frame' mode: send this rank's last frame to rank+1 and receive
+    rank-1's last frame into `halo`.  Returns the halo (None on rank 0)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return None
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    ops = []
+    if rank + 1 < world and local_frames.shape[0] > 0:
+        ops.append(dist.P2POp(dist.isend, local_frames[-1].contiguous(), rank + 1, group))
+    if rank > 0:
+        ops.append(dist.P2POp(dist.irecv, halo, rank - 1, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return halo if rank > 0 else None
+
+
+class SeriesGather:
+    """Reassemble the per-rank series on rank 0 with one gather.
+
+    Shards may differ by one frame; every rank pads to the largest shard so
+    the gather moves equal-size buffers, and rank 0 trims the padding."""
+
+    def __init__(self, n_total: int, device: torch.device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.ranges = frame_ranges(n_total, self.world)
+        self.max_n = max(e - s for s, e in self.ranges)
+        self.n_total = n_total
+        self.send = torch.zeros((self.max_n, SERIES_COLS), dtype=torch.int64, device=device)
+        self.recv = ([torch.zeros_like(self.send) for _ in range(self.world)]
+                     if self.rank == 0 else None)
+
+    def __call__(self, local_series: torch.Tensor) -> Optional[torch.Tensor]:
+        n = local_series.shape[0]
+        if self.world == 1:
+            return local_series
+        if n == self.max_n:
+            send = local_series
+        else:
+            self.send[:n].copy_(local_series)
+            send = self.send
+        dist.gather(send, self.recv, dst=0, group=self.group)
+        if self.rank != 0:
+            return None
+        return torch.cat([buf[: e - s] for buf, (s, e) in zip(self.recv, self.ranges)], dim=0)
+
+
+def sharded_series(local_frames: torch.Tensor, *, per_frame: bool, n_total: int,
+                   compute: Callable[[torch.Tensor, Optional[torch.Tensor], torch.Tensor], None],
+                   reference: Optional[torch.Tensor] = None, group=None,
+                   gather: Optional[SeriesGather] = None) -> Optional[torch.Tensor]:
+    """One batch of the sharded path.
+
+    local_frames: this rank's frames [n_k, ...]; reference: 'overall' mode's
+    reference (already broadcast); compute(frames, ref, series_out) fills
+    series_out [n_k, 4] (int64).  Returns the full series on rank 0."""
+    device = local_frames.device
+    series = torch.zeros((local_frames.shape[0], SERIES_COLS), dtype=torch.int64, device=device)
+    if per_frame:
+        halo = torch.empty_like(local_frames[0])
+        ref = exchange_halo(local_frames, halo, group)
+    else:
+        ref = reference
+    compute(local_frames, ref, series)
+    gather = gather or SeriesGather(n_total, device, group)
+    return gather(series)

@@ -1,0 +1,187 @@
+/*
+ * dips_hip.h -- C ABI of the MI355X-native DiPs frame-difference path.
+ *
+ * This is the drop-in boundary.  The reference crate (RubenMovsesyan/DiPs,
+ * Rust) reaches its GPU operator only through
+ *     type CallbackFunction = fn(u32, u32, &[u8], &mut ComputeState) -> Vec<u8>
+ * (dips/src/lib.rs:23) and the three ComputeState methods new / add_texture /
+ * dispatch (dips/src/gpu/mod.rs:59, :170, :306; identical copies in
+ * dips_opencv/src/gpu/mod.rs:59, :172, :308).  Each entry point below names
+ * the reference item it replaces.  Everything is plain C: pointers, sizes,
+ * status codes.  No exception or panic crosses this boundary.
+ *
+ * Threading: a handle is not internally synchronised (the reference uses
+ * ComputeState under an RwLock write guard, dips/src/frame_extractor.rs:232);
+ * a handle may move between threads.  The caller owns every buffer.
+ */
+#ifndef DIPS_HIP_H
+#define DIPS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DIPS_ABI_VERSION 1
+
+typedef enum dips_status {
+    DIPS_OK = 0,
+    DIPS_ERR_INVALID = -1,  /* bad argument / shape / parameter */
+    DIPS_ERR_HIP = -2,      /* HIP runtime error (see dips_last_error) */
+    DIPS_ERR_STATE = -3,    /* call not valid in the handle's state */
+    DIPS_ERR_NOMEM = -4,    /* device or host allocation failed */
+    DIPS_ERR_CAPACITY = -5, /* caller's output buffer too small */
+    DIPS_ERR_NODEVICE = -6  /* no HIP device / device index out of range */
+} dips_status;
+
+/* DiPsFilter -> override id 3 (dips/src/lib.rs:25-41, dips_shader.wgsl:20). */
+#define DIPS_FILTER_SIGMOID 0u
+#define DIPS_FILTER_INVERSE_SIGMOID 1u
+#define DIPS_FILTER_UNFILTERED 255u
+/* ChromaFilter -> override id 4 (dips/src/lib.rs:43-61, dips_shader.wgsl:21). */
+#define DIPS_CHROMA_NONE 0u
+#define DIPS_CHROMA_RED 1u
+#define DIPS_CHROMA_GREEN 2u
+#define DIPS_CHROMA_BLUE 3u
+
+/* Pixel formats of the series path (the compat path is RGBA8 only, like the
+ * reference's appsink caps, dips/src/frame_extractor.rs:141-148). */
+#define DIPS_FMT_GRAY8 1u
+#define DIPS_FMT_RGB8 3u
+#define DIPS_FMT_RGBA8 4u
+
+/* Reference choice of the series path (README.md:7-11). */
+#define DIPS_MODE_OVERALL 0u   /* against frame 0 (or the given reference) */
+#define DIPS_MODE_PER_FRAME 1u /* against the previous frame */
+
+/* dips_params.flags */
+#define DIPS_FLAG_DEVICE_PTRS 0x1u /* series pointers are device (HBM) pointers */
+#define DIPS_FLAG_TIME_KERNEL 0x2u /* record hipEvents around the series kernel */
+#define DIPS_FLAG_FORCE_GENERIC 0x4u /* use the generic (any-shape) series kernel */
+
+/* Operator parameters.  The first five mirror ComputeState::new's arguments
+ * (dips/src/gpu/mod.rs:59-65) and DiPsProperties (dips/src/lib.rs:63-86);
+ * the rest configure the batch series path. */
+typedef struct dips_params {
+    uint8_t colorize;            /* override id 0; default 0 (lib.rs:80) */
+    int32_t spatial_window_size; /* override id 1; 1..11; default 1 (lib.rs:81) */
+    float sensitivity;           /* override id 2; default 5.0 (lib.rs:82) */
+    uint32_t filter_type;        /* DIPS_FILTER_*; default UNFILTERED (lib.rs:83) */
+    uint32_t chroma_filter;      /* DIPS_CHROMA_*; default NONE (lib.rs:84) */
+    uint32_t mode;               /* DIPS_MODE_*; default OVERALL */
+    uint32_t format;             /* DIPS_FMT_*; default RGB8 */
+    float tau;                   /* intensity threshold, >= 0; default 0 */
+    uint32_t flags;              /* DIPS_FLAG_* */
+} dips_params;
+
+/* One entry of the per-frame difference series.
+ *   sad      = sum over pixels and channels of |F_t - R|          (exact)
+ *   sj       = sum over pixels of |J_t - J_R|, J = max+min bytes   (exact)
+ *   count    = number of pixels with dI > tau
+ *   si_fixed = sum of dI over those pixels, scaled by 2^32         (exact)
+ * dI = |I_t - I_R| in f32 with I = get_intensity (dips_shader.wgsl:64-82).
+ * The f64 intensity sum is si_fixed * 2^-32 (dips_series_si). */
+typedef struct dips_series_entry {
+    uint64_t sad;
+    uint64_t sj;
+    uint64_t count;
+    uint64_t si_fixed;
+} dips_series_entry;
+
+typedef struct dips_handle dips_handle;
+
+/* Fill `p` with DiPsProperties::new() defaults (dips/src/lib.rs:74-86). */
+dips_status dips_params_default(dips_params *p);
+
+/* Replaces ComputeState::new (dips/src/gpu/mod.rs:59-165): binds HIP device
+ * `device`, validates the parameters, creates the stream and tables. */
+dips_status dips_create(const dips_params *params, int device, dips_handle **out);
+
+/* Replaces Drop of ComputeState. */
+void dips_destroy(dips_handle *h);
+
+/* Last error message for `h` (or the last creation failure if h == NULL). */
+const char *dips_last_error(const dips_handle *h);
+
+/* Run subsequent work on `stream` (a hipStream_t; NULL = the handle's own). */
+dips_status dips_set_stream(dips_handle *h, void *stream);
+
+/* Block until all work issued through `h` has finished. */
+dips_status dips_synchronize(dips_handle *h);
+
+/* Replaces ComputeState::add_texture (dips/src/gpu/mod.rs:170-216): queue an
+ * RGBA8 host frame (len = width*height*4, stride = width*4 as at
+ * bind_groups.rs:264); the 4th frame builds the start texture and the
+ * temporal ring, later frames replace the ring slot. */
+dips_status dips_add_texture(dips_handle *h, uint32_t width, uint32_t height,
+                             const uint8_t *frame_rgba, size_t len);
+
+/* Replaces ComputeState::dispatch (dips/src/gpu/mod.rs:306-397): returns 1
+ * and writes width*height*4 RGBA8 bytes to `out` (Some), 0 while fewer than
+ * four frames were added (None), or a negative dips_status. */
+int dips_dispatch(dips_handle *h, uint8_t *out_rgba, size_t cap);
+
+/* Replaces frame_callback (dips/src/lib.rs:233-246): add_texture, then
+ * dispatch; if dispatch gives None the input is copied to `out`.  Returns 1
+ * when `out` holds the visualisation, 0 when it holds the passthrough copy,
+ * negative on error. */
+int dips_frame_callback(dips_handle *h, uint32_t width, uint32_t height,
+                        const uint8_t *frame_rgba, size_t len, uint8_t *out, size_t cap);
+
+/* Copy the start texture (RGBA8 gray, pre_compute_shader.wgsl:92-132) built
+ * at the 4th frame.  Returns 1 if available, 0 if not yet built. */
+int dips_start_texture(dips_handle *h, uint8_t *out_rgba, size_t cap);
+
+/* North-star batch path: the per-frame difference series of `n_frames`
+ * contiguous frames (each width*height*C bytes, C from params.format).
+ *   ref: overall mode -> the reference frame (NULL = frames[0]);
+ *        per-frame mode -> the frame preceding frames[0] (NULL = frames[0]).
+ *   series: n_frames entries (required).
+ *   absdiff_map: optional n_frames*width*height*C bytes, |F_t - R| per byte.
+ * With DIPS_FLAG_DEVICE_PTRS all four pointers are device pointers and the
+ * call is asynchronous on the handle's stream; otherwise they are host
+ * pointers and the call returns when the results are in host memory. */
+dips_status dips_diff_series(dips_handle *h, uint32_t width, uint32_t height,
+                             const uint8_t *frames, uint32_t n_frames,
+                             const uint8_t *ref, dips_series_entry *series,
+                             uint8_t *absdiff_map);
+
+/* f64 intensity sum of one entry: si_fixed * 2^-32. */
+double dips_series_si(const dips_series_entry *e);
+
+/* Streaming front-end feed (next-1 of SURVEY.md s8f): frames in pageable or
+ * pinned HOST memory are staged through pinned buffers and copied to HBM
+ * with hipMemcpyAsync on a side stream, overlapping the series kernel of the
+ * previous chunk.  Same semantics as dips_diff_series with host pointers;
+ * `chunk_frames` = frames per DMA chunk (0 = automatic). */
+dips_status dips_diff_series_streamed(dips_handle *h, uint32_t width, uint32_t height,
+                                      const uint8_t *host_frames, uint32_t n_frames,
+                                      const uint8_t *host_ref, dips_series_entry *series,
+                                      uint32_t chunk_frames);
+
+/* Synthetic frames (shared integer generator, bit-identical to the oracle),
+ * global frame indices t0 .. t0+n_frames-1, written to DEVICE memory `dst`. */
+dips_status dips_synth_frames(dips_handle *h, uint32_t width, uint32_t height,
+                              uint64_t seed, uint64_t t0, uint32_t n_frames, uint8_t *dst);
+
+/* Kernel timing (DIPS_FLAG_TIME_KERNEL): total milliseconds and launch count
+ * of the series kernel since the last reset, from hipEvents recorded on the
+ * launch stream.  Synchronises the handle's stream. */
+dips_status dips_kernel_time(dips_handle *h, double *total_ms, uint64_t *launches);
+dips_status dips_kernel_time_reset(dips_handle *h);
+
+/* Geometry of the series kernel for a frame shape (for roofline accounting):
+ * waves launched, tiles per frame, bytes of partial records per frame. */
+dips_status dips_series_geometry(dips_handle *h, uint32_t width, uint32_t height,
+                                 uint32_t n_frames, uint64_t *waves, uint64_t *tiles,
+                                 uint64_t *partial_bytes);
+
+/* Library ABI version (DIPS_ABI_VERSION). */
+int dips_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DIPS_HIP_H */

@@ -1,0 +1,77 @@
+/*
+ * dips_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the DiPs per-pixel frame-difference path, used as the
+ * parity oracle for the HIP product in dips_amd/.  Only tests/, the smoke()
+ * entry point and bench.py's cpu_baseline leg may load this library; the
+ * product never links or calls it.
+ *
+ * Parity status: the reference (RubenMovsesyan/DiPs, Rust + WGSL through
+ * wgpu 24 / naga 24.0.0) cannot be built in this image (no cargo/rustc, crates
+ * not vendored) and ships no tests, fixtures or golden vectors (SURVEY.md
+ * s4, s8c).  This oracle is therefore pinned only by analytic known-answer
+ * tests and by an independent numpy restatement (oracle/np_restatement.py);
+ * against the reference itself it is "parity unpinned".  The pinned choices
+ * for backend-defined behaviour are:
+ *   - naga bounds-check policy `Restrict` (Vulkan/DX12) for the
+ *     out-of-bounds bubble-sort index (dips_shader.wgsl:198-203),
+ *   - rgba8unorm load u(c) = c / 255.0f (IEEE division),
+ *   - rgba8unorm store q(x) = rint(clamp(x,0,1) * 255.0f), round-half-even,
+ *     NaN stored as 0,
+ *   - exp/log: the deterministic f32 algorithms documented in DESIGN.md
+ *     (the reference uses the GPU driver's exp/log, <= a few ulp away).
+ */
+#ifndef DIPS_ORACLE_H
+#define DIPS_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* scalar helpers (exported so tests can pin them) */
+float   dips_oracle_u(uint8_t c);          /* rgba8unorm load  */
+uint8_t dips_oracle_q(float x);            /* rgba8unorm store */
+float   dips_oracle_expf(float x);
+float   dips_oracle_logf(float x);
+float   dips_oracle_upper_median4(const float v[4]);
+
+/* Difference series (north-star path).
+ * channels: 1 (gray8), 3 (RGB8), 4 (RGBA8); chroma 0..3; mode 0 overall /
+ * 1 per-frame.  out4[t*4 + {0,1,2,3}] = {SAD, SJ, count, SI_fixed}
+ * (SI_fixed = sum of dI * 2^32, exact).  si_f64[t] = sequential double sum
+ * of dI in pixel order.  dmap (optional) = |F_t - R| per byte.
+ * Returns 0 on success, <0 on invalid arguments. */
+int dips_oracle_series(int channels, int chroma, int mode, float tau,
+                       uint32_t width, uint32_t height,
+                       const uint8_t *frames, uint32_t n_frames,
+                       const uint8_t *ref, uint64_t *out4, double *si_f64,
+                       uint8_t *dmap);
+/* Same, frames split over `nthreads` POSIX threads (CPU baseline). */
+int dips_oracle_series_mt(int channels, int chroma, int mode, float tau,
+                          uint32_t width, uint32_t height,
+                          const uint8_t *frames, uint32_t n_frames,
+                          const uint8_t *ref, uint64_t *out4, double *si_f64,
+                          uint8_t *dmap, int nthreads);
+
+/* Synthetic frame generator (global frame indices t0 .. t0+n-1). */
+void dips_oracle_synth(int channels, uint32_t width, uint32_t height,
+                       uint64_t seed, uint64_t t0, uint32_t n_frames,
+                       uint8_t *out);
+
+/* dips-compat ComputeState emulation (dips/src/gpu/mod.rs:39-398). */
+typedef struct dips_oracle_cs dips_oracle_cs;
+dips_oracle_cs *dips_oracle_cs_new(uint8_t colorize, int32_t window,
+                                   float sensitivity, uint32_t filter,
+                                   uint32_t chroma);
+int  dips_oracle_cs_add_texture(dips_oracle_cs *cs, uint32_t width,
+                                uint32_t height, const uint8_t *rgba);
+int  dips_oracle_cs_dispatch(dips_oracle_cs *cs, uint8_t *out_rgba);
+int  dips_oracle_cs_start_texture(const dips_oracle_cs *cs, uint8_t *out_rgba);
+void dips_oracle_cs_free(dips_oracle_cs *cs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,163 @@
+"""ctypes wrapper for the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg
+import this module.  It loads ``oracle/libdips_oracle.so`` (built by
+``oracle/Makefile``), a plain-C restatement of the DiPs reference semantics
+(see dips_oracle.h for the citations and the "parity unpinned" status).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB: Optional[ctypes.CDLL] = None
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_f64p = ctypes.POINTER(ctypes.c_double)
+
+
+def build(native: bool = False) -> str:
+    """Build the oracle library with make; returns its path."""
+    target = "native" if native else "all"
+    subprocess.run(["make", "-s", "-C", _HERE, target], check=True)
+    return os.path.join(_HERE, "libdips_oracle_native.so" if native else "libdips_oracle.so")
+
+
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    global _LIB
+    if path is None and _LIB is not None:
+        return _LIB
+    if path is None:
+        path = os.path.join(_HERE, "libdips_oracle.so")
+        if not os.path.exists(path):
+            build()
+    lib = ctypes.CDLL(path)
+    lib.dips_oracle_u.argtypes = [ctypes.c_uint8]
+    lib.dips_oracle_u.restype = ctypes.c_float
+    lib.dips_oracle_q.argtypes = [ctypes.c_float]
+    lib.dips_oracle_q.restype = ctypes.c_uint8
+    lib.dips_oracle_expf.argtypes = [ctypes.c_float]
+    lib.dips_oracle_expf.restype = ctypes.c_float
+    lib.dips_oracle_logf.argtypes = [ctypes.c_float]
+    lib.dips_oracle_logf.restype = ctypes.c_float
+    lib.dips_oracle_upper_median4.argtypes = [ctypes.POINTER(ctypes.c_float)]
+    lib.dips_oracle_upper_median4.restype = ctypes.c_float
+    sargs = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+             ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.c_uint32, _u8p,
+             _u64p, _f64p, _u8p]
+    lib.dips_oracle_series.argtypes = sargs
+    lib.dips_oracle_series.restype = ctypes.c_int
+    lib.dips_oracle_series_mt.argtypes = sargs + [ctypes.c_int]
+    lib.dips_oracle_series_mt.restype = ctypes.c_int
+    lib.dips_oracle_synth.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, _u8p]
+    lib.dips_oracle_synth.restype = None
+    lib.dips_oracle_cs_new.argtypes = [ctypes.c_uint8, ctypes.c_int32, ctypes.c_float,
+                                       ctypes.c_uint32, ctypes.c_uint32]
+    lib.dips_oracle_cs_new.restype = ctypes.c_void_p
+    lib.dips_oracle_cs_add_texture.argtypes = [ctypes.c_void_p, ctypes.c_uint32,
+                                               ctypes.c_uint32, _u8p]
+    lib.dips_oracle_cs_add_texture.restype = ctypes.c_int
+    lib.dips_oracle_cs_dispatch.argtypes = [ctypes.c_void_p, _u8p]
+    lib.dips_oracle_cs_dispatch.restype = ctypes.c_int
+    lib.dips_oracle_cs_start_texture.argtypes = [ctypes.c_void_p, _u8p]
+    lib.dips_oracle_cs_start_texture.restype = ctypes.c_int
+    lib.dips_oracle_cs_free.argtypes = [ctypes.c_void_p]
+    lib.dips_oracle_cs_free.restype = None
+    if path == os.path.join(_HERE, "libdips_oracle.so"):
+        _LIB = lib
+    return lib
+
+
+def _p(a: Optional[np.ndarray], t=_u8p):
+    if a is None:
+        return ctypes.cast(None, t)
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(t)
+
+
+def series(frames: np.ndarray, *, mode: int = 0, chroma: int = 0, tau: float = 0.0,
+           ref: Optional[np.ndarray] = None, want_map: bool = False,
+           nthreads: int = 1, lib: Optional[ctypes.CDLL] = None):
+    """frames: uint8 [N, H, W] (gray) or [N, H, W, C].  Returns
+    (out4 uint64 [N,4] = SAD, SJ, count, SI_fixed; si_f64 [N]; dmap or None)."""
+    lib = lib or load()
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    n = frames.shape[0]
+    h, w = frames.shape[1], frames.shape[2]
+    c = 1 if frames.ndim == 3 else frames.shape[3]
+    out4 = np.zeros((n, 4), dtype=np.uint64)
+    si = np.zeros(n, dtype=np.float64)
+    dmap = np.zeros_like(frames) if want_map else None
+    if ref is not None:
+        ref = np.ascontiguousarray(ref, dtype=np.uint8)
+        assert ref.size == h * w * c
+    args = (c, chroma, mode, ctypes.c_float(tau), w, h, _p(frames), n, _p(ref),
+            _p(out4, _u64p), _p(si, _f64p), _p(dmap))
+    if nthreads > 1:
+        rc = lib.dips_oracle_series_mt(*args, nthreads)
+    else:
+        rc = lib.dips_oracle_series(*args)
+    if rc != 0:
+        raise ValueError(f"dips_oracle_series rc={rc}")
+    return out4, si, dmap
+
+
+def synth(channels: int, width: int, height: int, seed: int, t0: int, n: int,
+          lib: Optional[ctypes.CDLL] = None) -> np.ndarray:
+    lib = lib or load()
+    shape = (n, height, width) if channels == 1 else (n, height, width, channels)
+    out = np.zeros(shape, dtype=np.uint8)
+    lib.dips_oracle_synth(channels, width, height, seed, t0, n, _p(out))
+    return out
+
+
+class ComputeState:
+    """Oracle twin of dips/src/gpu/mod.rs ComputeState (new/add_texture/dispatch)."""
+
+    def __init__(self, colorize: bool, spatial_window_size: int, sensitivity: float,
+                 filter_type: int, chroma_filter: int):
+        self._lib = load()
+        self._h = self._lib.dips_oracle_cs_new(1 if colorize else 0, spatial_window_size,
+                                               ctypes.c_float(sensitivity), filter_type,
+                                               chroma_filter)
+        if not self._h:
+            raise ValueError("invalid ComputeState parameters")
+        self._w = self._hgt = 0
+
+    def add_texture(self, width: int, height: int, frame: np.ndarray) -> None:
+        frame = np.ascontiguousarray(frame, dtype=np.uint8)
+        assert frame.size == width * height * 4
+        rc = self._lib.dips_oracle_cs_add_texture(self._h, width, height, _p(frame))
+        if rc != 0:
+            raise ValueError(f"add_texture rc={rc}")
+        self._w, self._hgt = width, height
+
+    def dispatch(self) -> Optional[np.ndarray]:
+        out = np.zeros((self._hgt, self._w, 4), dtype=np.uint8)
+        rc = self._lib.dips_oracle_cs_dispatch(self._h, _p(out))
+        return out if rc == 1 else None
+
+    def start_texture(self) -> Optional[np.ndarray]:
+        out = np.zeros((self._hgt, self._w, 4), dtype=np.uint8)
+        rc = self._lib.dips_oracle_cs_start_texture(self._h, _p(out))
+        return out if rc == 1 else None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.dips_oracle_cs_free(h)
+            self._h = None
+
+
+def frame_callback(width: int, height: int, frame: np.ndarray, compute: ComputeState) -> np.ndarray:
+    """dips/src/lib.rs:233-246: add_texture, then dispatch or pass the input through."""
+    compute.add_texture(width, height, frame)
+    out = compute.dispatch()
+    return out if out is not None else np.array(frame, dtype=np.uint8, copy=True).reshape(height, width, 4)

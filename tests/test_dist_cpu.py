@@ -1,0 +1,85 @@
+"""World-size-2 gloo tests of the frame-range sharding protocol
+(dips_amd.shard): halo exchange, reference broadcast and the single series
+gather reassemble exactly the single-process series.  The per-rank compute
+here is the CPU oracle (test seam); on GPUs it is the HIP operator."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dips_amd import shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _oracle_compute(mode, tau):
+    from oracle import oracle
+
+    def compute(frames, ref, series_out):
+        f = frames.numpy()
+        r = ref.numpy() if ref is not None else None
+        out4, _, _ = oracle.series(f, mode=mode, tau=tau, ref=r)
+        series_out.copy_(torch.from_numpy(out4.view(np.int64)))
+    return compute
+
+
+def _worker(rank, world, port, n_total, mode, tau, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle
+        all_frames = oracle.synth(3, 32, 16, 5, 0, n_total)
+        s, e = shard.frame_range(n_total, world, rank)
+        local = torch.from_numpy(all_frames[s:e].copy())
+        reference = None
+        if mode == 0:
+            reference = torch.from_numpy(all_frames[0].copy()) if rank == 0 else torch.empty_like(local[0])
+            shard.broadcast_reference(reference)
+        full = shard.sharded_series(local, per_frame=(mode == 1), n_total=n_total,
+                                    compute=_oracle_compute(mode, tau), reference=reference)
+        if rank == 0:
+            result_q.put(full.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("n_total", [7, 8])
+def test_sharded_equals_single(mode, n_total):
+    from oracle import oracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, mode, 2 / 255, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    frames = oracle.synth(3, 32, 16, 5, 0, n_total)
+    want, _, _ = oracle.series(frames, mode=mode, tau=2 / 255)
+    assert np.array_equal(got.view(np.uint64), want)
+
+
+def test_frame_ranges_cover_and_balance():
+    for n in (1, 7, 40000):
+        for world in (1, 2, 3, 8):
+            r = shard.frame_ranges(n, world)
+            assert r[0][0] == 0 and r[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+            sizes = [e - s for s, e in r]
+            assert max(sizes) - min(sizes) <= 1

@@ -1,0 +1,159 @@
+"""GPU parity tests of the batch difference series (HIP, through the C ABI)
+against the CPU oracle (oracle/dips_oracle.c) on the same seeded inputs.
+
+Bar: bit-exact for SAD, SJ, count, SI_fixed and the |F-R| byte map; the f64
+intensity sum within 1e-6 relative of the oracle's sequential f64 sum."""
+import itertools
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+SI_RTOL = 1e-6
+
+
+def _frames(c, w, h, n, seed, kind):
+    if kind == "synth":
+        return oracle.synth(c, w, h, seed, 0, n)
+    rng = np.random.default_rng(seed)
+    shape = (n, h, w) if c == 1 else (n, h, w, c)
+    f = rng.integers(0, 256, shape, dtype=np.uint8)
+    if n > 2:
+        f[2] = f[1]  # an exact repeat -> zero row in per-frame mode
+    return f
+
+
+def _check(got, want_out4, want_si, got_map=None, want_map=None):
+    arr = got.as_array()
+    assert np.array_equal(arr, want_out4), (arr, want_out4)
+    np.testing.assert_allclose(got.si, want_si, rtol=SI_RTOL, atol=1e-9)
+    if want_map is not None:
+        assert np.array_equal(got_map, want_map)
+
+
+FAST_SHAPES = [(64, 48), (128, 8)]     # pixels % 16 == 0 -> fast kernel
+GENERIC_SHAPES = [(37, 23), (1, 1), (5, 3)]
+
+
+@pytest.mark.parametrize("c", [1, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("shape", FAST_SHAPES + GENERIC_SHAPES)
+def test_series_matches_oracle(c, mode, shape):
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    w, h = shape
+    for chroma, tau, kind in itertools.product([0, 2] if c != 1 else [0], [0.0, 8 / 255], ["synth", "random"]):
+        frames = _frames(c, w, h, 7, 11 + chroma, kind)
+        op = DiffSeriesOperator(PixelFormat(c), Mode(mode), tau, chroma)
+        try:
+            got, gmap = op(frames, want_map=True)
+            got_nomap, _ = op(frames)
+        finally:
+            op.close()
+        out4, si, dmap = oracle.series(frames, mode=mode, chroma=chroma, tau=tau, want_map=True)
+        _check(got, out4, si, gmap, dmap)
+        _check(got_nomap, out4, si)
+
+
+@pytest.mark.parametrize("c", [1, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_series_explicit_ref(c, mode):
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    frames = _frames(c, 64, 32, 5, 3, "synth")
+    ref = _frames(c, 64, 32, 1, 99, "random")[0]
+    op = DiffSeriesOperator(PixelFormat(c), Mode(mode), 0.0, 0)
+    try:
+        got, _ = op(frames, ref=ref)
+    finally:
+        op.close()
+    out4, si, _ = oracle.series(frames, mode=mode, ref=ref)
+    _check(got, out4, si)
+
+
+@pytest.mark.parametrize("c", [1, 3, 4])
+def test_fast_equals_generic(c):
+    from dips_amd import diff_series, Mode, PixelFormat
+    frames = _frames(c, 256, 64, 9, 5, "synth")
+    for mode in (Mode.Overall, Mode.PerFrame):
+        a, am = diff_series(frames, fmt=PixelFormat(c), mode=mode, tau=3 / 255, want_map=True)
+        b, bm = diff_series(frames, fmt=PixelFormat(c), mode=mode, tau=3 / 255, want_map=True,
+                            force_generic=True)
+        assert np.array_equal(a.as_array(), b.as_array())
+        assert np.array_equal(am, bm)
+
+
+def test_single_pixel_known_answer():
+    """one pixel (0,0,0) -> (255,255,255): SJ = 510, SI = 1.0."""
+    from dips_amd import diff_series, PixelFormat
+    for w, h in [(64, 48), (7, 5)]:
+        f = np.zeros((2, h, w, 3), dtype=np.uint8)
+        f[1, h // 2, w // 3] = 255
+        s, _ = diff_series(f, fmt=PixelFormat.RGB8)
+        assert list(s.sj) == [0, 510]
+        assert list(s.sad) == [0, 765]
+        assert list(s.count) == [0, 1]
+        assert s.si[1] == 1.0
+
+
+def test_identical_frames_zero():
+    from dips_amd import diff_series, PixelFormat, Mode
+    f = np.repeat(oracle.synth(3, 64, 48, 1, 0, 1), 6, axis=0)
+    for mode in (Mode.Overall, Mode.PerFrame):
+        s, m = diff_series(f, fmt=PixelFormat.RGB8, mode=mode, want_map=True)
+        assert not s.as_array().any()
+        assert not m.any()
+
+
+def test_streamed_equals_batch():
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    frames = _frames(3, 64, 48, 23, 7, "synth")
+    ref = _frames(3, 64, 48, 1, 8, "random")[0]
+    for mode in (Mode.Overall, Mode.PerFrame):
+        op = DiffSeriesOperator(PixelFormat.RGB8, mode, 1 / 255, 0)
+        try:
+            for chunk in (1, 4, 5, 0):
+                for r in (None, ref):
+                    a = op.streamed(frames, ref=r, chunk_frames=chunk)
+                    out4, _, _ = oracle.series(frames, mode=int(mode), tau=1 / 255, ref=r)
+                    assert np.array_equal(a.as_array(), out4), (mode, chunk, r is None)
+        finally:
+            op.close()
+
+
+@pytest.mark.parametrize("c", [1, 3, 4])
+def test_synth_device_bit_exact(c):
+    import torch
+    from dips_amd import DiffSeriesOperator, PixelFormat
+    w, h, n, t0 = 61, 37, 5, 1234
+    shape = (n, h, w) if c == 1 else (n, h, w, c)
+    dst = torch.empty(shape, dtype=torch.uint8, device="cuda")
+    op = DiffSeriesOperator(PixelFormat(c))
+    try:
+        op.synth_device(dst, w, h, 0xD1B5, t0)
+        torch.cuda.synchronize()
+    finally:
+        op.close()
+    want = oracle.synth(c, w, h, 0xD1B5, t0, n)
+    assert np.array_equal(dst.cpu().numpy(), want)
+
+
+def test_device_path_matches_host_path():
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    w, h, n = 3840, 2160, 6
+    for mode in (Mode.Overall, Mode.PerFrame):
+        op = DiffSeriesOperator(PixelFormat.RGB8, mode, 8 / 255, 0)
+        try:
+            dev = torch.empty((n, h, w, 3), dtype=torch.uint8, device="cuda")
+            op.synth_device(dev, w, h, 0xD1B5, 100)
+            ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+            op.run_device(dev, ser)
+            torch.cuda.synchronize()
+            host = dev.cpu().numpy()
+            out4, si, _ = oracle.series(host, mode=int(mode), tau=8 / 255, nthreads=8)
+            got = ser.cpu().numpy().view(np.uint64)
+            assert np.array_equal(got, out4)
+        finally:
+            op.close()
