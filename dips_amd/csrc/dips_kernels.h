@@ -11,6 +11,15 @@ namespace dips {
 // Unroll (vecs per lane) of the fast series kernel; a tile = 64 * U vecs.
 constexpr int kUnrollRGB = 4;   // 1024 px / wave / frame for RGB8 and RGBA8
 constexpr int kUnrollGray = 2;  // 2048 px / wave / frame for GRAY8
+// Prefetch depth: frames of loads each wave keeps in flight.
+#ifndef DIPS_DEPTH_RGB
+#define DIPS_DEPTH_RGB 2
+#endif
+#ifndef DIPS_DEPTH_GRAY
+#define DIPS_DEPTH_GRAY 2
+#endif
+constexpr int kDepthRGB = DIPS_DEPTH_RGB;
+constexpr int kDepthGray = DIPS_DEPTH_GRAY;
 
 struct SeriesArgs {
     const uint8_t* frames;   // n_frames * frame_bytes, contiguous

@@ -84,11 +84,33 @@ __device__ __forceinline__ uint32_t absdiff_bytes(uint32_t a, uint32_t b) {
     return as_u32(de) | (as_u32(dd) << 8);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Exact rgba8unorm load without a division or a table: u(c) = c / 255
+// correctly rounded equals fma(c, K_HI, c * K_LO) for every byte c, with
+// K_HI + K_LO the double-float split of 1/255 (checked exhaustively in
+// tests/test_oracle.py::test_unorm_fma_identity).  Two values per packed op.
+constexpr float kUnormHi = 0x1.010102p-8f;
+constexpr float kUnormLo = -0x1.fdfdfep-33f;
+
+__device__ __forceinline__ f32x2 unorm2(f32x2 c) {
+    const f32x2 hi = {kUnormHi, kUnormHi};
+    const f32x2 lo = {kUnormLo, kUnormLo};
+    return __builtin_elementwise_fma(c, hi, c * lo);
+}
+
+__device__ __forceinline__ f32x2 u16x2_to_f32x2(u16x2 v) {
+    // byte values in the low byte of each half: v_cvt_f32_ubyte0 / ubyte2
+    const uint32_t w = as_u32(v);
+    return f32x2{(float)(w & 0xFFu), (float)((w >> 16) & 0xFFu)};
+}
+
 // Derived state of 4 RGB(A) pixels: J = max+min as two u16 pairs and the
-// doubled intensity I2 = u(max) + u(min) (= 2 * get_intensity, exact).
+// doubled intensity I2 = u(max) + u(min) (= 2 * get_intensity, exact), as
+// two f32 pairs.
 struct Px4 {
     uint32_t j[2];
-    float i2[4];
+    f32x2 i2[2];
 };
 
 // Pair planes (two pixels per dword, one byte per u16 half) of one vec.
@@ -114,56 +136,81 @@ __device__ __forceinline__ void pair_planes(const uint32_t (&d)[Fmt<C>::NDW], u1
     }
 }
 
+// Placeholder kept in the signatures of the per-vec helpers; the exact
+// arithmetic u() needs no table (an LDS table measured slower on gfx950).
+struct Lut {
+    const float* p;
+    uint32_t lb;  // lane & 31
+};
+
+__device__ __forceinline__ f32x2 unorm_pair(u16x2 v, Lut) { return unorm2(u16x2_to_f32x2(v)); }
+
 template <int C, int CH>
-__device__ __forceinline__ void derive_px4(const uint32_t (&d)[Fmt<C>::NDW], const float* lut, Px4& s) {
+__device__ __forceinline__ void derive_px4(const uint32_t (&d)[Fmt<C>::NDW], Px4& s, Lut lut) {
     u16x2 r[2], g[2], b[2];
     pair_planes<C>(d, r, g, b);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        u16x2 mx, mn;
         if constexpr (CH == 0) {
-            mx = __builtin_elementwise_max(__builtin_elementwise_max(r[k], g[k]), b[k]);
-            mn = __builtin_elementwise_min(__builtin_elementwise_min(r[k], g[k]), b[k]);
-        } else if constexpr (CH == 1) {
-            mx = mn = r[k];
-        } else if constexpr (CH == 2) {
-            mx = mn = g[k];
+            const u16x2 mx = __builtin_elementwise_max(__builtin_elementwise_max(r[k], g[k]), b[k]);
+            const u16x2 mn = __builtin_elementwise_min(__builtin_elementwise_min(r[k], g[k]), b[k]);
+            s.j[k] = as_u32(mx + mn);
+            s.i2[k] = unorm_pair(mx, lut) + unorm_pair(mn, lut);
         } else {
-            mx = mn = b[k];
+            const u16x2 ch = CH == 1 ? r[k] : (CH == 2 ? g[k] : b[k]);
+            s.j[k] = as_u32(ch + ch);
+            const f32x2 uc = unorm_pair(ch, lut);
+            s.i2[k] = uc + uc;
         }
-        s.j[k] = as_u32(mx + mn);
-        s.i2[2 * k + 0] = lut[mx.x] + lut[mn.x];
-        s.i2[2 * k + 1] = lut[mx.y] + lut[mn.y];
     }
 }
 
 template <int C> struct RefState;
 template <> struct RefState<3> { uint32_t b[3]; Px4 px; };
 template <> struct RefState<4> { uint32_t b[4]; Px4 px; };
-template <> struct RefState<1> { uint32_t b[4]; float i[16]; };
+template <> struct RefState<1> { uint32_t b[4]; f32x2 i[8]; };
 
+// Per-lane accumulators.  Each selected dI is an f32 multiple of 2^-31
+// (RGB, I2 units) or 2^-32 (gray) in [0, 2], so a per-lane f64 sum of up to
+// 32 of them is EXACT (< 2^6 with 2^-32 granularity: 38 bits < 53).  The
+// pixel count is wave-wide: the popcount of each compare mask on the scalar
+// unit (measured: an LDS table for u() and a per-lane count in VALU are both
+// slower; an f32 hi/lo split of dI is exact too but costs more VALU).
 struct Acc {
-    uint32_t sad, sj, cnt;
-    double si;
+    uint32_t sad, sj;  // per lane
+    uint32_t cnt;      // wave-wide
+    double si;         // per lane
 };
 
+__device__ __forceinline__ void acc_intensity(Acc& acc, f32x2 cur, f32x2 ref, float thr) {
+    const f32x2 d = cur - ref;
+    const float a0 = fabsf(d.x), a1 = fabsf(d.y);
+    const bool s0 = a0 > thr, s1 = a1 > thr;
+    acc.cnt += (uint32_t)__builtin_popcountll(__ballot(s0)) + (uint32_t)__builtin_popcountll(__ballot(s1));
+    acc.si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
+}
+
 template <int C, int CH>
-__device__ __forceinline__ void derive_ref(const uint32_t (&d)[Fmt<C>::NDW], const float* lut, RefState<C>& s) {
+__device__ __forceinline__ void derive_ref(const uint32_t (&d)[Fmt<C>::NDW], RefState<C>& s, Lut lut) {
 #pragma unroll
     for (int k = 0; k < Fmt<C>::NDW; ++k) s.b[k] = d[k];
     if constexpr (C == 1) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) s.i[k] = lut[(d[k >> 2] >> (8 * (k & 3))) & 0xFFu];
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t w = d[k >> 1] >> (16 * (k & 1));
+            s.i[k] = unorm2(f32x2{(float)(w & 0xFFu), (float)((w >> 8) & 0xFFu)});
+        }
     } else {
-        derive_px4<C, CH>(d, lut, s.px);
+        derive_px4<C, CH>(d, s.px, lut);
     }
 }
 
-// Accumulate one vec of the current frame against the reference state; in
-// per-frame mode the state then becomes the current frame's.
+// Accumulate one vec of the current frame against the reference state `ref`;
+// in per-frame mode the current frame's state is written to `next` (the
+// caller ping-pongs two state arrays, so no register copies are needed).
 template <int C, int CH, bool PF, bool MAP>
-__device__ __forceinline__ void process_vec(RefState<C>& ref, const uint32_t (&f)[Fmt<C>::NDW], const float* lut,
-                                            float thr, Acc& acc, uint32_t (&map)[Fmt<C>::NDW]) {
+__device__ __forceinline__ void process_vec(const RefState<C>& ref, RefState<C>& next, const uint32_t (&f)[Fmt<C>::NDW],
+                                            float thr, Acc& acc, uint32_t (&map)[Fmt<C>::NDW], Lut lut) {
 #pragma unroll
     for (int k = 0; k < Fmt<C>::NDW; ++k) {
         acc.sad = __builtin_amdgcn_sad_u8(f[k], ref.b[k], acc.sad);
@@ -171,61 +218,170 @@ __device__ __forceinline__ void process_vec(RefState<C>& ref, const uint32_t (&f
     }
     if constexpr (C == 1) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const float cur = lut[(f[k >> 2] >> (8 * (k & 3))) & 0xFFu];
-            const float a = fabsf(cur - ref.i[k]);
-            const bool sel = a > thr;
-            acc.cnt += sel ? 1u : 0u;
-            acc.si += (double)(sel ? a : 0.0f);
-            if constexpr (PF) ref.i[k] = cur;
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t w = f[k >> 1] >> (16 * (k & 1));
+            const f32x2 cur = unorm2(f32x2{(float)(w & 0xFFu), (float)((w >> 8) & 0xFFu)});
+            acc_intensity(acc, cur, ref.i[k], thr);
+            if constexpr (PF) next.i[k] = cur;
         }
     } else {
         Px4 cur;
-        derive_px4<C, CH>(f, lut, cur);
+        derive_px4<C, CH>(f, cur, lut);
         acc.sj = __builtin_amdgcn_sad_u16(cur.j[0], ref.px.j[0], acc.sj);
         acc.sj = __builtin_amdgcn_sad_u16(cur.j[1], ref.px.j[1], acc.sj);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float a = fabsf(cur.i2[k] - ref.px.i2[k]);
-            const bool sel = a > thr;
-            acc.cnt += sel ? 1u : 0u;
-            acc.si += (double)(sel ? a : 0.0f);
-        }
-        if constexpr (PF) ref.px = cur;
+        acc_intensity(acc, cur.i2[0], ref.px.i2[0], thr);
+        acc_intensity(acc, cur.i2[1], ref.px.i2[1], thr);
+        if constexpr (PF) next.px = cur;
     }
     if constexpr (PF) {
 #pragma unroll
-        for (int k = 0; k < Fmt<C>::NDW; ++k) ref.b[k] = f[k];
+        for (int k = 0; k < Fmt<C>::NDW; ++k) next.b[k] = f[k];
     }
 }
 
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// ---------------------------------------------------------------------------
+// Cross-lane reduction of several per-lane values at once, no LDS.
+// N = 4 or 8 values.  The first steps exchange HALF of the values with the
+// partner lane (xor 32 by v_permlane32_swap, xor 16 by v_permlane16_swap,
+// xor 8 by DPP row_ror:8 when N = 8), so each lane ends up owning one value
+// index; the remaining steps are plain DPP butterflies inside 8-lane groups.
+// Value v's wave sum then sits in lane 8v (N = 8) or 16v (N = 4).  Compared
+// with N separate butterflies this is ~1/3 of the instructions and the N
+// chains overlap instead of running back to back.
+// ---------------------------------------------------------------------------
+#define DIPS_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), 0xF, 0xF, false))
+
+__device__ __forceinline__ uint32_t swap32_sum(uint32_t a, uint32_t b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    return r[0] + r[1];
 }
 
-__device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+__device__ __forceinline__ uint32_t swap16_sum(uint32_t a, uint32_t b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    return r[0] + r[1];
 }
 
+__device__ __forceinline__ uint32_t group8_sum(uint32_t y) {
+    y += DIPS_DPP(y, 0xB1);   // quad_perm [1,0,3,2]  (xor 1)
+    y += DIPS_DPP(y, 0x4E);   // quad_perm [2,3,0,1]  (xor 2)
+    y += DIPS_DPP(y, 0x141);  // row_half_mirror      (xor 7 inside 8 lanes)
+    return y;
+}
+
+// out[v] = sum over the 64 lanes of in[v] (wave-uniform results).
+__device__ __forceinline__ void wave_sum8(const uint32_t (&in)[8], uint32_t (&out)[8], uint32_t lane) {
+    uint32_t w[4], x[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = swap32_sum(in[k], in[4 + k]);  // lane owns 4*b5 + k
+    x[0] = swap16_sum(w[0], w[2]);                                     // owns 4*b5 + 2*b4 + 0
+    x[1] = swap16_sum(w[1], w[3]);                                     // owns 4*b5 + 2*b4 + 1
+    const bool b3 = (lane & 8u) != 0;
+    const uint32_t keep = b3 ? x[1] : x[0];
+    const uint32_t send = b3 ? x[0] : x[1];
+    const uint32_t y = group8_sum(keep + DIPS_DPP(send, 0x128));      // row_ror:8 (xor 8)
+#pragma unroll
+    for (int v = 0; v < 8; ++v) out[v] = (uint32_t)__builtin_amdgcn_readlane((int)y, 8 * v);
+}
+
+__device__ __forceinline__ void wave_sum4(const uint32_t (&in)[4], uint32_t (&out)[4]) {
+    const uint32_t w0 = swap32_sum(in[0], in[2]);  // lane owns 2*b5 + 0
+    const uint32_t w1 = swap32_sum(in[1], in[3]);  // lane owns 2*b5 + 1
+    uint32_t y = swap16_sum(w0, w1);               // owns 2*b5 + b4
+    y += DIPS_DPP(y, 0x128);                       // row_ror:8 (xor 8)
+    y = group8_sum(y);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) out[v] = (uint32_t)__builtin_amdgcn_readlane((int)y, 16 * v);
+}
+
+// Accumulate one frame of one tile into four per-lane reduction values
+//   RGB(A): {SAD, SJ + count << 20, H, L};  gray: {SAD + count << 20, H, L, 0}
+// (H, L: the exact fixed-point split of the intensity sum, see Acc).  The
+// count rides in bits 20.. because both wave sums stay below 2^20 for the
+// tile sizes used here (1024 RGB / 2048 gray pixels per wave and frame).
 template <int C, int CH, int U, bool PF, bool MAP>
-__global__ __launch_bounds__(256) void series_fast_kernel(SeriesArgs a) {
+__device__ __forceinline__ void frame_accumulate(const SeriesArgs& a, const RefState<C> (&ref)[U],
+                                                 RefState<C> (&next)[U], const uint32_t (&cur)[U][Fmt<C>::NDW],
+                                                 const uint32_t (&voff)[U], uint32_t t, uint32_t* vals, Lut lut) {
     using F = Fmt<C>;
-    __shared__ float lut[256];
-    lut[threadIdx.x] = unorm_load(threadIdx.x);
-    __syncthreads();
+    constexpr int kScaleBits = (C == 1) ? 32 : 31;
+    Acc acc{};
+    uint32_t map[U][F::NDW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) process_vec<C, CH, PF, MAP>(ref[u], next[u], cur[u], a.thr, acc, map[u], lut);
+    if constexpr (MAP) {
+        const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.frame_bytes);
+#pragma unroll
+        for (int u = 0; u < U; ++u) store_vec<C>(rm, voff[u], map[u]);
+    }
+    // the wave-wide count enters the lane sum through lane 0 only
+    acc.cnt = (threadIdx.x & 63u) == 0u ? acc.cnt : 0u;
+    // exact per-lane fixed point, split so both halves sum in u32 over the
+    // wave: H = whole units of 2^-16, L = the remainder in 2^-kScaleBits
+    const double q = acc.si * 65536.0;
+    const uint32_t hfix = (uint32_t)q;  // trunc
+    const int32_t lfix = (int32_t)((q - (double)hfix) * (double)(1ull << (kScaleBits - 16)));
+    if constexpr (C == 1) {
+        vals[0] = acc.sad + (acc.cnt << 20);
+        vals[1] = hfix;
+        vals[2] = (uint32_t)lfix;
+        vals[3] = 0u;
+    } else {
+        vals[0] = acc.sad;
+        vals[1] = acc.sj + (acc.cnt << 20);
+        vals[2] = hfix;
+        vals[3] = (uint32_t)lfix;
+    }
+}
 
+// Partial record of one (tile, frame) from the four wave sums; written by
+// lane 0 only, branch free: the other lanes' offsets fall outside the
+// descriptor's range and the hardware drops them.
+template <int C>
+__device__ __forceinline__ void write_record(__amdgpu_buffer_rsrc_t rpart, uint32_t t, uint32_t lane,
+                                             const uint32_t* s) {
+    constexpr int kScaleBits = (C == 1) ? 32 : 31;
+    uint32_t sad, sj, cnt, hsum;
+    int32_t lsum;
+    if constexpr (C == 1) {
+        sad = s[0] & 0xFFFFFu;
+        cnt = s[0] >> 20;
+        sj = 2u * sad;
+        hsum = s[1];
+        lsum = (int32_t)s[2];
+    } else {
+        sad = s[0];
+        sj = s[1] & 0xFFFFFu;
+        cnt = s[1] >> 20;
+        hsum = s[2];
+        lsum = (int32_t)s[3];
+    }
+    const uint64_t sif = ((uint64_t)hsum << (kScaleBits - 16)) + (uint64_t)(int64_t)lsum;
+    const uint64_t hi = sif | ((uint64_t)cnt << 48);
+    u32x4 rec;
+    rec.x = sad;
+    rec.y = sj;
+    rec.z = (uint32_t)hi;
+    rec.w = (uint32_t)(hi >> 32);
+    __builtin_amdgcn_raw_buffer_store_b128(rec, rpart, lane == 0 ? t * 16u : 0x80000000u, 0, 0);
+}
+
+// D = frames of loads kept in flight per wave (register ring of D frames);
+// frames are processed in pairs whose eight reduction values share one
+// wave_sum8.
+#ifndef DIPS_MIN_WAVES_PER_SIMD
+#define DIPS_MIN_WAVES_PER_SIMD 1
+#endif
+template <int C, int CH, int U, int D, bool PF, bool MAP>
+__global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kernel(SeriesArgs a) {
+    static_assert(D % 2 == 0, "frames are processed in pairs: D must be even");
+    using F = Fmt<C>;
     const uint32_t lane = threadIdx.x & 63u;
+    const Lut lut{nullptr, lane & 31u};
     // wave id through readfirstlane: every loop bound and address below is
     // then provably wave-uniform (scalar registers, no waterfall loops).
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (wave >= a.n_waves) return;
     const uint32_t fb = a.frame_bytes;
-    // Doubled-intensity units for RGB(A) (I2 = 2I), plain intensity for gray.
-    constexpr double kFixScale = (C == 1) ? 4294967296.0 : 2147483648.0;
 
     uint64_t i = (uint64_t)wave * a.items / a.n_waves;
     const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
@@ -240,59 +396,77 @@ __global__ __launch_bounds__(256) void series_fast_kernel(SeriesArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) voff[u] = ((tile * U + u) * 64u + lane) * (uint32_t)F::VB;
 
-        // Reference state of this tile.
+        // Reference state of this tile (ping-pong pair in per-frame mode:
+        // even frames read sa and write sb, odd frames the reverse).
         const uint8_t* rp = PF ? (t == 0 ? a.ref0 : a.frames + (uint64_t)(t - 1) * fb) : a.ref0;
-        RefState<C> ref[U];
+        RefState<C> sa[U], sb[U];
         {
             const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, fb);
             uint32_t d[U][F::NDW];
 #pragma unroll
             for (int u = 0; u < U; ++u) load_vec<C>(rr, voff[u], d[u]);
 #pragma unroll
-            for (int u = 0; u < U; ++u) derive_ref<C, CH>(d[u], lut, ref[u]);
+            for (int u = 0; u < U; ++u) derive_ref<C, CH>(d[u], sa[u], lut);
         }
+        const __amdgpu_buffer_rsrc_t rpart = make_rsrc(a.partials + 2 * (uint64_t)tile * a.n_frames, a.n_frames * 16u);
+#ifdef DIPS_PROBE_SAMEFRAME
+        // probe build only: every frame load re-reads the segment's first
+        // frame (L2/MALL hits) -- the kernel's compute-only time
+        const uint32_t tlast = t;
+#else
+        const uint32_t tlast = tend - 1;
+#endif
 
-        uint32_t cur[U][F::NDW];
-        {
-            const __amdgpu_buffer_rsrc_t rf = make_rsrc(a.frames + (uint64_t)t * fb, fb);
+        // Ring of D frames in flight; loads past the segment are clamped to
+        // its last frame (one redundant frame per segment, no branches).
+        uint32_t buf[D][U][F::NDW];
 #pragma unroll
-            for (int u = 0; u < U; ++u) load_vec<C>(rf, voff[u], cur[u]);
+        for (int d = 0; d < D; ++d) {
+            const uint32_t tl = min(t + (uint32_t)d, tlast);
+            const __amdgpu_buffer_rsrc_t rf = make_rsrc(a.frames + (uint64_t)tl * fb, fb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) load_vec<C>(rf, voff[u], buf[d][u]);
         }
-        for (; t < tend; ++t) {
-            uint32_t nxt[U][F::NDW];
-            if (t + 1 < tend) {
-                const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.frames + (uint64_t)(t + 1) * fb, fb);
+        // Steady state: D frames per iteration, straight-line code.
+        for (; t + D <= tend; t += D) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) load_vec<C>(rn, voff[u], nxt[u]);
+            for (int d = 0; d < D; d += 2) {
+                uint32_t v[8], sum[8];
+                frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, buf[d], voff, t + d, v, lut);
+                // keep the refill of buf[d] behind its last use: hoisting it
+                // would cost a register copy of the whole buffer
+                __builtin_amdgcn_sched_barrier(0);
+                {
+                    const uint32_t tl = min(t + (uint32_t)(d + D), tlast);
+                    const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.frames + (uint64_t)tl * fb, fb);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) load_vec<C>(rn, voff[u], buf[d][u]);
+                }
+                if constexpr (PF) frame_accumulate<C, CH, U, PF, MAP>(a, sb, sa, buf[d + 1], voff, t + d + 1, v + 4, lut);
+                else frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, buf[d + 1], voff, t + d + 1, v + 4, lut);
+                __builtin_amdgcn_sched_barrier(0);
+                {
+                    const uint32_t tl = min(t + (uint32_t)(d + 1 + D), tlast);
+                    const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.frames + (uint64_t)tl * fb, fb);
+#pragma unroll
+                    for (int u = 0; u < U; ++u) load_vec<C>(rn, voff[u], buf[d + 1][u]);
+                }
+                wave_sum8(v, sum, lane);
+                write_record<C>(rpart, t + d, lane, sum);
+                write_record<C>(rpart, t + d + 1, lane, sum + 4);
             }
-            Acc acc{0u, 0u, 0u, 0.0};
-            uint32_t map[U][F::NDW];
+        }
+        // Tail (< D frames): already in buf[0 .. tend - t - 1].  State parity
+        // is even here (D is even), so frame t + d reads sa when d is even.
 #pragma unroll
-            for (int u = 0; u < U; ++u) process_vec<C, CH, PF, MAP>(ref[u], cur[u], lut, a.thr, acc, map[u]);
-            if constexpr (MAP) {
-                const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * fb, fb);
-#pragma unroll
-                for (int u = 0; u < U; ++u) store_vec<C>(rm, voff[u], map[u]);
+        for (int d = 0; d < D - 1; ++d) {
+            if (t + d < tend) {
+                uint32_t v[4], sum[4];
+                if (PF && (d & 1)) frame_accumulate<C, CH, U, PF, MAP>(a, sb, sa, buf[d], voff, t + d, v, lut);
+                else frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, buf[d], voff, t + d, v, lut);
+                wave_sum4(v, sum);
+                write_record<C>(rpart, t + d, lane, sum);
             }
-            uint32_t sad = wave_sum_u32(acc.sad);
-            uint32_t sj = (C == 1) ? 0u : wave_sum_u32(acc.sj);
-            uint32_t cnt = wave_sum_u32(acc.cnt);
-            double si = wave_sum_f64(acc.si);
-            if (lane == 0) {
-                if constexpr (C == 1) sj = 2u * sad;
-                const uint64_t sif = (uint64_t)(si * kFixScale);
-                u32x4 rec;
-                rec.x = sad;
-                rec.y = sj;
-                const uint64_t hi = sif | ((uint64_t)cnt << 48);
-                rec.z = (uint32_t)hi;
-                rec.w = (uint32_t)(hi >> 32);
-                *reinterpret_cast<u32x4*>(a.partials + 2 * ((uint64_t)tile * a.n_frames + t)) = rec;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int k = 0; k < F::NDW; ++k) cur[u][k] = nxt[u][k];
         }
     }
 }
@@ -387,7 +561,8 @@ __global__ __launch_bounds__(256) void series_generic_kernel(GenericArgs a) {
 }
 
 // Synthetic frames: F_t[y,x,c] = clamp(base + blob_t + noise, 0, 255)
-// (bit-identical to oracle/dips_oracle.c dips_oracle_synth).
+// (bit-identical to the CPU generator of the test oracle,
+// checked by tests/test_gpu_series.py::test_synth_device_bit_exact).
 __global__ __launch_bounds__(256) void synth_kernel(SynthArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * 256u;
     const uint64_t n_chunks = (a.total_bytes + 15u) / 16u;
@@ -447,7 +622,7 @@ __global__ __launch_bounds__(256) void synth_kernel(SynthArgs a) {
 
 template <int C, int CH, int U, bool PF, bool MAP>
 static const void* fast_ptr() {
-    return reinterpret_cast<const void*>(&series_fast_kernel<C, CH, U, PF, MAP>);
+    return reinterpret_cast<const void*>(&series_fast_kernel<C, CH, U, (C == 1 ? kDepthGray : kDepthRGB), PF, MAP>);
 }
 
 template <int C, int U>

@@ -1,0 +1,90 @@
+"""Generate the committed golden fixtures (TEST INFRASTRUCTURE).
+
+The reference (Rust + WGSL through wgpu) cannot run in this image and ships
+no fixtures, so the fixtures are produced by the
+independent numpy restatement (oracle/np_restatement.py) and accepted only
+where the C oracle (oracle/dips_oracle.c) agrees bit for bit.  They pin the
+oracle against regressions; against the reference they are "parity
+unpinned" (DESIGN.md "Oracle").
+
+Run: python tests/golden/make_golden.py   (writes *.npz + manifest.json here)
+"""
+import itertools
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import np_restatement as nr  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+
+def main():
+    manifest = {
+        "generator": "tests/golden/make_golden.py (numpy restatement, cross-checked with the C oracle)",
+        "pins": {
+            "bounds_policy": "naga Restrict (Vulkan/DX12)",
+            "unorm_load": "c / 255.0f (IEEE division)",
+            "unorm_store": "rint(clamp(x,0,1)*255.0f), round half to even, NaN -> 0",
+            "exp_log": "deterministic f32 algorithms of DESIGN.md",
+            "spatial_filter_race": "filter reads the slot as it was before the dispatch",
+        },
+        "series": [],
+        "compute_state": [],
+    }
+    rng = np.random.default_rng(20261015)
+    cases = []
+    for c, mode in itertools.product([1, 3, 4], [0, 1]):
+        for chroma in ([0] if c == 1 else [0, 2]):
+            for tau in (0.0, 8 / 255):
+                cases.append((c, mode, chroma, tau))
+    for idx, (c, mode, chroma, tau) in enumerate(cases):
+        w, h = (64, 48) if idx % 2 == 0 else (37, 23)
+        frames = nr.synth(c, w, h, 1 + idx, 0, 6)
+        if idx % 3 == 0:  # mix in random frames and an exact repeat
+            frames[2] = rng.integers(0, 256, frames[2].shape, dtype=np.uint8)
+            frames[3] = frames[2]
+        ref = rng.integers(0, 256, frames[0].shape, dtype=np.uint8) if idx % 4 == 1 else None
+        out4, si, dmap = nr.series(frames, mode=mode, chroma=chroma, tau=tau, ref=ref)
+        o4, si_c, dm_c = oracle.series(frames, mode=mode, chroma=chroma, tau=tau, ref=ref, want_map=True)
+        assert np.array_equal(out4, o4) and np.array_equal(dmap, dm_c)
+        assert np.allclose(si, si_c, rtol=1e-12)
+        name = f"series_{idx:02d}_c{c}_m{mode}_ch{chroma}_t{int(round(tau * 255))}.npz"
+        arrays = dict(frames=frames, out4=out4, si=si_c, dmap=dmap)
+        if ref is not None:
+            arrays["ref"] = ref
+        np.savez_compressed(os.path.join(HERE, name), **arrays)
+        manifest["series"].append({"file": name, "channels": c, "mode": mode, "chroma": chroma,
+                                   "tau": tau, "width": w, "height": h, "frames": int(frames.shape[0]),
+                                   "ref": ref is not None})
+    cs_cases = [(False, 1, 5.0, 255, 0), (True, 1, 5.0, 0, 0), (False, 1, 3.0, 1, 2),
+                (True, 3, 5.0, 255, 0), (False, 5, 2.0, 0, 1), (True, 2, 5.0, 1, 3)]
+    for idx, params in enumerate(cs_cases):
+        w, h = 24, 16
+        frames = rng.integers(0, 256, (8, h, w, 4), dtype=np.uint8)
+        frames[5] = frames[4]
+        a = nr.ComputeState(*params)
+        b = oracle.ComputeState(*params)
+        outs = []
+        for k in range(8):
+            a.add_texture(w, h, frames[k])
+            b.add_texture(w, h, frames[k])
+            x, y = a.dispatch(), b.dispatch()
+            assert (x is None) == (y is None)
+            if x is not None:
+                assert np.array_equal(x, y)
+                outs.append(x)
+        name = f"compute_state_{idx:02d}.npz"
+        np.savez_compressed(os.path.join(HERE, name), frames=frames, outputs=np.stack(outs))
+        manifest["compute_state"].append({"file": name, "params": list(params)})
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    print(f"wrote {len(manifest['series'])} series + {len(manifest['compute_state'])} ComputeState fixtures")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,224 @@
+"""CPU tests of the oracle (test infrastructure): analytic known answers
+(SURVEY.md s8c), the C restatement against the independent numpy
+restatement, the committed golden fixtures, and the arithmetic identities
+the HIP kernels rely on."""
+import ctypes
+import itertools
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import np_restatement as nr
+from oracle import oracle
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_unorm_load_and_store_pins(oracle_lib):
+    for c in range(256):
+        u = oracle_lib.dips_oracle_u(c)
+        assert np.float32(u) == np.float32(c) / np.float32(255.0)
+        assert oracle_lib.dips_oracle_q(u) == c  # q(u(c)) round-trips
+    # ties round half to even (SURVEY.md s8 "Canonical definitions")
+    assert oracle_lib.dips_oracle_q(np.float32(20.5) / np.float32(255.0)) in (20,)
+    assert oracle_lib.dips_oracle_q(float("nan")) == 0
+    assert oracle_lib.dips_oracle_q(-1.0) == 0 and oracle_lib.dips_oracle_q(7.0) == 255
+
+
+def test_upper_median_known_answer(oracle_lib):
+    a = (ctypes.c_float * 4)(0.1, 0.4, 0.2, 0.3)
+    assert abs(oracle_lib.dips_oracle_upper_median4(a) - 0.3) < 1e-7
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        v = rng.random(4).astype(np.float32)
+        a = (ctypes.c_float * 4)(*v)
+        assert np.float32(oracle_lib.dips_oracle_upper_median4(a)) == np.sort(v)[2]
+
+
+def test_unorm_fma_identity():
+    """The HIP kernels compute u(c) = c/255 as fma(c, K_HI, c*K_LO)
+    (dips_amd/csrc/series_kernels.hip unorm2): exact for every byte."""
+    from fractions import Fraction
+    k_hi = np.float32(float.fromhex("0x1.010102p-8"))
+    k_lo = np.float32(float.fromhex("-0x1.fdfdfep-33"))
+
+    def round_f32(x: Fraction) -> np.float32:
+        cand = np.float32(float(x))
+        best = cand
+        for nb in (np.nextafter(cand, np.float32(-1)), np.nextafter(cand, np.float32(2))):
+            if abs(Fraction(float(nb)) - x) < abs(Fraction(float(best)) - x):
+                best = nb
+        return best
+
+    for c in range(256):
+        lo = np.float32(np.float32(c) * k_lo)
+        fma = round_f32(Fraction(c) * Fraction(float(k_hi)) + Fraction(float(lo)))
+        assert fma == nr.U_LUT[c], c
+
+
+def test_i2_pair_identity():
+    """I2 = u(max) + u(min) equals 2 * get_intensity exactly, and the f32
+    difference of I2 values is exactly twice the difference of I values."""
+    a = np.arange(256, dtype=np.int64)
+    mx, mn = np.meshgrid(a, a, indexing="ij")
+    keep = mx >= mn
+    mx, mn = mx[keep], mn[keep]
+    i2 = (nr.U_LUT[mx] + nr.U_LUT[mn]).astype(np.float32)
+    i = ((nr.U_LUT[mx] + nr.U_LUT[mn]).astype(np.float32) / np.float32(2.0)).astype(np.float32)
+    assert np.array_equal(i2, (i * np.float32(2.0)).astype(np.float32))
+    rng = np.random.default_rng(1)
+    p, q = rng.integers(0, i.size, 200000), rng.integers(0, i.size, 200000)
+    d2 = np.abs((i2[p] - i2[q]).astype(np.float32))
+    d1 = np.abs((i[p] - i[q]).astype(np.float32))
+    assert np.array_equal(d2, (d1 * np.float32(2.0)).astype(np.float32))
+    # every |dI| is a multiple of 2^-32: dI * 2^32 is an exact integer
+    assert np.all(np.ldexp(d1.astype(np.float64), 32) == np.floor(np.ldexp(d1.astype(np.float64), 32)))
+
+
+def test_exp_log_close_to_libm(oracle_lib):
+    xs = np.linspace(-30, 30, 20001).astype(np.float32)
+    got = np.array([oracle_lib.dips_oracle_expf(float(x)) for x in xs])
+    np.testing.assert_allclose(got, np.exp(xs.astype(np.float64)), rtol=5e-7)
+    ys = np.geomspace(1e-30, 1e30, 20001).astype(np.float32)
+    got = np.array([oracle_lib.dips_oracle_logf(float(y)) for y in ys])
+    np.testing.assert_allclose(got, np.log(ys.astype(np.float64)), rtol=5e-7, atol=1e-7)
+
+
+def test_exp_log_c_equals_numpy(oracle_lib):
+    rng = np.random.default_rng(2)
+    xs = np.concatenate([rng.uniform(-110, 95, 50000), rng.uniform(-3, 3, 50000),
+                         [0.0, -0.0, np.inf, -np.inf]]).astype(np.float32)
+    c = np.array([oracle_lib.dips_oracle_expf(float(x)) for x in xs], dtype=np.float32)
+    assert np.array_equal(c.view(np.uint32), nr.expf(xs).view(np.uint32))
+    ys = np.concatenate([rng.uniform(0, 4, 50000), 10.0 ** rng.uniform(-44, 38, 50000),
+                         [0.0, np.inf]]).astype(np.float32)
+    c = np.array([oracle_lib.dips_oracle_logf(float(y)) for y in ys], dtype=np.float32)
+    assert np.array_equal(c.view(np.uint32), nr.logf(ys).view(np.uint32))
+
+
+@pytest.mark.parametrize("c", [1, 3, 4])
+def test_synth_c_equals_numpy(c):
+    assert np.array_equal(oracle.synth(c, 37, 23, 5, 1000, 4), nr.synth(c, 37, 23, 5, 1000, 4))
+
+
+@pytest.mark.parametrize("c", [1, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_series_c_equals_numpy(c, mode):
+    for chroma, tau, seed in itertools.product([0, 1, 2, 3] if c != 1 else [0], [0.0, 8 / 255], [1, 2]):
+        frames = oracle.synth(c, 29, 17, seed, 0, 5)
+        ref = oracle.synth(c, 29, 17, seed + 100, 0, 1)[0]
+        for r in (None, ref):
+            a, sa, da = oracle.series(frames, mode=mode, chroma=chroma, tau=tau, ref=r, want_map=True)
+            b, sb, db = nr.series(frames, mode=mode, chroma=chroma, tau=tau, ref=r)
+            assert np.array_equal(a, b)
+            assert np.array_equal(da, db)
+            np.testing.assert_allclose(sa, sb, rtol=1e-12)
+            # the f64 sum agrees with the exact fixed-point sum
+            np.testing.assert_allclose(sa, np.ldexp(a[:, 3].astype(np.float64), -32), rtol=1e-12)
+
+
+def test_series_multithread_equals_single():
+    frames = oracle.synth(3, 40, 30, 9, 0, 13)
+    for mode in (0, 1):
+        a, sa, _ = oracle.series(frames, mode=mode, tau=1 / 255)
+        b, sb, _ = oracle.series(frames, mode=mode, tau=1 / 255, nthreads=4)
+        assert np.array_equal(a, b) and np.array_equal(sa, sb)
+
+
+def test_series_known_answers():
+    # identical frames: everything zero
+    f = np.repeat(oracle.synth(3, 16, 8, 1, 0, 1), 4, axis=0)
+    out4, si, dmap = oracle.series(f, mode=0, want_map=True)
+    assert not out4.any() and not si.any() and not dmap.any()
+    # single pixel black -> white: SJ = 510, SI = 1.0, SAD = 765
+    f = np.zeros((2, 8, 8, 3), np.uint8)
+    f[1, 3, 4] = 255
+    out4, si, _ = oracle.series(f)
+    assert out4[1].tolist() == [765, 510, 1, 1 << 32] and si[1] == 1.0
+
+
+def test_series_rejects_bad_args(oracle_lib):
+    f = np.zeros((1, 2, 2, 3), np.uint8)
+    with pytest.raises(ValueError):
+        oracle.series(f, tau=-1.0)
+    with pytest.raises(ValueError):
+        oracle.series(f, chroma=4)
+
+
+PARAMS = list(itertools.product([False, True], [1, 2, 3, 5, 11], [5.0, 0.7], [255, 0, 1], [0, 1, 3]))
+
+
+@pytest.mark.parametrize("colorize,window,sens,filt,chroma", PARAMS[::3])
+def test_compute_state_c_equals_numpy(colorize, window, sens, filt, chroma):
+    rng = np.random.default_rng(window * 7 + filt)
+    w, h = 19, 13
+    frames = rng.integers(0, 256, (8, h, w, 4), dtype=np.uint8)
+    frames[3] = frames[2]
+    a = oracle.ComputeState(colorize, window, sens, filt, chroma)
+    b = nr.ComputeState(colorize, window, sens, filt, chroma)
+    for k in range(8):
+        a.add_texture(w, h, frames[k])
+        b.add_texture(w, h, frames[k])
+        x, y = a.dispatch(), b.dispatch()
+        assert (x is None) == (y is None)
+        if x is not None:
+            assert np.array_equal(x, y)
+
+
+def test_compute_state_known_answers():
+    """Identical frames: 128 for gray pixels; odd max+min (10,20,31) gives
+    129 while unquantised slots decide the median (t = 3..5)."""
+    w = h = 8
+    f = np.zeros((h, w, 4), np.uint8)
+    f[..., 3] = 255
+    f[0, 0, :3] = (10, 20, 31)
+    f[0, 1, :3] = (100, 101, 102)
+    cs = oracle.ComputeState(False, 1, 5.0, 255, 0)
+    outs = []
+    for _ in range(8):
+        cs.add_texture(w, h, f)
+        outs.append(cs.dispatch())
+    assert outs[0] is None and outs[1] is None and outs[2] is None
+    assert [int(o[0, 0, 0]) for o in outs[3:]] == [129, 129, 129, 128, 128]
+    assert all(int(o[0, 1, 0]) == 128 and int(o[4, 4, 0]) == 128 for o in outs[3:])
+    # W = 3 spatial filter: the quirky median is always 0
+    cs3 = oracle.ComputeState(False, 3, 5.0, 255, 0)
+    for _ in range(4):
+        cs3.add_texture(w, h, f)
+    st = cs3.start_texture()
+    assert not st[..., :3].any()
+
+
+def _load_golden(name):
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def test_golden_manifest_and_fixtures():
+    """The committed fixtures (made by tests/golden/make_golden.py from the
+    numpy restatement, cross-checked there against the C oracle) still match
+    the oracle."""
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        manifest = json.load(f)
+    assert manifest["pins"]["bounds_policy"] == "naga Restrict (Vulkan/DX12)"
+    for case in manifest["series"]:
+        z = _load_golden(case["file"])
+        out4, si, dmap = oracle.series(z["frames"], mode=case["mode"], chroma=case["chroma"],
+                                       tau=case["tau"], ref=z["ref"] if "ref" in z else None,
+                                       want_map=True)
+        assert np.array_equal(out4, z["out4"]), case["file"]
+        assert np.array_equal(dmap, z["dmap"]), case["file"]
+        np.testing.assert_allclose(si, z["si"], rtol=1e-12)
+    for case in manifest["compute_state"]:
+        z = _load_golden(case["file"])
+        cs = oracle.ComputeState(*case["params"])
+        outs = z["outputs"]
+        for k, fr in enumerate(z["frames"]):
+            cs.add_texture(fr.shape[1], fr.shape[0], fr)
+            o = cs.dispatch()
+            if k < 3:
+                assert o is None
+            else:
+                assert np.array_equal(o, outs[k - 3]), (case["file"], k)
