@@ -70,20 +70,23 @@ def cpu_baseline(frames_dev, mode: int, tau: float, target_s: float):
         lib = oracle.load()
         build = "gcc -O3 -ffp-contract=off (prebuilt)"
     threads = max(1, min(16, os.cpu_count() or 1))
-    probe = frames_dev[:threads].cpu().numpy()
-    t = time.perf_counter()
-    oracle.series(probe, mode=mode, tau=tau, nthreads=threads, lib=lib)
-    per_round = time.perf_counter() - t  # `threads` frames in parallel
-    rounds = int(max(1, min(12, target_s / max(per_round, 1e-3))))
-    n = min(frames_dev.shape[0], threads * rounds)
+    # bounded host sample: 12 frames per thread (~3.6 GB at 4K RGB8), passed
+    # over repeatedly until about `target_s` of CPU work has been timed
+    n = min(frames_dev.shape[0], threads * 12)
     sample = frames_dev[:n].cpu().numpy()
+    passes = 0
     t = time.perf_counter()
-    oracle.series(sample, mode=mode, tau=tau, nthreads=threads, lib=lib)
-    dt = time.perf_counter() - t
-    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} frames of the same synthetic 4K RGB8 batch, series only "
-                      f"(oracle/dips_oracle.c, {build}, {threads} threads over frame ranges), "
-                      f"{dt:.2f} s"}
+    while True:
+        oracle.series(sample, mode=mode, tau=tau, nthreads=threads, lib=lib)
+        passes += 1
+        dt = time.perf_counter() - t
+        if dt >= target_s or passes >= 50:
+            break
+    n_done = n * passes
+    return {"value": round(n_done / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} frames of the same synthetic 4K RGB8 batch x {passes} passes, "
+                      f"series only (oracle/dips_oracle.c, {build}, {threads} threads over frame "
+                      f"ranges), {dt:.2f} s"}
 
 
 def main():
@@ -216,7 +219,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "series_fast_kernel<3,0,4,PF,false>",
+                "kernel": f"series_fast_kernel<3,0,4,2,{'true' if mode == Mode.PerFrame else 'false'},false>",
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "partial_bytes_per_launch": int(pbytes) * F,

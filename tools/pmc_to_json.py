@@ -1,0 +1,50 @@
+"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes of bench.py into the
+per-launch HBM traffic of the series kernel (profiles/pmc_traffic.json).
+
+gfx950 corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reads exactly
+half the bytes of a wide coalesced streaming read -> x2; WRITE_SIZE is exact
+for streaming stores.  Both are reported in KiB per dispatch."""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter):
+    vals = []
+    for f in glob.glob(os.path.join(d, counter, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "series_fast_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    d, frames, mode, out = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    fetch = per_dispatch(d, "FETCH_SIZE")
+    write = per_dispatch(d, "WRITE_SIZE")
+    if not fetch or not write:
+        raise SystemExit(f"no series_fast_kernel rows (fetch {len(fetch)}, write {len(write)})")
+    fk = sum(fetch) / len(fetch)
+    wk = sum(write) / len(write)
+    W, H, C = 3840, 2160, 3
+    algo = frames * W * H * C
+    res = {
+        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on bench.py, "
+                  "series_fast_kernel dispatches; FETCH_SIZE x2 (gfx950 wide-stream correction)",
+        "width": W, "height": H, "frames": frames, "mode": mode,
+        "fetch_kib_raw": fk, "write_kib": wk,
+        "read_bytes_per_launch": 2 * fk * 1024, "write_bytes_per_launch": wk * 1024,
+        "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
+        "algorithmic_bytes_per_launch": algo,
+        "traffic_over_algorithmic": (2 * fk * 1024 + wk * 1024) / algo,
+        "dispatches": [len(fetch), len(write)],
+    }
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
