@@ -58,7 +58,7 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(frames_dev, mode: int, tau: float, target_s: float):
+def cpu_baseline(frames_dev, series_dev, mode: int, tau: float, target_s: float):
     """The oracle ('port' of the reference semantics) timed on this host's
     cores on a bounded prefix of the same frames (per-frame cost is constant)."""
     from oracle import oracle
@@ -75,18 +75,23 @@ def cpu_baseline(frames_dev, mode: int, tau: float, target_s: float):
     n = min(frames_dev.shape[0], threads * 12)
     sample = frames_dev[:n].cpu().numpy()
     passes = 0
+    out4 = None
     t = time.perf_counter()
     while True:
-        oracle.series(sample, mode=mode, tau=tau, nthreads=threads, lib=lib)
+        out4, _, _ = oracle.series(sample, mode=mode, tau=tau, nthreads=threads, lib=lib)
         passes += 1
         dt = time.perf_counter() - t
         if dt >= target_s or passes >= 50:
             break
     n_done = n * passes
+    # the same sample doubles as a parity check of the timed GPU series
+    gpu = series_dev[:n].cpu().numpy().view(np.uint64)
+    matches = bool(np.array_equal(gpu, out4))
     return {"value": round(n_done / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"first {n} frames of the same synthetic 4K RGB8 batch x {passes} passes, "
                       f"series only (oracle/dips_oracle.c, {build}, {threads} threads over frame "
-                      f"ranges), {dt:.2f} s"}
+                      f"ranges), {dt:.2f} s",
+            "series_matches_gpu": matches}
 
 
 def main():
@@ -104,7 +109,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat, shard
 
     W, H, F = args.width, args.height, args.frames_per_gpu
     C = 3
@@ -120,31 +125,27 @@ def main():
     torch.cuda.synchronize()
     log(f"rank {rank}: {F} frames {W}x{H} RGB8 = {F * fb / 1e9:.1f} GB generated in HBM")
 
-    # Reference frame of the rank's first frame.
+    # Reference frame of the rank's first frame ('overall': broadcast once per
+    # job, the reference is fixed; 'per-frame': the halo frame, exchanged
+    # every step by dips_amd.shard.exchange_halo).
     if mode == Mode.Overall:
         if rank == 0:
             ref.copy_(frames[0])
-        if world > 1:
-            dist.broadcast(ref, src=0)   # once per job: the reference is fixed
-    gathered = torch.zeros((world * F, 4), dtype=torch.int64, device=dev) if rank == 0 else None
+        shard.broadcast_reference(ref, src=0)
+    gather = shard.SeriesGather(world * F, dev)
+
+    def compute(fr, r, out):
+        op.run_device(fr, out, ref=r)
 
     def step():
-        r = None
         if mode == Mode.Overall:
             r = ref
-        elif world > 1:
-            ops = []
-            if rank + 1 < world:
-                ops.append(dist.P2POp(dist.isend, frames[F - 1], rank + 1))
-            if rank > 0:
-                ops.append(dist.P2POp(dist.irecv, ref, rank - 1))
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
-            r = ref if rank > 0 else None
-        op.run_device(frames, series, ref=r)
-        if world > 1:
-            dist.gather(series, [gathered[k * F:(k + 1) * F] for k in range(world)] if rank == 0 else None, dst=0)
+        else:
+            r = shard.exchange_halo(frames, ref)
+        compute(frames, r, series)
+        return gather(series)
 
+    final = None
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -154,7 +155,7 @@ def main():
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        final = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -167,7 +168,7 @@ def main():
 
     if rank == 0:
         # validity: the gathered series must be the series of frames 0..N*F-1
-        final = (gathered if world > 1 else series).cpu().numpy().view(np.uint64)
+        final = final.cpu().numpy().view(np.uint64)
         assert final.shape == (world * F, 4)
         if mode == Mode.PerFrame:
             assert final[0].sum() == 0  # frame 0 against itself
@@ -189,7 +190,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(frames, int(mode), args.tau, args.cpu_seconds)
+                cpu = cpu_baseline(frames, series, int(mode), args.tau, args.cpu_seconds)
             except Exception as e:  # report, never hide
                 cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port",
                        "sample": f"failed: {e}"}

@@ -155,7 +155,11 @@ __device__ __forceinline__ void derive_px4(const uint32_t (&d)[Fmt<C>::NDW], Px4
             const u16x2 mx = __builtin_elementwise_max(__builtin_elementwise_max(r[k], g[k]), b[k]);
             const u16x2 mn = __builtin_elementwise_min(__builtin_elementwise_min(r[k], g[k]), b[k]);
             s.j[k] = as_u32(mx + mn);
+#ifdef DIPS_ABL_NOU
+            s.i2[k] = f32x2{__uint_as_float(as_u32(mx)), __uint_as_float(as_u32(mn))};
+#else
             s.i2[k] = unorm_pair(mx, lut) + unorm_pair(mn, lut);
+#endif
         } else {
             const u16x2 ch = CH == 1 ? r[k] : (CH == 2 ? g[k] : b[k]);
             s.j[k] = as_u32(ch + ch);
@@ -180,14 +184,30 @@ struct Acc {
     uint32_t sad, sj;  // per lane
     uint32_t cnt;      // wave-wide
     double si;         // per lane
+#ifdef DIPS_ABL_F32ACC
+    float sf;
+#endif
 };
 
 __device__ __forceinline__ void acc_intensity(Acc& acc, f32x2 cur, f32x2 ref, float thr) {
     const f32x2 d = cur - ref;
     const float a0 = fabsf(d.x), a1 = fabsf(d.y);
+#if defined(DIPS_ABL_NOTHR)
+    acc.si += (double)a0 + (double)a1;
+    (void)thr;
+#elif defined(DIPS_ABL_VCNT)
+    const bool s0 = a0 > thr, s1 = a1 > thr;
+    acc.cnt += (uint32_t)s0 + (uint32_t)s1;
+    acc.si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
+#elif defined(DIPS_ABL_F32ACC)
+    const bool s0 = a0 > thr, s1 = a1 > thr;
+    acc.cnt += (uint32_t)__builtin_popcountll(__ballot(s0)) + (uint32_t)__builtin_popcountll(__ballot(s1));
+    acc.sf += (s0 ? a0 : 0.0f) + (s1 ? a1 : 0.0f);
+#else
     const bool s0 = a0 > thr, s1 = a1 > thr;
     acc.cnt += (uint32_t)__builtin_popcountll(__ballot(s0)) + (uint32_t)__builtin_popcountll(__ballot(s1));
     acc.si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
+#endif
 }
 
 template <int C, int CH>
@@ -317,7 +337,11 @@ __device__ __forceinline__ void frame_accumulate(const SeriesArgs& a, const RefS
     acc.cnt = (threadIdx.x & 63u) == 0u ? acc.cnt : 0u;
     // exact per-lane fixed point, split so both halves sum in u32 over the
     // wave: H = whole units of 2^-16, L = the remainder in 2^-kScaleBits
+#ifdef DIPS_ABL_F32ACC
+    const double q = ((double)acc.sf + acc.si) * 65536.0;
+#else
     const double q = acc.si * 65536.0;
+#endif
     const uint32_t hfix = (uint32_t)q;  // trunc
     const int32_t lfix = (int32_t)((q - (double)hfix) * (double)(1ull << (kScaleBits - 16)));
     if constexpr (C == 1) {
@@ -432,7 +456,11 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 #pragma unroll
             for (int d = 0; d < D; d += 2) {
                 uint32_t v[8], sum[8];
+#ifdef DIPS_PF_INPLACE
+                frame_accumulate<C, CH, U, PF, MAP>(a, sa, sa, buf[d], voff, t + d, v, lut);
+#else
                 frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, buf[d], voff, t + d, v, lut);
+#endif
                 // keep the refill of buf[d] behind its last use: hoisting it
                 // would cost a register copy of the whole buffer
                 __builtin_amdgcn_sched_barrier(0);
@@ -442,8 +470,12 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 #pragma unroll
                     for (int u = 0; u < U; ++u) load_vec<C>(rn, voff[u], buf[d][u]);
                 }
+#ifdef DIPS_PF_INPLACE
+                frame_accumulate<C, CH, U, PF, MAP>(a, sa, sa, buf[d + 1], voff, t + d + 1, v + 4, lut);
+#else
                 if constexpr (PF) frame_accumulate<C, CH, U, PF, MAP>(a, sb, sa, buf[d + 1], voff, t + d + 1, v + 4, lut);
                 else frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, buf[d + 1], voff, t + d + 1, v + 4, lut);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
                 {
                     const uint32_t tl = min(t + (uint32_t)(d + 1 + D), tlast);
@@ -451,9 +483,18 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 #pragma unroll
                     for (int u = 0; u < U; ++u) load_vec<C>(rn, voff[u], buf[d + 1][u]);
                 }
+#ifdef DIPS_PROBE_NORED
+                // probe build only: no cross-lane reduction / record store
+                uint32_t keep = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) keep ^= v[k];
+                asm volatile("" ::"v"(keep));
+                (void)sum;
+#else
                 wave_sum8(v, sum, lane);
                 write_record<C>(rpart, t + d, lane, sum);
                 write_record<C>(rpart, t + d + 1, lane, sum + 4);
+#endif
             }
         }
         // Tail (< D frames): already in buf[0 .. tend - t - 1].  State parity
@@ -462,13 +503,160 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
         for (int d = 0; d < D - 1; ++d) {
             if (t + d < tend) {
                 uint32_t v[4], sum[4];
+#ifdef DIPS_PF_INPLACE
+                frame_accumulate<C, CH, U, PF, MAP>(a, sa, sa, buf[d], voff, t + d, v, lut);
+#else
                 if (PF && (d & 1)) frame_accumulate<C, CH, U, PF, MAP>(a, sb, sa, buf[d], voff, t + d, v, lut);
                 else frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, buf[d], voff, t + d, v, lut);
+#endif
                 wave_sum4(v, sum);
                 write_record<C>(rpart, t + d, lane, sum);
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// LDS-staged variant: the frame stream goes global -> LDS by buffer_load ...
+// lds (LDS-DMA, no VGPR destination), into a per-wave ring of DS frame slots;
+// the arithmetic reads its vecs back with ds_read_b32 (stride 12 B across
+// lanes: conflict free).  No loop-carried frame buffers in VGPRs, so the
+// ring can be deeper and the register allocator has no buffers to shuffle.
+// Ordering: LDS-DMA completion is tracked only by the issuing wave's vmcnt,
+// so every slot read is preceded by an explicit s_waitcnt vmcnt(U*(DS-1))
+// (exactly U DMA ops per frame are issued in order; younger record stores
+// only make the wait more conservative), and every slot refill by
+// s_waitcnt lgkmcnt(0) (the slot's ds_reads have returned).
+// ---------------------------------------------------------------------------
+template <int C, int U, int DS>
+struct LdsRing {
+    static constexpr uint32_t kTile = 64u * U * Fmt<C>::VB;      // bytes per wave per frame
+    static constexpr uint32_t kWaveBytes = kTile * DS;
+    static constexpr uint32_t kBlockBytes = 4u * kWaveBytes;      // 4 waves per workgroup
+};
+
+// (device pass only: address_space(3) pointers and the LDS-DMA builtin do
+// not exist for the host target)
+#if defined(__HIP_DEVICE_COMPILE__)
+template <int C, int U>
+__device__ __forceinline__ void dma_frame(__amdgpu_buffer_rsrc_t r, uint8_t __attribute__((address_space(3)))* slot,
+                                          const uint32_t (&voff)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        auto* dst = slot + (uint32_t)u * 64u * Fmt<C>::VB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (void __attribute__((address_space(3)))*)dst, Fmt<C>::VB, voff[u],
+                                                 0, 0, kAuxNT);
+    }
+}
+
+template <int C, int U>
+__device__ __forceinline__ void read_frame(const uint8_t __attribute__((address_space(3)))* slot, uint32_t lane,
+                                           uint32_t (&cur)[U][Fmt<C>::NDW]) {
+    const uint32_t __attribute__((address_space(3)))* w = (const uint32_t __attribute__((address_space(3)))*)slot;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < Fmt<C>::NDW; ++k) cur[u][k] = w[(u * 64 + lane) * Fmt<C>::NDW + k];
+}
+
+#endif  // __HIP_DEVICE_COMPILE__
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int C, int CH, int U, int DS, bool PF, bool MAP>
+__global__ __launch_bounds__(256) void series_lds_kernel(SeriesArgs a) {
+    using F = Fmt<C>;
+    using R = LdsRing<C, U, DS>;
+    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[R::kBlockBytes];
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (wave >= a.n_waves) return;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t __attribute__((address_space(3)))* ring =
+        (uint8_t __attribute__((address_space(3)))*)ring_mem + wid * R::kWaveBytes;
+    const uint32_t fb = a.frame_bytes;
+    const Lut lut{nullptr, lane & 31u};
+
+    uint64_t i = (uint64_t)wave * a.items / a.n_waves;
+    const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
+    while (i < iend) {
+        const uint32_t tile = (uint32_t)(i / a.n_frames);
+        uint32_t t = (uint32_t)(i - (uint64_t)tile * a.n_frames);
+        const uint64_t remaining = iend - i;
+        const uint32_t tend = (uint32_t)((uint64_t)a.n_frames < t + remaining ? (uint64_t)a.n_frames : t + remaining);
+        i += tend - t;
+
+        uint32_t voff[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) voff[u] = ((tile * U + u) * 64u + lane) * (uint32_t)F::VB;
+
+        const uint8_t* rp = PF ? (t == 0 ? a.ref0 : a.frames + (uint64_t)(t - 1) * fb) : a.ref0;
+        RefState<C> sa[U], sb[U];
+        {
+            const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, fb);
+            uint32_t d[U][F::NDW];
+#pragma unroll
+            for (int u = 0; u < U; ++u) load_vec<C>(rr, voff[u], d[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) derive_ref<C, CH>(d[u], sa[u], lut);
+        }
+        const __amdgpu_buffer_rsrc_t rpart = make_rsrc(a.partials + 2 * (uint64_t)tile * a.n_frames, a.n_frames * 16u);
+        const uint32_t tlast = tend - 1;
+        const uint32_t tseg = t;
+
+        // all previous reads of this wave's ring are complete before refilling it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int d = 0; d < DS; ++d) {
+            const uint32_t tl = min(t + (uint32_t)d, tlast);
+            dma_frame<C, U>(make_rsrc(a.frames + (uint64_t)tl * fb, fb), ring + d * R::kTile, voff);
+        }
+        // frame f lives in slot (f - tseg) % DS
+        for (; t + 2 <= tend; t += 2) {
+            uint32_t v[8], sum[8];
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+                const uint32_t tf = t + d;
+                uint8_t __attribute__((address_space(3)))* slot = ring + ((tf - tseg) % DS) * R::kTile;
+                uint32_t cur[U][F::NDW];
+                wait_vmcnt<U * (DS - 1)>();
+                read_frame<C, U>(slot, lane, cur);
+#ifdef DIPS_PF_INPLACE
+                frame_accumulate<C, CH, U, PF, MAP>(a, sa, sa, cur, voff, tf, v + 4 * d, lut);
+#else
+                if (PF && d == 1) frame_accumulate<C, CH, U, PF, MAP>(a, sb, sa, cur, voff, tf, v + 4 * d, lut);
+                else frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, cur, voff, tf, v + 4 * d, lut);
+#endif
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const uint32_t tl = min(tf + (uint32_t)DS, tlast);
+                dma_frame<C, U>(make_rsrc(a.frames + (uint64_t)tl * fb, fb), slot, voff);
+            }
+            wave_sum8(v, sum, lane);
+            write_record<C>(rpart, t, lane, sum);
+            write_record<C>(rpart, t + 1, lane, sum + 4);
+        }
+        if (t < tend) {  // one frame left
+            uint32_t v[4], sum[4];
+            uint8_t __attribute__((address_space(3)))* slot = ring + ((t - tseg) % DS) * R::kTile;
+            uint32_t cur[U][F::NDW];
+            wait_vmcnt<0>();
+            read_frame<C, U>(slot, lane, cur);
+            frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, cur, voff, t, v, lut);
+            wave_sum4(v, sum);
+            write_record<C>(rpart, t, lane, sum);
+        }
+        // drain this segment's clamped DMA refills before the ring is reused
+        wait_vmcnt<0>();
+    }
+#else
+    (void)a;
+    (void)ring_mem;
+#endif
 }
 
 // Sum the 16-byte partial records of `tiles_per_thread` tiles for one frame

@@ -161,6 +161,21 @@ int main(int argc, char** argv) {
     }
     SERIES(4, 2, true)
     SERIES(4, 2, false)
+#define SLDS(U, D, PF)                                                                                \
+    {                                                                                                 \
+        SeriesArgs a; uint32_t blocks; int occ;                                                       \
+        const void* k = (const void*)&series_lds_kernel<3, 0, U, D, PF, false>;                       \
+        geom(12, U, k, a, blocks, occ);                                                               \
+        a.partials = partials;                                                                        \
+        vs.push_back({"lds<U=" #U ",D=" #D ",PF=" #PF "> occ=" + std::to_string(occ) + " waves=" +     \
+                          std::to_string(a.n_waves),                                                  \
+                      [=]() { hipLaunchKernelGGL((series_lds_kernel<3, 0, U, D, PF, false>), dim3(blocks), dim3(256), 0, 0, a); }, {}}); \
+    }
+    SLDS(4, 2, true)
+    SLDS(4, 3, true)
+    SLDS(4, 4, true)
+    SLDS(2, 4, true)
+    SLDS(4, 3, false)
 SERIES(4, 4, true)
     SERIES(2, 2, true)
     SERIES(2, 4, true)
