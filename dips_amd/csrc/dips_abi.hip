@@ -235,7 +235,7 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         a.n_frames = n_frames;
         a.n_tiles = (uint32_t)g.n_tiles;
         a.n_waves = (uint32_t)g.n_waves;
-        a.thr = C == 1 ? h->p.tau : 2.0f * h->p.tau;
+        a.thr = dips::series_threshold(C, h->p.tau);
         DIPS_HIP(h, dips::launch_series_fast(a, C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map != nullptr,
                                              (uint32_t)g.blocks, s));
     } else {
@@ -260,7 +260,8 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         DIPS_HIP(h, hipEventRecord(e1, s));
         h->ev_pending.emplace_back(e0, e1);
     }
-    if (g.ok) DIPS_HIP(h, dips::launch_series_reduce(h->partials.as<uint64_t>(), n_frames, (uint32_t)g.n_tiles, series, s));
+    if (g.ok)
+        DIPS_HIP(h, dips::launch_series_reduce(h->partials.as<uint64_t>(), n_frames, (uint32_t)g.n_tiles, C == 1, series, s));
     return DIPS_OK;
 }
 

@@ -11,6 +11,7 @@ namespace dips {
 // Unroll (vecs per lane) of the fast series kernel; a tile = 64 * U vecs.
 constexpr int kUnrollRGB = 4;   // 1024 px / wave / frame for RGB8 and RGBA8
 constexpr int kUnrollGray = 2;  // 2048 px / wave / frame for GRAY8
+constexpr int kUnrollV2 = 2;    // series_v2_kernel (RGB8/RGBA8): 512 px / wave / frame
 // Prefetch depth: frames of loads each wave keeps in flight.
 #ifndef DIPS_DEPTH_RGB
 #define DIPS_DEPTH_RGB 2
@@ -31,7 +32,7 @@ struct SeriesArgs {
     uint32_t n_frames;
     uint32_t n_tiles;
     uint32_t n_waves;
-    float thr;               // threshold in kernel units (2*tau for RGB(A), tau for gray)
+    float thr;               // threshold in kernel units: series_threshold()
 };
 
 struct GenericArgs {
@@ -77,9 +78,12 @@ struct CompatArgs {
 int pixels_per_vec(int channels);
 int fast_unroll(int channels);
 const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map);
+const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool map);
+// threshold argument (SeriesArgs::thr) of the kernel series_fast_kernel_ptr picks
+float series_threshold(int channels, float tau);
 hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, bool per_frame, bool map,
                               uint32_t blocks, hipStream_t s);
-hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles,
+hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, bool gray,
                                 dips_series_entry* series, hipStream_t s);
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);

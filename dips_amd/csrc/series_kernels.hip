@@ -20,90 +20,9 @@
 //  * per (tile, frame) the wave reduces in registers/DPP and lane 0 writes one
 //    16-byte partial record; series_reduce sums the records per frame with
 //    64-bit integer atomics (order-independent, hence bit-reproducible).
-#include "dips_math.h"
-#include "dips_kernels.h"
+#include "series_common.h"
 
 namespace dips {
-
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// gfx950 buffer-resource flags word (raw buffer, 32-bit format).
-constexpr int kRsrcFlags = 0x00020000;
-// cache policy of the streamed frame loads: nt (stream once).
-constexpr int kAuxNT = 2;
-
-template <int C> struct Fmt;
-template <> struct Fmt<3> { static constexpr int NDW = 3, PPV = 4, VB = 12; };
-template <> struct Fmt<4> { static constexpr int NDW = 4, PPV = 4, VB = 16; };
-template <> struct Fmt<1> { static constexpr int NDW = 4, PPV = 16, VB = 16; };
-
-// Buffer descriptor of a wave-uniform byte range.  The inputs go through
-// readfirstlane so the compiler can PROVE the descriptor uniform; otherwise
-// it wraps every buffer op in a waterfall loop (cdna_hip_programming.md T20).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
-    const uint64_t a = (uint64_t)(uintptr_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    void* base = (void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
-    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), kRsrcFlags);
-}
-
-template <int C>
-__device__ __forceinline__ void load_vec(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t (&v)[Fmt<C>::NDW]) {
-    if constexpr (Fmt<C>::NDW == 3) {
-        const u32x3 x = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, kAuxNT);
-        v[0] = x.x; v[1] = x.y; v[2] = x.z;
-    } else {
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxNT);
-        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-    }
-}
-
-template <int C>
-__device__ __forceinline__ void store_vec(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint32_t (&v)[Fmt<C>::NDW]) {
-    if constexpr (Fmt<C>::NDW == 3) {
-        u32x3 x; x.x = v[0]; x.y = v[1]; x.z = v[2];
-        __builtin_amdgcn_raw_buffer_store_b96(x, r, off, 0, kAuxNT);
-    } else {
-        u32x4 x; x.x = v[0]; x.y = v[1]; x.z = v[2]; x.w = v[3];
-        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, kAuxNT);
-    }
-}
-
-__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
-__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
-
-// |a - b| per byte of two packed dwords.
-__device__ __forceinline__ uint32_t absdiff_bytes(uint32_t a, uint32_t b) {
-    const u16x2 ae = as_u16x2(a & 0x00FF00FFu), be = as_u16x2(b & 0x00FF00FFu);
-    const u16x2 ao = as_u16x2((a >> 8) & 0x00FF00FFu), bo = as_u16x2((b >> 8) & 0x00FF00FFu);
-    const u16x2 de = __builtin_elementwise_max(ae, be) - __builtin_elementwise_min(ae, be);
-    const u16x2 dd = __builtin_elementwise_max(ao, bo) - __builtin_elementwise_min(ao, bo);
-    return as_u32(de) | (as_u32(dd) << 8);
-}
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// Exact rgba8unorm load without a division or a table: u(c) = c / 255
-// correctly rounded equals fma(c, K_HI, c * K_LO) for every byte c, with
-// K_HI + K_LO the double-float split of 1/255 (checked exhaustively in
-// tests/test_oracle.py::test_unorm_fma_identity).  Two values per packed op.
-constexpr float kUnormHi = 0x1.010102p-8f;
-constexpr float kUnormLo = -0x1.fdfdfep-33f;
-
-__device__ __forceinline__ f32x2 unorm2(f32x2 c) {
-    const f32x2 hi = {kUnormHi, kUnormHi};
-    const f32x2 lo = {kUnormLo, kUnormLo};
-    return __builtin_elementwise_fma(c, hi, c * lo);
-}
-
-__device__ __forceinline__ f32x2 u16x2_to_f32x2(u16x2 v) {
-    // byte values in the low byte of each half: v_cvt_f32_ubyte0 / ubyte2
-    const uint32_t w = as_u32(v);
-    return f32x2{(float)(w & 0xFFu), (float)((w >> 16) & 0xFFu)};
-}
 
 // Derived state of 4 RGB(A) pixels: J = max+min as two u16 pairs and the
 // doubled intensity I2 = u(max) + u(min) (= 2 * get_intensity, exact), as
@@ -112,29 +31,6 @@ struct Px4 {
     uint32_t j[2];
     f32x2 i2[2];
 };
-
-// Pair planes (two pixels per dword, one byte per u16 half) of one vec.
-template <int C>
-__device__ __forceinline__ void pair_planes(const uint32_t (&d)[Fmt<C>::NDW], u16x2 (&r)[2], u16x2 (&g)[2],
-                                            u16x2 (&b)[2]) {
-    if constexpr (C == 3) {
-        // d0 = r0 g0 b0 r1 | d1 = g1 b1 r2 g2 | d2 = b2 r3 g3 b3 (byte 0 first)
-        r[0] = as_u16x2(__builtin_amdgcn_perm(d[0], d[0], 0x0C030C00u));
-        g[0] = as_u16x2(__builtin_amdgcn_perm(d[1], d[0], 0x0C040C01u));
-        b[0] = as_u16x2(__builtin_amdgcn_perm(d[1], d[0], 0x0C050C02u));
-        r[1] = as_u16x2(__builtin_amdgcn_perm(d[2], d[1], 0x0C050C02u));
-        g[1] = as_u16x2(__builtin_amdgcn_perm(d[2], d[1], 0x0C060C03u));
-        b[1] = as_u16x2(__builtin_amdgcn_perm(d[2], d[2], 0x0C030C00u));
-    } else {
-        // d_k = r g b a
-        r[0] = as_u16x2(__builtin_amdgcn_perm(d[1], d[0], 0x0C040C00u));
-        g[0] = as_u16x2(__builtin_amdgcn_perm(d[1], d[0], 0x0C050C01u));
-        b[0] = as_u16x2(__builtin_amdgcn_perm(d[1], d[0], 0x0C060C02u));
-        r[1] = as_u16x2(__builtin_amdgcn_perm(d[3], d[2], 0x0C040C00u));
-        g[1] = as_u16x2(__builtin_amdgcn_perm(d[3], d[2], 0x0C050C01u));
-        b[1] = as_u16x2(__builtin_amdgcn_perm(d[3], d[2], 0x0C060C02u));
-    }
-}
 
 // Placeholder kept in the signatures of the per-vec helpers; the exact
 // arithmetic u() needs no table (an LDS table measured slower on gfx950).
@@ -155,11 +51,7 @@ __device__ __forceinline__ void derive_px4(const uint32_t (&d)[Fmt<C>::NDW], Px4
             const u16x2 mx = __builtin_elementwise_max(__builtin_elementwise_max(r[k], g[k]), b[k]);
             const u16x2 mn = __builtin_elementwise_min(__builtin_elementwise_min(r[k], g[k]), b[k]);
             s.j[k] = as_u32(mx + mn);
-#ifdef DIPS_ABL_NOU
-            s.i2[k] = f32x2{__uint_as_float(as_u32(mx)), __uint_as_float(as_u32(mn))};
-#else
             s.i2[k] = unorm_pair(mx, lut) + unorm_pair(mn, lut);
-#endif
         } else {
             const u16x2 ch = CH == 1 ? r[k] : (CH == 2 ? g[k] : b[k]);
             s.j[k] = as_u32(ch + ch);
@@ -184,30 +76,14 @@ struct Acc {
     uint32_t sad, sj;  // per lane
     uint32_t cnt;      // wave-wide
     double si;         // per lane
-#ifdef DIPS_ABL_F32ACC
-    float sf;
-#endif
 };
 
 __device__ __forceinline__ void acc_intensity(Acc& acc, f32x2 cur, f32x2 ref, float thr) {
     const f32x2 d = cur - ref;
     const float a0 = fabsf(d.x), a1 = fabsf(d.y);
-#if defined(DIPS_ABL_NOTHR)
-    acc.si += (double)a0 + (double)a1;
-    (void)thr;
-#elif defined(DIPS_ABL_VCNT)
-    const bool s0 = a0 > thr, s1 = a1 > thr;
-    acc.cnt += (uint32_t)s0 + (uint32_t)s1;
-    acc.si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
-#elif defined(DIPS_ABL_F32ACC)
-    const bool s0 = a0 > thr, s1 = a1 > thr;
-    acc.cnt += (uint32_t)__builtin_popcountll(__ballot(s0)) + (uint32_t)__builtin_popcountll(__ballot(s1));
-    acc.sf += (s0 ? a0 : 0.0f) + (s1 ? a1 : 0.0f);
-#else
     const bool s0 = a0 > thr, s1 = a1 > thr;
     acc.cnt += (uint32_t)__builtin_popcountll(__ballot(s0)) + (uint32_t)__builtin_popcountll(__ballot(s1));
     acc.si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
-#endif
 }
 
 template <int C, int CH>
@@ -259,60 +135,6 @@ __device__ __forceinline__ void process_vec(const RefState<C>& ref, RefState<C>&
     }
 }
 
-// ---------------------------------------------------------------------------
-// Cross-lane reduction of several per-lane values at once, no LDS.
-// N = 4 or 8 values.  The first steps exchange HALF of the values with the
-// partner lane (xor 32 by v_permlane32_swap, xor 16 by v_permlane16_swap,
-// xor 8 by DPP row_ror:8 when N = 8), so each lane ends up owning one value
-// index; the remaining steps are plain DPP butterflies inside 8-lane groups.
-// Value v's wave sum then sits in lane 8v (N = 8) or 16v (N = 4).  Compared
-// with N separate butterflies this is ~1/3 of the instructions and the N
-// chains overlap instead of running back to back.
-// ---------------------------------------------------------------------------
-#define DIPS_DPP(v, ctrl) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), 0xF, 0xF, false))
-
-__device__ __forceinline__ uint32_t swap32_sum(uint32_t a, uint32_t b) {
-    const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-    return r[0] + r[1];
-}
-
-__device__ __forceinline__ uint32_t swap16_sum(uint32_t a, uint32_t b) {
-    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
-    return r[0] + r[1];
-}
-
-__device__ __forceinline__ uint32_t group8_sum(uint32_t y) {
-    y += DIPS_DPP(y, 0xB1);   // quad_perm [1,0,3,2]  (xor 1)
-    y += DIPS_DPP(y, 0x4E);   // quad_perm [2,3,0,1]  (xor 2)
-    y += DIPS_DPP(y, 0x141);  // row_half_mirror      (xor 7 inside 8 lanes)
-    return y;
-}
-
-// out[v] = sum over the 64 lanes of in[v] (wave-uniform results).
-__device__ __forceinline__ void wave_sum8(const uint32_t (&in)[8], uint32_t (&out)[8], uint32_t lane) {
-    uint32_t w[4], x[2];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = swap32_sum(in[k], in[4 + k]);  // lane owns 4*b5 + k
-    x[0] = swap16_sum(w[0], w[2]);                                     // owns 4*b5 + 2*b4 + 0
-    x[1] = swap16_sum(w[1], w[3]);                                     // owns 4*b5 + 2*b4 + 1
-    const bool b3 = (lane & 8u) != 0;
-    const uint32_t keep = b3 ? x[1] : x[0];
-    const uint32_t send = b3 ? x[0] : x[1];
-    const uint32_t y = group8_sum(keep + DIPS_DPP(send, 0x128));      // row_ror:8 (xor 8)
-#pragma unroll
-    for (int v = 0; v < 8; ++v) out[v] = (uint32_t)__builtin_amdgcn_readlane((int)y, 8 * v);
-}
-
-__device__ __forceinline__ void wave_sum4(const uint32_t (&in)[4], uint32_t (&out)[4]) {
-    const uint32_t w0 = swap32_sum(in[0], in[2]);  // lane owns 2*b5 + 0
-    const uint32_t w1 = swap32_sum(in[1], in[3]);  // lane owns 2*b5 + 1
-    uint32_t y = swap16_sum(w0, w1);               // owns 2*b5 + b4
-    y += DIPS_DPP(y, 0x128);                       // row_ror:8 (xor 8)
-    y = group8_sum(y);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) out[v] = (uint32_t)__builtin_amdgcn_readlane((int)y, 16 * v);
-}
-
 // Accumulate one frame of one tile into four per-lane reduction values
 //   RGB(A): {SAD, SJ + count << 20, H, L};  gray: {SAD + count << 20, H, L, 0}
 // (H, L: the exact fixed-point split of the intensity sum, see Acc).  The
@@ -337,11 +159,7 @@ __device__ __forceinline__ void frame_accumulate(const SeriesArgs& a, const RefS
     acc.cnt = (threadIdx.x & 63u) == 0u ? acc.cnt : 0u;
     // exact per-lane fixed point, split so both halves sum in u32 over the
     // wave: H = whole units of 2^-16, L = the remainder in 2^-kScaleBits
-#ifdef DIPS_ABL_F32ACC
-    const double q = ((double)acc.sf + acc.si) * 65536.0;
-#else
     const double q = acc.si * 65536.0;
-#endif
     const uint32_t hfix = (uint32_t)q;  // trunc
     const int32_t lfix = (int32_t)((q - (double)hfix) * (double)(1ull << (kScaleBits - 16)));
     if constexpr (C == 1) {
@@ -357,35 +175,18 @@ __device__ __forceinline__ void frame_accumulate(const SeriesArgs& a, const RefS
     }
 }
 
-// Partial record of one (tile, frame) from the four wave sums; written by
-// lane 0 only, branch free: the other lanes' offsets fall outside the
-// descriptor's range and the hardware drops them.
+// Partial record of one (tile, frame): the four raw wave sums (decoded by
+// series_reduce_kernel, see decode_record); written by lane 0 only, branch
+// free: the other lanes' offsets fall outside the descriptor's range and the
+// hardware drops them.
 template <int C>
 __device__ __forceinline__ void write_record(__amdgpu_buffer_rsrc_t rpart, uint32_t t, uint32_t lane,
                                              const uint32_t* s) {
-    constexpr int kScaleBits = (C == 1) ? 32 : 31;
-    uint32_t sad, sj, cnt, hsum;
-    int32_t lsum;
-    if constexpr (C == 1) {
-        sad = s[0] & 0xFFFFFu;
-        cnt = s[0] >> 20;
-        sj = 2u * sad;
-        hsum = s[1];
-        lsum = (int32_t)s[2];
-    } else {
-        sad = s[0];
-        sj = s[1] & 0xFFFFFu;
-        cnt = s[1] >> 20;
-        hsum = s[2];
-        lsum = (int32_t)s[3];
-    }
-    const uint64_t sif = ((uint64_t)hsum << (kScaleBits - 16)) + (uint64_t)(int64_t)lsum;
-    const uint64_t hi = sif | ((uint64_t)cnt << 48);
     u32x4 rec;
-    rec.x = sad;
-    rec.y = sj;
-    rec.z = (uint32_t)hi;
-    rec.w = (uint32_t)(hi >> 32);
+    rec.x = s[0];
+    rec.y = s[1];
+    rec.z = s[2];
+    rec.w = s[3];
     __builtin_amdgcn_raw_buffer_store_b128(rec, rpart, lane == 0 ? t * 16u : 0x80000000u, 0, 0);
 }
 
@@ -456,11 +257,7 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 #pragma unroll
             for (int d = 0; d < D; d += 2) {
                 uint32_t v[8], sum[8];
-#ifdef DIPS_PF_INPLACE
-                frame_accumulate<C, CH, U, PF, MAP>(a, sa, sa, buf[d], voff, t + d, v, lut);
-#else
                 frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, buf[d], voff, t + d, v, lut);
-#endif
                 // keep the refill of buf[d] behind its last use: hoisting it
                 // would cost a register copy of the whole buffer
                 __builtin_amdgcn_sched_barrier(0);
@@ -470,12 +267,8 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 #pragma unroll
                     for (int u = 0; u < U; ++u) load_vec<C>(rn, voff[u], buf[d][u]);
                 }
-#ifdef DIPS_PF_INPLACE
-                frame_accumulate<C, CH, U, PF, MAP>(a, sa, sa, buf[d + 1], voff, t + d + 1, v + 4, lut);
-#else
                 if constexpr (PF) frame_accumulate<C, CH, U, PF, MAP>(a, sb, sa, buf[d + 1], voff, t + d + 1, v + 4, lut);
                 else frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, buf[d + 1], voff, t + d + 1, v + 4, lut);
-#endif
                 __builtin_amdgcn_sched_barrier(0);
                 {
                     const uint32_t tl = min(t + (uint32_t)(d + 1 + D), tlast);
@@ -483,18 +276,9 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 #pragma unroll
                     for (int u = 0; u < U; ++u) load_vec<C>(rn, voff[u], buf[d + 1][u]);
                 }
-#ifdef DIPS_PROBE_NORED
-                // probe build only: no cross-lane reduction / record store
-                uint32_t keep = 0;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) keep ^= v[k];
-                asm volatile("" ::"v"(keep));
-                (void)sum;
-#else
                 wave_sum8(v, sum, lane);
                 write_record<C>(rpart, t + d, lane, sum);
                 write_record<C>(rpart, t + d + 1, lane, sum + 4);
-#endif
             }
         }
         // Tail (< D frames): already in buf[0 .. tend - t - 1].  State parity
@@ -503,12 +287,8 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
         for (int d = 0; d < D - 1; ++d) {
             if (t + d < tend) {
                 uint32_t v[4], sum[4];
-#ifdef DIPS_PF_INPLACE
-                frame_accumulate<C, CH, U, PF, MAP>(a, sa, sa, buf[d], voff, t + d, v, lut);
-#else
                 if (PF && (d & 1)) frame_accumulate<C, CH, U, PF, MAP>(a, sb, sa, buf[d], voff, t + d, v, lut);
                 else frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, buf[d], voff, t + d, v, lut);
-#endif
                 wave_sum4(v, sum);
                 write_record<C>(rpart, t + d, lane, sum);
             }
@@ -516,167 +296,38 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
     }
 }
 
-// ---------------------------------------------------------------------------
-// LDS-staged variant: the frame stream goes global -> LDS by buffer_load ...
-// lds (LDS-DMA, no VGPR destination), into a per-wave ring of DS frame slots;
-// the arithmetic reads its vecs back with ds_read_b32 (stride 12 B across
-// lanes: conflict free).  No loop-carried frame buffers in VGPRs, so the
-// ring can be deeper and the register allocator has no buffers to shuffle.
-// Ordering: LDS-DMA completion is tracked only by the issuing wave's vmcnt,
-// so every slot read is preceded by an explicit s_waitcnt vmcnt(U*(DS-1))
-// (exactly U DMA ops per frame are issued in order; younger record stores
-// only make the wait more conservative), and every slot refill by
-// s_waitcnt lgkmcnt(0) (the slot's ds_reads have returned).
-// ---------------------------------------------------------------------------
-template <int C, int U, int DS>
-struct LdsRing {
-    static constexpr uint32_t kTile = 64u * U * Fmt<C>::VB;      // bytes per wave per frame
-    static constexpr uint32_t kWaveBytes = kTile * DS;
-    static constexpr uint32_t kBlockBytes = 4u * kWaveBytes;      // 4 waves per workgroup
-};
-
-// (device pass only: address_space(3) pointers and the LDS-DMA builtin do
-// not exist for the host target)
-#if defined(__HIP_DEVICE_COMPILE__)
-template <int C, int U>
-__device__ __forceinline__ void dma_frame(__amdgpu_buffer_rsrc_t r, uint8_t __attribute__((address_space(3)))* slot,
-                                          const uint32_t (&voff)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        auto* dst = slot + (uint32_t)u * 64u * Fmt<C>::VB;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (void __attribute__((address_space(3)))*)dst, Fmt<C>::VB, voff[u],
-                                                 0, 0, kAuxNT);
-    }
-}
-
-template <int C, int U>
-__device__ __forceinline__ void read_frame(const uint8_t __attribute__((address_space(3)))* slot, uint32_t lane,
-                                           uint32_t (&cur)[U][Fmt<C>::NDW]) {
-    const uint32_t __attribute__((address_space(3)))* w = (const uint32_t __attribute__((address_space(3)))*)slot;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int k = 0; k < Fmt<C>::NDW; ++k) cur[u][k] = w[(u * 64 + lane) * Fmt<C>::NDW + k];
-}
-
-#endif  // __HIP_DEVICE_COMPILE__
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(N >= 0 && N < 64, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int C, int CH, int U, int DS, bool PF, bool MAP>
-__global__ __launch_bounds__(256) void series_lds_kernel(SeriesArgs a) {
-    using F = Fmt<C>;
-    using R = LdsRing<C, U, DS>;
-    __shared__ __attribute__((aligned(16))) uint8_t ring_mem[R::kBlockBytes];
-#if defined(__HIP_DEVICE_COMPILE__)
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-    if (wave >= a.n_waves) return;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    uint8_t __attribute__((address_space(3)))* ring =
-        (uint8_t __attribute__((address_space(3)))*)ring_mem + wid * R::kWaveBytes;
-    const uint32_t fb = a.frame_bytes;
-    const Lut lut{nullptr, lane & 31u};
-
-    uint64_t i = (uint64_t)wave * a.items / a.n_waves;
-    const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
-    while (i < iend) {
-        const uint32_t tile = (uint32_t)(i / a.n_frames);
-        uint32_t t = (uint32_t)(i - (uint64_t)tile * a.n_frames);
-        const uint64_t remaining = iend - i;
-        const uint32_t tend = (uint32_t)((uint64_t)a.n_frames < t + remaining ? (uint64_t)a.n_frames : t + remaining);
-        i += tend - t;
-
-        uint32_t voff[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) voff[u] = ((tile * U + u) * 64u + lane) * (uint32_t)F::VB;
-
-        const uint8_t* rp = PF ? (t == 0 ? a.ref0 : a.frames + (uint64_t)(t - 1) * fb) : a.ref0;
-        RefState<C> sa[U], sb[U];
-        {
-            const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, fb);
-            uint32_t d[U][F::NDW];
-#pragma unroll
-            for (int u = 0; u < U; ++u) load_vec<C>(rr, voff[u], d[u]);
-#pragma unroll
-            for (int u = 0; u < U; ++u) derive_ref<C, CH>(d[u], sa[u], lut);
-        }
-        const __amdgpu_buffer_rsrc_t rpart = make_rsrc(a.partials + 2 * (uint64_t)tile * a.n_frames, a.n_frames * 16u);
-        const uint32_t tlast = tend - 1;
-        const uint32_t tseg = t;
-
-        // all previous reads of this wave's ring are complete before refilling it
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int d = 0; d < DS; ++d) {
-            const uint32_t tl = min(t + (uint32_t)d, tlast);
-            dma_frame<C, U>(make_rsrc(a.frames + (uint64_t)tl * fb, fb), ring + d * R::kTile, voff);
-        }
-        // frame f lives in slot (f - tseg) % DS
-        for (; t + 2 <= tend; t += 2) {
-            uint32_t v[8], sum[8];
-#pragma unroll
-            for (int d = 0; d < 2; ++d) {
-                const uint32_t tf = t + d;
-                uint8_t __attribute__((address_space(3)))* slot = ring + ((tf - tseg) % DS) * R::kTile;
-                uint32_t cur[U][F::NDW];
-                wait_vmcnt<U * (DS - 1)>();
-                read_frame<C, U>(slot, lane, cur);
-#ifdef DIPS_PF_INPLACE
-                frame_accumulate<C, CH, U, PF, MAP>(a, sa, sa, cur, voff, tf, v + 4 * d, lut);
-#else
-                if (PF && d == 1) frame_accumulate<C, CH, U, PF, MAP>(a, sb, sa, cur, voff, tf, v + 4 * d, lut);
-                else frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, cur, voff, tf, v + 4 * d, lut);
-#endif
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                const uint32_t tl = min(tf + (uint32_t)DS, tlast);
-                dma_frame<C, U>(make_rsrc(a.frames + (uint64_t)tl * fb, fb), slot, voff);
-            }
-            wave_sum8(v, sum, lane);
-            write_record<C>(rpart, t, lane, sum);
-            write_record<C>(rpart, t + 1, lane, sum + 4);
-        }
-        if (t < tend) {  // one frame left
-            uint32_t v[4], sum[4];
-            uint8_t __attribute__((address_space(3)))* slot = ring + ((t - tseg) % DS) * R::kTile;
-            uint32_t cur[U][F::NDW];
-            wait_vmcnt<0>();
-            read_frame<C, U>(slot, lane, cur);
-            frame_accumulate<C, CH, U, PF, MAP>(a, sa, sb, cur, voff, t, v, lut);
-            wave_sum4(v, sum);
-            write_record<C>(rpart, t, lane, sum);
-        }
-        // drain this segment's clamped DMA refills before the ring is reused
-        wait_vmcnt<0>();
-    }
-#else
-    (void)a;
-    (void)ring_mem;
-#endif
-}
-
-// Sum the 16-byte partial records of `tiles_per_thread` tiles for one frame
-// and add them to the series with 64-bit integer atomics.
+// Sum the 16-byte partial records of `tiles_per_block` tiles for one frame
+// and add them to the series with 64-bit integer atomics.  A record holds the
+// four wave sums of one (tile, frame):
+//   RGB(A): {SAD, SJ + count << 20, H, L}     SI_fixed = H << 15 + L
+//   gray:   {SAD + count << 20, H, L, 0}      SI_fixed = H << 16 + L, SJ = 2 SAD
+// (H, L: the split of the exact per-lane fixed-point intensity sum).
 __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __restrict__ partials, uint32_t n_frames,
-                                                            uint32_t n_tiles, uint32_t tiles_per_block,
+                                                            uint32_t n_tiles, uint32_t tiles_per_block, uint32_t gray,
                                                             dips_series_entry* __restrict__ series) {
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
     if (t >= n_frames) return;
     const uint32_t tile0 = blockIdx.y * tiles_per_block;
     const uint32_t tile1 = min(n_tiles, tile0 + tiles_per_block);
-    uint64_t sad = 0, sj = 0, cnt = 0, sif = 0;
+    uint64_t sad = 0, sj = 0, cnt = 0, h = 0;
+    int64_t l = 0;
     for (uint32_t tile = tile0; tile < tile1; ++tile) {
         const u32x4 rec = *reinterpret_cast<const u32x4*>(partials + 2 * ((uint64_t)tile * n_frames + t));
-        sad += rec.x;
-        sj += rec.y;
-        const uint64_t hi = ((uint64_t)rec.w << 32) | rec.z;
-        cnt += hi >> 48;
-        sif += hi & 0x0000FFFFFFFFFFFFull;
+        if (gray) {
+            sad += rec.x & 0xFFFFFu;
+            cnt += rec.x >> 20;
+            h += rec.y;
+            l += (int64_t)(int32_t)rec.z;
+        } else {
+            sad += rec.x;
+            sj += rec.y & 0xFFFFFu;
+            cnt += rec.y >> 20;
+            h += rec.z;
+            l += (int64_t)(int32_t)rec.w;
+        }
     }
+    if (gray) sj = 2u * sad;
+    const uint64_t sif = (h << (gray ? 16 : 15)) + (uint64_t)l;
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].sad), (unsigned long long)sad);
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].sj), (unsigned long long)sj);
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].count), (unsigned long long)cnt);
@@ -835,16 +486,21 @@ static const void* pick_fast_u(int chroma, bool pf, bool map) {
     }
 }
 
-int fast_unroll(int channels) { return channels == 1 ? kUnrollGray : kUnrollRGB; }
+// RGB8 / RGBA8 run series_v2_kernel (series_v2.hip); GRAY8 the kernel above.
+int fast_unroll(int channels) { return channels == 1 ? kUnrollGray : kUnrollV2; }
 
 const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map) {
     switch (channels) {
         case 1: return pick_fast_u<1, kUnrollGray>(chroma, per_frame, map);
-        case 3: return pick_fast_u<3, kUnrollRGB>(chroma, per_frame, map);
-        case 4: return pick_fast_u<4, kUnrollRGB>(chroma, per_frame, map);
+        case 3:
+        case 4: return series_v2_kernel_ptr(channels, chroma, per_frame, map);
         default: return nullptr;
     }
 }
+
+// gray: dI > tau on the f32 intensity; RGB(A) v2: |dI2s| > tau * 2^23 with
+// I2s = 2 I * 2^22 (exact power-of-two scalings of the reference comparison)
+float series_threshold(int channels, float tau) { return channels == 1 ? tau : tau * 8388608.0f; }
 
 int pixels_per_vec(int channels) { return channels == 1 ? 16 : 4; }
 
@@ -857,11 +513,12 @@ hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, boo
     return hipLaunchKernel(k, dim3(blocks), dim3(256), params, 0, s);
 }
 
-hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles,
+hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, bool gray,
                                 dips_series_entry* series, hipStream_t s) {
     const uint32_t tpb = 64;
     dim3 grid((n_frames + 255u) / 256u, (n_tiles + tpb - 1u) / tpb);
-    hipLaunchKernelGGL(series_reduce_kernel, grid, dim3(256), 0, s, partials, n_frames, n_tiles, tpb, series);
+    hipLaunchKernelGGL(series_reduce_kernel, grid, dim3(256), 0, s, partials, n_frames, n_tiles, tpb, gray ? 1u : 0u,
+                       series);
     return hipGetLastError();
 }
 

@@ -1,0 +1,310 @@
+// series_v2.hip -- the RGB8/RGBA8 series kernel (hot path of the north star).
+//
+// Same contract as series_fast_kernel (series_kernels.hip): per (tile, frame)
+// one 16-byte record of wave sums {SAD, SJ + count << 20, H, L}, summed per
+// frame by series_reduce_kernel.  What differs is how the work is shaped for
+// the CDNA4 VALU (measured issue costs: tools/vbench.hip, profiles/):
+//
+//  * intensity without conversions: with J = max+min (integer, needed for SJ
+//    anyway) and E = P(max) + P(min), P(c) = the largest power of two <= c,
+//        2 * get_intensity = u(max) + u(min) = RNE(J * 65793 * 2^-24 + E * 2^-31)
+//    exactly (u(c) = c/255 rounds UP to c*65793*2^-24 + 2^(msb(c)-31); the
+//    identity is checked exhaustively in tests/test_oracle.py).  J enters one
+//    v_fma_mix_f32 as an f16 DENORMAL (its u16 bits unchanged, value J*2^-24)
+//    and E comes from the exponent field of the f16 value c*2^-9 (one packed
+//    f16 multiply + an AND): 3.5 packed/mixed ops per pixel pair replace four
+//    v_cvt_f32_ubyte and five packed f32 ops.  Intensities live in the 2^22
+//    scaled domain I2s = I2 * 2^22 (exact power-of-two scaling);
+//  * a 4-slot register ring of frame vecs, rotated by unrolling four frames,
+//    so the bytes of frame t double as the SAD reference of frame t+1 with no
+//    register copies (the previous kernel spent ~10% of its VALU on v_mov);
+//  * U = 2 vecs per lane: <= 64 VGPRs, 8 waves per SIMD -- the VALU classes
+//    this kernel uses issue 20-35% faster at 8 waves than at 4 (vbench);
+//  * the two frames of a pair are reduced together and their 8 wave sums are
+//    stored straight from the lanes that hold them (no v_readlane).
+#include "series_common.h"
+
+namespace dips {
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+// 65793 * 2^7: J * 2^-9 (normal f16) times this is J * 65793 / 4.
+constexpr float kI2Mul = 8421504.0f;
+// SJ from the intensity difference: 255 * |dI2| = |dJ| + err, |err| < 1.1e-4
+// (u() rounds up by < 2^-24, the sum and difference round by <= 2^-24 each),
+// so the per-lane f32 sum of |dI2s| * 255 * 2^-22 (exact multiplier, <= 8 px x
+// 510 < 4096: rounding < 2^-13 per add) is within 0.002 of the integer SJ.
+constexpr float kSjMul = 255.0f / 4194304.0f;
+
+// v_fma_mix_f32 on the low / high f16 halves of j and e (f32 multiplier k):
+// one fused op, the f16 operands widened exactly.  (hipcc does not form it
+// from fmaf((float)half, k, (float)half): it emits two v_cvt_f32_f16 and a
+// v_pk_fma_f32.)  The f16 operands must be NORMAL numbers: with an f16
+// denormal operand the gfx950 result is not the exact fused value
+// (tools/i2check.hip), hence J enters as J * 2^-9.
+__device__ __forceinline__ float fma_mix_lo(uint32_t j, float k, uint32_t e) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(j), "s"(k), "v"(e));
+    return r;
+}
+__device__ __forceinline__ float fma_mix_hi(uint32_t j, float k, uint32_t e) {
+    float r;
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(j), "s"(k), "v"(e));
+    return r;
+}
+
+// c * 2^-9 as normal f16s: the u16 pair read as f16 denormals (c * 2^-24)
+// times 2^15 (exact).
+__device__ __forceinline__ h2 norm_h2(u16x2 c) {
+    return __builtin_bit_cast(h2, c) * (h2){(_Float16)32768.0f, (_Float16)32768.0f};
+}
+// sign and exponent bits only: the largest power of two <= x (0 for 0)
+__device__ __forceinline__ h2 pow2_floor_h2(h2 x) {
+    return __builtin_bit_cast(h2, __builtin_bit_cast(uint32_t, x) & 0xFC00FC00u);
+}
+
+// Derived state of one vec (4 px): the scaled intensity pairs I2s.
+struct St2 {
+    f32x2 i[2];
+};
+
+template <int C, int CH>
+__device__ __forceinline__ void derive_v2(const uint32_t (&d)[Fmt<C>::NDW], St2& s) {
+    u16x2 r[2], g[2], b[2];
+    pair_planes<C>(d, r, g, b);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        u16x2 mx, mn;
+        if constexpr (CH == 0) {
+            mx = __builtin_elementwise_max(__builtin_elementwise_max(r[k], g[k]), b[k]);
+            mn = __builtin_elementwise_min(__builtin_elementwise_min(r[k], g[k]), b[k]);
+        } else {
+            mx = mn = CH == 1 ? r[k] : (CH == 2 ? g[k] : b[k]);
+        }
+        const h2 xn = norm_h2(mx), nn = norm_h2(mn);
+        const uint32_t jn = __builtin_bit_cast(uint32_t, xn + nn);  // J * 2^-9, exact
+        const uint32_t e = __builtin_bit_cast(uint32_t, pow2_floor_h2(xn) + pow2_floor_h2(nn));
+        s.i[k] = f32x2{fma_mix_lo(jn, kI2Mul, e), fma_mix_hi(jn, kI2Mul, e)};
+    }
+}
+
+// One frame of one tile: accumulate against the reference state `st`
+// (updated to this frame's state in per-frame mode) and the reference bytes
+// `rb`; produce the 4 per-lane values {SAD, SJ, H, L} and the wave-wide count.
+template <int C, int CH, int U, bool PF, bool MAP, int SK>
+__device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], const uint32_t (&rb)[U][Fmt<C>::NDW],
+                                         const uint32_t (&cur)[U][Fmt<C>::NDW], uint32_t voff, uint32_t t,
+                                         uint32_t* vals, uint32_t& cnt) {
+    using F = Fmt<C>;
+    uint32_t sad = 0, c = 0;
+    float sj = 0.5f;  // + 0.5: the final truncation rounds to nearest
+    // exact per-lane intensity sum, offset by 2^43 so that the f64's low 52
+    // mantissa bits ARE the fixed-point value n = sum(a_s) * 2^9 (ulp(2^43)
+    // = 2^-9, the a_s granularity; n < 2^35 keeps every add exact)
+    double si = 0x1p43;
+    uint32_t map[U][F::NDW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int k = 0; k < F::NDW; ++k) {
+            sad = __builtin_amdgcn_sad_u8(cur[u][k], rb[u][k], sad);
+            if constexpr (MAP) map[u][k] = absdiff_bytes(cur[u][k], rb[u][k]);
+        }
+        St2 n;
+        derive_v2<C, CH>(cur[u], n);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const f32x2 d = n.i[k] - st[u].i[k];
+            const float a0 = fabsf(d.x), a1 = fabsf(d.y);
+            sj = __builtin_fmaf(a0, kSjMul, sj);
+            sj = __builtin_fmaf(a1, kSjMul, sj);
+            const bool s0 = a0 > a.thr, s1 = a1 > a.thr;
+            const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
+            c += (uint32_t)__builtin_popcountll(m0) + (uint32_t)__builtin_popcountll(m1);
+            // SK: the exact sum only where some lane of the wave has a pixel
+            // above the threshold (wave-uniform branch: only additions of
+            // zero are skipped, the result is identical)
+            if constexpr (SK) {
+                if (m0 | m1) {
+                    si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
+                    asm volatile("");  // keep this a branch: hipcc otherwise if-converts it
+                }
+            } else {
+                si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
+            }
+        }
+        if constexpr (PF) st[u] = n;
+    }
+    if constexpr (MAP) {
+        const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.frame_bytes);
+#pragma unroll
+        for (int u = 0; u < U; ++u) store_vec<C>(rm, voff + (uint32_t)(u * 64 * F::VB), map[u]);
+    }
+    const uint64_t yb = __builtin_bit_cast(uint64_t, si);
+    const uint32_t lo = (uint32_t)yb, hi = (uint32_t)(yb >> 32);
+    vals[0] = sad;
+    vals[1] = (uint32_t)sj;
+    vals[2] = __builtin_amdgcn_alignbit(hi, lo, 15);  // H = n >> 15 (n < 2^35: no exponent bits)
+    vals[3] = lo & 0x7FFFu;                           // L = n mod 2^15
+    cnt = c;
+}
+
+// Records of frames t, t+1 from their 8 reduced values (lanes 8v hold v).
+__device__ __forceinline__ void store_pair(__amdgpu_buffer_rsrc_t rpart, uint32_t t, uint32_t rec_off8,
+                                           uint32_t lane, uint32_t y, uint32_t cnt0, uint32_t cnt1) {
+    const uint32_t add = lane == 8u ? (cnt0 << 20) : (lane == 40u ? (cnt1 << 20) : 0u);
+    __builtin_amdgcn_raw_buffer_store_b32(y + add, rpart, rec_off8, t * 16u, 0);
+}
+
+__device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t t, uint32_t rec_off4,
+                                          uint32_t lane, uint32_t y, uint32_t cnt) {
+    const uint32_t add = lane == 16u ? (cnt << 20) : 0u;
+    __builtin_amdgcn_raw_buffer_store_b32(y + add, rpart, rec_off4, t * 16u, 0);
+}
+
+// Minimum waves per SIMD asked of the register allocator: the RGB8
+// per-frame kernel fits 64 VGPRs (8 waves) without spilling; the other
+// variants hold more state (fixed reference bytes, RGBA vecs, map stores) and
+// keep their natural allocation (5-7 waves).
+template <int C, bool PF, bool MAP, int SK>
+constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? (SK ? 7 : 8) : 1; }
+
+template <int C, int CH, int U, bool PF, bool MAP, int SK = 0>
+__global__ __launch_bounds__(256, (v2_min_waves<C, PF, MAP, SK>())) void series_v2_kernel(SeriesArgs a) {
+    using F = Fmt<C>;
+    static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (wave >= a.n_waves) return;
+    const uint32_t fb = a.frame_bytes;
+    // record dword offsets of the lanes that store reduced values; other
+    // lanes point past the descriptor and their stores are dropped
+    const uint32_t rec_off8 = (lane & 7u) == 0u ? (lane >> 5) * 16u + ((lane >> 3) & 3u) * 4u : 0x80000000u;
+    const uint32_t rec_off4 = (lane & 15u) == 0u ? (lane >> 4) * 4u : 0x80000000u;
+
+    uint64_t i = (uint64_t)wave * a.items / a.n_waves;
+    const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
+    while (i < iend) {
+        const uint32_t tile = (uint32_t)(i / a.n_frames);
+        const uint32_t t0 = (uint32_t)(i - (uint64_t)tile * a.n_frames);
+        const uint64_t remaining = iend - i;
+        const uint32_t tend =
+            (uint32_t)((uint64_t)a.n_frames < t0 + remaining ? (uint64_t)a.n_frames : t0 + remaining);
+        i += tend - t0;
+        const uint32_t n = tend - t0;  // frames of this segment (>= 1)
+        const uint32_t tlast = tend - 1;
+        const uint32_t voff = (tile * U * 64u + lane) * (uint32_t)F::VB;
+        const __amdgpu_buffer_rsrc_t rpart =
+            make_rsrc(a.partials + 2 * (uint64_t)tile * a.n_frames, a.n_frames * 16u);
+
+        auto load_frame = [&](uint32_t tf, uint32_t (&dst)[U][F::NDW]) {
+#ifdef DIPS_PROBE_SAMEFRAME
+            // probe build only (tools/probe.hip): every load re-reads the
+            // segment's first frame -- the kernel's compute-only time
+            tf = t0;
+#endif
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)min(tf, tlast) * fb, fb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) load_vec<C>(r, voff + (uint32_t)(u * 64 * F::VB), dst[u]);
+        };
+
+        // ring: PF -- frame k of the segment in slot (k+1)&3, its reference
+        // (frame k-1) in slot k&3; overall -- frame k in slot k&3, the fixed
+        // reference bytes in rb
+        uint32_t buf[4][U][F::NDW];
+        uint32_t rb[U][F::NDW];  // overall mode only
+        St2 st[U];
+        {
+            const uint8_t* rp = PF ? (t0 == 0 ? a.ref0 : a.frames + (uint64_t)(t0 - 1) * fb) : a.ref0;
+            const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, fb);
+            uint32_t (&dref)[U][F::NDW] = PF ? buf[0] : rb;
+#pragma unroll
+            for (int u = 0; u < U; ++u) load_vec<C>(rr, voff + (uint32_t)(u * 64 * F::VB), dref[u]);
+            if constexpr (PF) {
+                load_frame(t0, buf[1]);
+                load_frame(t0 + 1, buf[2]);
+                load_frame(t0 + 2, buf[3]);
+            } else {
+                load_frame(t0, buf[0]);
+                load_frame(t0 + 1, buf[1]);
+                load_frame(t0 + 2, buf[2]);
+                load_frame(t0 + 3, buf[3]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) derive_v2<C, CH>(dref[u], st[u]);
+        }
+
+        uint32_t k = 0;
+        for (; k + 4 <= n; k += 4) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint32_t v[8], c0, c1;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int j = 2 * h + q;
+                    const uint32_t tf = t0 + k + (uint32_t)j;
+                    if constexpr (PF) {
+                        frame_v2<C, CH, U, PF, MAP, SK>(a, st, buf[j], buf[(j + 1) & 3], voff, tf, v + 4 * q,
+                                                    q ? c1 : c0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        load_frame(tf + 3, buf[j]);
+                    } else {
+                        frame_v2<C, CH, U, PF, MAP, SK>(a, st, rb, buf[j], voff, tf, v + 4 * q, q ? c1 : c0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        load_frame(tf + 4, buf[j]);
+                    }
+                }
+                const uint32_t y = wave_sum8_lanes(v, lane);
+                store_pair(rpart, t0 + k + 2 * h, rec_off8, lane, y, c0, c1);
+            }
+        }
+        // tail: up to 3 frames, already in flight in their slots
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if (k + (uint32_t)j < n) {
+                uint32_t v[4], c;
+                const uint32_t tf = t0 + k + (uint32_t)j;
+                if constexpr (PF)
+                    frame_v2<C, CH, U, PF, MAP, SK>(a, st, buf[j], buf[j + 1], voff, tf, v, c);
+                else
+                    frame_v2<C, CH, U, PF, MAP, SK>(a, st, rb, buf[j], voff, tf, v, c);
+                const uint32_t y = wave_sum4_lanes(v);
+                store_one(rpart, tf, rec_off4, lane, y, c);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// instantiation table
+// ---------------------------------------------------------------------------
+template <int C, int CH, bool PF, bool MAP>
+static const void* v2_ptr() {
+    return reinterpret_cast<const void*>(&series_v2_kernel<C, CH, kUnrollV2, PF, MAP>);
+}
+
+template <int C>
+static const void* pick_v2(int chroma, bool pf, bool map) {
+#define DIPS_PICK_V2(CHV)                                                                        \
+    case CHV:                                                                                    \
+        return pf ? (map ? v2_ptr<C, CHV, true, true>() : v2_ptr<C, CHV, true, false>())         \
+                  : (map ? v2_ptr<C, CHV, false, true>() : v2_ptr<C, CHV, false, false>());
+    switch (chroma) {
+        DIPS_PICK_V2(0)
+        DIPS_PICK_V2(1)
+        DIPS_PICK_V2(2)
+        DIPS_PICK_V2(3)
+        default: return nullptr;
+    }
+#undef DIPS_PICK_V2
+}
+
+const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool map) {
+    switch (channels) {
+        case 3: return pick_v2<3>(chroma, per_frame, map);
+        case 4: return pick_v2<4>(chroma, per_frame, map);
+        default: return nullptr;
+    }
+}
+
+}  // namespace dips

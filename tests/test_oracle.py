@@ -222,3 +222,44 @@ def test_golden_manifest_and_fixtures():
                 assert o is None
             else:
                 assert np.array_equal(o, outs[k - 3]), (case["file"], k)
+
+
+def test_v2_intensity_identity():
+    """series_v2 (dips_amd/csrc/series_v2.hip) computes 2*get_intensity
+    without conversions: u(c) = c/255 rounds UP to c*65793*2^-24 +
+    2^(msb(c)-31), hence u(max) + u(min) = RNE(J*65793*2^-24 + E*2^-31) with
+    J = max+min and E = P(max)+P(min).  Exhaustive over every byte pair."""
+    from fractions import Fraction
+    for c in range(1, 256):
+        p = 1 << (c.bit_length() - 1)
+        assert Fraction(float(nr.U_LUT[c])) == Fraction(c * 65793, 1 << 24) + Fraction(p, 1 << 31), c
+    mx, mn = np.meshgrid(np.arange(256), np.arange(256), indexing="ij")
+    keep = mx >= mn
+    mx, mn = mx[keep], mn[keep]
+    pw = lambda c: np.where(c > 0, np.left_shift(1, np.floor(np.log2(np.maximum(c, 1))).astype(np.int64)), 0)
+    # exact in f64 (< 2^34 significant bits), then one rounding to f32
+    i2s = ((mx + mn) * 65793 / 4.0 + (pw(mx) + pw(mn)) / 512.0).astype(np.float32)
+    want = (nr.U_LUT[mx] + nr.U_LUT[mn]).astype(np.float32) * np.float32(2.0 ** 22)
+    assert np.array_equal(i2s, want)
+
+
+def test_v2_sj_from_intensity_difference():
+    """series_v2 derives SJ = sum |dJ| from the intensity differences:
+    |255 * |dI2| - |dJ|| < 1.1e-4 per pixel (checked on 2M random pixel
+    pairs, plus the bound's extreme cases), so the per-lane f32 sum rounds to
+    the exact integer."""
+    rng = np.random.default_rng(5)
+    mx, mn = np.meshgrid(np.arange(256), np.arange(256), indexing="ij")
+    keep = mx >= mn
+    mx, mn = mx[keep], mn[keep]
+    i2 = (nr.U_LUT[mx] + nr.U_LUT[mn]).astype(np.float32)
+    j = mx + mn
+    p = rng.integers(0, i2.size, 2_000_000)
+    q = rng.integers(0, i2.size, 2_000_000)
+    a = np.abs((i2[p] - i2[q]).astype(np.float32)).astype(np.float64)
+    err = np.abs(255.0 * a - np.abs(j[p] - j[q]))
+    assert err.max() < 1.1e-4
+    # extremes: largest and smallest intensities against everything
+    for k in (0, i2.size - 1, int(np.argmax(j)), int(np.argmin(j))):
+        a = np.abs((i2 - i2[k]).astype(np.float32)).astype(np.float64)
+        assert (np.abs(255.0 * a - np.abs(j - j[k]))).max() < 1.1e-4

@@ -5,10 +5,12 @@
 // Variants are timed interleaved in one process (cdna_hip_programming.md
 // §5.4 rule 24): median of R rounds per variant, GB/s of frame bytes.
 #include "../dips_amd/csrc/series_kernels.hip"
+#include "../dips_amd/csrc/series_v2.hip"
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <string>
 #include <vector>
@@ -110,6 +112,7 @@ int main(int argc, char** argv) {
         std::string name;
         std::function<void()> run;
         std::vector<float> ms;
+        std::string group;  // variants of one group must give identical series
     };
     std::vector<Variant> vs;
 
@@ -147,8 +150,8 @@ int main(int argc, char** argv) {
     }
     WALK(12, 4)
 
-    // product-kernel variants: series_fast_kernel<3, 0, U, D, PF, false>
-    CK(hipMalloc(&partials, (uint64_t)F * 8100 * 4 * 16));
+    // kernels: series_fast_kernel (previous RGB kernel) and series_v2_kernel
+    CK(hipMalloc(&partials, (uint64_t)F * 16200 * 16 + 4096));
 #define SERIES(U, D, PF)                                                                              \
     {                                                                                                 \
         SeriesArgs a; uint32_t blocks; int occ;                                                       \
@@ -157,36 +160,70 @@ int main(int argc, char** argv) {
         a.partials = partials;                                                                        \
         vs.push_back({"series<U=" #U ",D=" #D ",PF=" #PF "> occ=" + std::to_string(occ) + " waves=" +  \
                           std::to_string(a.n_waves),                                                  \
-                      [=]() { hipLaunchKernelGGL((series_fast_kernel<3, 0, U, D, PF, false>), dim3(blocks), dim3(256), 0, 0, a); }, {}}); \
+                      [=]() { hipLaunchKernelGGL((series_fast_kernel<3, 0, U, D, PF, false>), dim3(blocks), dim3(256), 0, 0, a); \
+                              CK(launch_series_reduce(partials, F, a.n_tiles, false, series, 0)); }, {}, "PF=" #PF " tau=8.0f"}); \
     }
-    SERIES(4, 2, true)
-    SERIES(4, 2, false)
-#define SLDS(U, D, PF)                                                                                \
+#define SERIES_V2U(PF, U) SERIES_V2X(PF, U, 8.0f, 0)
+#define SERIES_V2X(PF, U, TAU255, SK)                                                                             \
     {                                                                                                 \
         SeriesArgs a; uint32_t blocks; int occ;                                                       \
-        const void* k = (const void*)&series_lds_kernel<3, 0, U, D, PF, false>;                       \
+        const void* k = (const void*)&series_v2_kernel<3, 0, U, PF, false, SK>;                           \
         geom(12, U, k, a, blocks, occ);                                                               \
         a.partials = partials;                                                                        \
-        vs.push_back({"lds<U=" #U ",D=" #D ",PF=" #PF "> occ=" + std::to_string(occ) + " waves=" +     \
-                          std::to_string(a.n_waves),                                                  \
-                      [=]() { hipLaunchKernelGGL((series_lds_kernel<3, 0, U, D, PF, false>), dim3(blocks), dim3(256), 0, 0, a); }, {}}); \
+        a.thr = series_threshold(3, TAU255 / 255.0f);                                                 \
+        vs.push_back({"v2<U=" #U ",PF=" #PF ",SK=" #SK "> tau=" #TAU255 "/255 occ=" + std::to_string(occ) + " waves=" + std::to_string(a.n_waves), \
+                      [=]() { hipLaunchKernelGGL((series_v2_kernel<3, 0, U, PF, false, SK>), dim3(blocks), dim3(256), 0, 0, a); \
+                              CK(launch_series_reduce(partials, F, a.n_tiles, false, series, 0)); }, {}, "PF=" #PF " tau=" #TAU255}); \
     }
-    SLDS(4, 2, true)
-    SLDS(4, 3, true)
-    SLDS(4, 4, true)
-    SLDS(2, 4, true)
-    SLDS(4, 3, false)
-SERIES(4, 4, true)
-    SERIES(2, 2, true)
-    SERIES(2, 4, true)
-    SERIES(8, 2, true)
-    SERIES(4, 4, false)
+#define SERIES_V2(PF) SERIES_V2U(PF, kUnrollV2)
+    SERIES(4, 2, true)
+    SERIES_V2(true)
+    SERIES(4, 2, false)
+    SERIES_V2(false)
+    SERIES_V2X(true, kUnrollV2, 0.0f, 0)
+    SERIES_V2X(true, kUnrollV2, 8.0f, 1)
+    SERIES_V2X(true, kUnrollV2, 0.0f, 1)
 
     if (argc > 3) {  // substring filter on variant names
         std::vector<Variant> keep;
         for (auto& v : vs)
             if (v.name.find(argv[3]) != std::string::npos) keep.push_back(v);
         vs.swap(keep);
+    }
+    // parity: every variant's series (last run) against the first variant of
+    // the same mode (names containing PF=true / PF=false)
+    std::vector<dips_series_entry> host(F);
+    auto run_series = [&](Variant& v) {
+        CK(hipMemset(series, 0, sizeof(dips_series_entry) * F));
+        v.run();
+        CK(hipDeviceSynchronize());
+        std::vector<dips_series_entry> h(F);
+        CK(hipMemcpy(h.data(), series, sizeof(dips_series_entry) * F, hipMemcpyDeviceToHost));
+        return h;
+    };
+    std::vector<std::string> groups;
+    for (auto& v : vs)
+        if (!v.group.empty() && std::find(groups.begin(), groups.end(), v.group) == groups.end()) groups.push_back(v.group);
+    for (const auto& grp : groups) {
+        std::vector<dips_series_entry> ref;
+        std::string refname;
+        for (auto& v : vs) {
+            if (v.group != grp) continue;
+            auto h = run_series(v);
+            if (ref.empty()) { ref = h; refname = v.name; continue; }
+            const bool same = memcmp(ref.data(), h.data(), sizeof(dips_series_entry) * F) == 0;
+            printf("parity %-30s vs %-30s : %s\n", v.name.c_str(), refname.c_str(), same ? "IDENTICAL" : "MISMATCH");
+            if (!same)
+                for (uint32_t t = 0; t < F; ++t)
+                    if (memcmp(&ref[t], &h[t], sizeof(dips_series_entry))) {
+                        printf("  frame %u: %llu %llu %llu %llu vs %llu %llu %llu %llu\n", t,
+                               (unsigned long long)ref[t].sad, (unsigned long long)ref[t].sj,
+                               (unsigned long long)ref[t].count, (unsigned long long)ref[t].si_fixed,
+                               (unsigned long long)h[t].sad, (unsigned long long)h[t].sj,
+                               (unsigned long long)h[t].count, (unsigned long long)h[t].si_fixed);
+                        break;
+                    }
+        }
     }
     Timer tm;
     for (int r = 0; r < R; ++r) {
