@@ -15,7 +15,7 @@ def per_dispatch(d, counter):
     vals = []
     for f in glob.glob(os.path.join(d, counter, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "series_fast_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if "series_v2_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     return vals
 
@@ -25,14 +25,14 @@ def main():
     fetch = per_dispatch(d, "FETCH_SIZE")
     write = per_dispatch(d, "WRITE_SIZE")
     if not fetch or not write:
-        raise SystemExit(f"no series_fast_kernel rows (fetch {len(fetch)}, write {len(write)})")
+        raise SystemExit(f"no series_v2_kernel rows (fetch {len(fetch)}, write {len(write)})")
     fk = sum(fetch) / len(fetch)
     wk = sum(write) / len(write)
     W, H, C = 3840, 2160, 3
     algo = frames * W * H * C
     res = {
         "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on bench.py, "
-                  "series_fast_kernel dispatches; FETCH_SIZE x2 (gfx950 wide-stream correction)",
+                  "series_v2_kernel dispatches; FETCH_SIZE x2 (gfx950 wide-stream correction)",
         "width": W, "height": H, "frames": frames, "mode": mode,
         "fetch_kib_raw": fk, "write_kib": wk,
         "read_bytes_per_launch": 2 * fk * 1024, "write_bytes_per_launch": wk * 1024,
