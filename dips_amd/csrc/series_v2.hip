@@ -53,11 +53,9 @@ __device__ __forceinline__ float fma_mix_hi(uint32_t j, float k, uint32_t e) {
     return r;
 }
 
-// c * 2^-9 as normal f16s: the u16 pair read as f16 denormals (c * 2^-24)
-// times 2^15 (exact).
-__device__ __forceinline__ h2 norm_h2(u16x2 c) {
-    return __builtin_bit_cast(h2, c) * (h2){(_Float16)32768.0f, (_Float16)32768.0f};
-}
+// c * 2^-9 as normal f16s from the u16 pair read as f16 denormals
+// (c * 2^-24) times 2^15 (exact).
+__device__ __forceinline__ h2 norm_h2(h2 c) { return c * (h2){(_Float16)32768.0f, (_Float16)32768.0f}; }
 // sign and exponent bits only: the largest power of two <= x (0 for 0)
 __device__ __forceinline__ h2 pow2_floor_h2(h2 x) {
     return __builtin_bit_cast(h2, __builtin_bit_cast(uint32_t, x) & 0xFC00FC00u);
@@ -74,12 +72,16 @@ __device__ __forceinline__ void derive_v2(const uint32_t (&d)[Fmt<C>::NDW], St2&
     pair_planes<C>(d, r, g, b);
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        u16x2 mx, mn;
+        // max / min of the channels on the u16 planes read as f16 denormals
+        // (c * 2^-24: same order as the bytes): one v_pk_maximum3_f16 and one
+        // v_pk_minimum3_f16 per pixel pair
+        h2 mx, mn;
         if constexpr (CH == 0) {
-            mx = __builtin_elementwise_max(__builtin_elementwise_max(r[k], g[k]), b[k]);
-            mn = __builtin_elementwise_min(__builtin_elementwise_min(r[k], g[k]), b[k]);
+            const h2 rh = __builtin_bit_cast(h2, r[k]), gh = __builtin_bit_cast(h2, g[k]), bh = __builtin_bit_cast(h2, b[k]);
+            mx = __builtin_elementwise_maximum(__builtin_elementwise_maximum(rh, gh), bh);
+            mn = __builtin_elementwise_minimum(__builtin_elementwise_minimum(rh, gh), bh);
         } else {
-            mx = mn = CH == 1 ? r[k] : (CH == 2 ? g[k] : b[k]);
+            mx = mn = __builtin_bit_cast(h2, CH == 1 ? r[k] : (CH == 2 ? g[k] : b[k]));
         }
         const h2 xn = norm_h2(mx), nn = norm_h2(mn);
         const uint32_t jn = __builtin_bit_cast(uint32_t, xn + nn);  // J * 2^-9, exact
