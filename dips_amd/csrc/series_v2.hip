@@ -93,7 +93,7 @@ __device__ __forceinline__ void derive_v2(const uint32_t (&d)[Fmt<C>::NDW], St2&
 // One frame of one tile: accumulate against the reference state `st`
 // (updated to this frame's state in per-frame mode) and the reference bytes
 // `rb`; produce the 4 per-lane values {SAD, SJ, H, L} and the wave-wide count.
-template <int C, int CH, int U, bool PF, bool MAP, int SK>
+template <int C, int CH, int U, bool PF, bool MAP>
 __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], const uint32_t (&rb)[U][Fmt<C>::NDW],
                                          const uint32_t (&cur)[U][Fmt<C>::NDW], uint32_t voff, uint32_t t,
                                          uint32_t* vals, uint32_t& cnt) {
@@ -123,17 +123,10 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
             const bool s0 = a0 > a.thr, s1 = a1 > a.thr;
             const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
             c += (uint32_t)__builtin_popcountll(m0) + (uint32_t)__builtin_popcountll(m1);
-            // SK: the exact sum only where some lane of the wave has a pixel
-            // above the threshold (wave-uniform branch: only additions of
-            // zero are skipped, the result is identical)
-            if constexpr (SK) {
-                if (m0 | m1) {
-                    si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
-                    asm volatile("");  // keep this a branch: hipcc otherwise if-converts it
-                }
-            } else {
-                si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
-            }
+            // (a wave-uniform skip of this exact sum when no lane has a pixel
+            // above the threshold measured slower: if-converted by hipcc, or
+            // as a forced branch it costs registers and occupancy)
+            si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
         }
         if constexpr (PF) st[u] = n;
     }
@@ -168,11 +161,11 @@ __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t
 // per-frame kernel fits 64 VGPRs (8 waves) without spilling; the other
 // variants hold more state (fixed reference bytes, RGBA vecs, map stores) and
 // keep their natural allocation (5-7 waves).
-template <int C, bool PF, bool MAP, int SK>
-constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? (SK ? 7 : 8) : 1; }
+template <int C, bool PF, bool MAP>
+constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? 8 : 1; }
 
-template <int C, int CH, int U, bool PF, bool MAP, int SK = 0>
-__global__ __launch_bounds__(256, (v2_min_waves<C, PF, MAP, SK>())) void series_v2_kernel(SeriesArgs a) {
+template <int C, int CH, int U, bool PF, bool MAP>
+__global__ __launch_bounds__(256, (v2_min_waves<C, PF, MAP>())) void series_v2_kernel(SeriesArgs a) {
     using F = Fmt<C>;
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;
@@ -246,12 +239,12 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, PF, MAP, SK>())) void series_
                     const int j = 2 * h + q;
                     const uint32_t tf = t0 + k + (uint32_t)j;
                     if constexpr (PF) {
-                        frame_v2<C, CH, U, PF, MAP, SK>(a, st, buf[j], buf[(j + 1) & 3], voff, tf, v + 4 * q,
+                        frame_v2<C, CH, U, PF, MAP>(a, st, buf[j], buf[(j + 1) & 3], voff, tf, v + 4 * q,
                                                     q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 3, buf[j]);
                     } else {
-                        frame_v2<C, CH, U, PF, MAP, SK>(a, st, rb, buf[j], voff, tf, v + 4 * q, q ? c1 : c0);
+                        frame_v2<C, CH, U, PF, MAP>(a, st, rb, buf[j], voff, tf, v + 4 * q, q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 4, buf[j]);
                     }
@@ -267,9 +260,9 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, PF, MAP, SK>())) void series_
                 uint32_t v[4], c;
                 const uint32_t tf = t0 + k + (uint32_t)j;
                 if constexpr (PF)
-                    frame_v2<C, CH, U, PF, MAP, SK>(a, st, buf[j], buf[j + 1], voff, tf, v, c);
+                    frame_v2<C, CH, U, PF, MAP>(a, st, buf[j], buf[j + 1], voff, tf, v, c);
                 else
-                    frame_v2<C, CH, U, PF, MAP, SK>(a, st, rb, buf[j], voff, tf, v, c);
+                    frame_v2<C, CH, U, PF, MAP>(a, st, rb, buf[j], voff, tf, v, c);
                 const uint32_t y = wave_sum4_lanes(v);
                 store_one(rpart, tf, rec_off4, lane, y, c);
             }

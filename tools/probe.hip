@@ -163,16 +163,16 @@ int main(int argc, char** argv) {
                       [=]() { hipLaunchKernelGGL((series_fast_kernel<3, 0, U, D, PF, false>), dim3(blocks), dim3(256), 0, 0, a); \
                               CK(launch_series_reduce(partials, F, a.n_tiles, false, series, 0)); }, {}, "PF=" #PF " tau=8.0f"}); \
     }
-#define SERIES_V2U(PF, U) SERIES_V2X(PF, U, 8.0f, 0)
-#define SERIES_V2X(PF, U, TAU255, SK)                                                                             \
+#define SERIES_V2U(PF, U) SERIES_V2X(PF, U, 8.0f)
+#define SERIES_V2X(PF, U, TAU255)                                                                             \
     {                                                                                                 \
         SeriesArgs a; uint32_t blocks; int occ;                                                       \
-        const void* k = (const void*)&series_v2_kernel<3, 0, U, PF, false, SK>;                           \
+        const void* k = (const void*)&series_v2_kernel<3, 0, U, PF, false>;                           \
         geom(12, U, k, a, blocks, occ);                                                               \
         a.partials = partials;                                                                        \
         a.thr = series_threshold(3, TAU255 / 255.0f);                                                 \
-        vs.push_back({"v2<U=" #U ",PF=" #PF ",SK=" #SK "> tau=" #TAU255 "/255 occ=" + std::to_string(occ) + " waves=" + std::to_string(a.n_waves), \
-                      [=]() { hipLaunchKernelGGL((series_v2_kernel<3, 0, U, PF, false, SK>), dim3(blocks), dim3(256), 0, 0, a); \
+        vs.push_back({"v2<U=" #U ",PF=" #PF "> tau=" #TAU255 "/255 occ=" + std::to_string(occ) + " waves=" + std::to_string(a.n_waves), \
+                      [=]() { hipLaunchKernelGGL((series_v2_kernel<3, 0, U, PF, false>), dim3(blocks), dim3(256), 0, 0, a); \
                               CK(launch_series_reduce(partials, F, a.n_tiles, false, series, 0)); }, {}, "PF=" #PF " tau=" #TAU255}); \
     }
 #define SERIES_V2(PF) SERIES_V2U(PF, kUnrollV2)
@@ -180,9 +180,7 @@ int main(int argc, char** argv) {
     SERIES_V2(true)
     SERIES(4, 2, false)
     SERIES_V2(false)
-    SERIES_V2X(true, kUnrollV2, 0.0f, 0)
-    SERIES_V2X(true, kUnrollV2, 8.0f, 1)
-    SERIES_V2X(true, kUnrollV2, 0.0f, 1)
+    SERIES_V2X(true, kUnrollV2, 0.0f)
 
     if (argc > 3) {  // substring filter on variant names
         std::vector<Variant> keep;
