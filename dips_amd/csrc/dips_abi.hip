@@ -15,6 +15,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -539,6 +540,30 @@ dips_status dips_diff_series(dips_handle* h, uint32_t width, uint32_t height, co
     return DIPS_OK;
 }
 
+// Host -> pinned staging copy split over several threads: one thread's
+// memcpy from pageable memory runs well below the PCIe DMA rate.
+static void staged_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
+    const size_t kMinPerThread = 8u << 20;
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt == 0 ? 1u : (nt > 8u ? 8u : nt);
+    if (bytes < 2 * kMinPerThread || nt == 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    if ((size_t)nt > bytes / kMinPerThread) nt = (unsigned)(bytes / kMinPerThread);
+    const size_t per = (bytes / nt + 63) & ~(size_t)63;
+    std::vector<std::thread> pool;
+    pool.reserve(nt - 1);
+    for (unsigned i = 1; i < nt; ++i) {
+        const size_t o = per * i;
+        if (o >= bytes) break;
+        const size_t len = o + per <= bytes ? per : bytes - o;
+        pool.emplace_back([=]() { std::memcpy(dst + o, src + o, len); });
+    }
+    std::memcpy(dst, src, per < bytes ? per : bytes);
+    for (auto& t : pool) t.join();
+}
+
 dips_status dips_diff_series_streamed(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* host_frames,
                                       uint32_t n_frames, const uint8_t* host_ref, dips_series_entry* series,
                                       uint32_t chunk_frames) {
@@ -577,7 +602,7 @@ dips_status dips_diff_series_streamed(dips_handle* h, uint32_t width, uint32_t h
         const uint32_t nk = (f0 + chunk <= n_frames) ? chunk : n_frames - f0;
         // pinned[hb] was last read by the DMA of chunk k-2
         if (k >= 2) DIPS_HIP(h, hipEventSynchronize(h->copy_done[(k - 2) % 3u]));
-        std::memcpy(h->pinned[hb].p, host_frames + (size_t)f0 * fb, (size_t)nk * fb);
+        staged_copy(static_cast<uint8_t*>(h->pinned[hb].p), host_frames + (size_t)f0 * fb, (size_t)nk * fb);
         // ring[b] was read by kernel k-3 (frames) and kernel k-2 (per-frame ref)
         if (k >= 2) DIPS_HIP(h, hipStreamWaitEvent(h->copy_stream, h->kernel_done[(k - 2) % 3u], 0));
         DIPS_HIP(h, hipMemcpyAsync(h->ring[b].p, h->pinned[hb].p, (size_t)nk * fb, hipMemcpyHostToDevice, h->copy_stream));
