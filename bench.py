@@ -220,7 +220,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": f"series_v2_kernel<3,0,2,{'true' if mode == Mode.PerFrame else 'false'},false>",
+                "kernel": f"series_v2_kernel<3,0,4,{'true' if mode == Mode.PerFrame else 'false'},false>",
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "partial_bytes_per_launch": int(pbytes) * F,

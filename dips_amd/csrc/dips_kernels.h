@@ -11,7 +11,7 @@ namespace dips {
 // Unroll (vecs per lane) of the fast series kernel; a tile = 64 * U vecs.
 constexpr int kUnrollRGB = 4;   // 1024 px / wave / frame for RGB8 and RGBA8
 constexpr int kUnrollGray = 2;  // 2048 px / wave / frame for GRAY8
-constexpr int kUnrollV2 = 2;    // series_v2_kernel (RGB8/RGBA8): 512 px / wave / frame
+constexpr int kUnrollV2 = 4;    // series_v2_kernel (RGB8/RGBA8): 1024 px / wave / frame
 // Prefetch depth: frames of loads each wave keeps in flight.
 #ifndef DIPS_DEPTH_RGB
 #define DIPS_DEPTH_RGB 2

@@ -18,8 +18,10 @@
 //  * a 4-slot register ring of frame vecs, rotated by unrolling four frames,
 //    so the bytes of frame t double as the SAD reference of frame t+1 with no
 //    register copies (the previous kernel spent ~10% of its VALU on v_mov);
-//  * U = 2 vecs per lane: <= 64 VGPRs, 8 waves per SIMD -- the VALU classes
-//    this kernel uses issue 20-35% faster at 8 waves than at 4 (vbench);
+//  * U = 4 vecs per lane (1024 px per wave and frame), 96 VGPRs, 5 waves
+//    per SIMD: measured against U = 2 at 8 waves and U = 3 at 6 waves, the
+//    per-frame reduction amortised over more pixels wins by 1.5 % and halves
+//    the partial records;
 //  * the two frames of a pair are reduced together and their 8 wave sums are
 //    stored straight from the lanes that hold them (no v_readlane).
 #include "series_common.h"
@@ -161,11 +163,11 @@ __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t
 // per-frame kernel fits 64 VGPRs (8 waves) without spilling; the other
 // variants hold more state (fixed reference bytes, RGBA vecs, map stores) and
 // keep their natural allocation (5-7 waves).
-template <int C, bool PF, bool MAP>
-constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? 8 : 1; }
+template <int C, int U, bool PF, bool MAP>
+constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : 5)) : 1; }
 
 template <int C, int CH, int U, bool PF, bool MAP>
-__global__ __launch_bounds__(256, (v2_min_waves<C, PF, MAP>())) void series_v2_kernel(SeriesArgs a) {
+__global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v2_kernel(SeriesArgs a) {
     using F = Fmt<C>;
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;

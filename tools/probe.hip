@@ -181,6 +181,8 @@ int main(int argc, char** argv) {
     SERIES(4, 2, false)
     SERIES_V2(false)
     SERIES_V2X(true, kUnrollV2, 0.0f)
+    SERIES_V2U(true, 2)
+    SERIES_V2U(true, 3)
 
     if (argc > 3) {  // substring filter on variant names
         std::vector<Variant> keep;
