@@ -59,6 +59,18 @@ class DipsParams(ctypes.Structure):
     ]
 
 
+class DipsAltParams(ctypes.Structure):
+    _fields_ = [
+        ("colorize", ctypes.c_uint8),
+        ("window_size", ctypes.c_int32),
+        ("sigmoid_horizontal_scalar", ctypes.c_float),
+        ("filter_type", ctypes.c_uint32),
+        ("chroma_filter", ctypes.c_uint32),
+        ("num_textures", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+    ]
+
+
 class SeriesEntry(ctypes.Structure):
     _fields_ = [
         ("sad", ctypes.c_uint64),
@@ -139,6 +151,18 @@ def load() -> ctypes.CDLL:
             "dips_kernel_time": ([_vp, P(ctypes.c_double), P(u64)], st),
             "dips_kernel_time_reset": ([_vp], st),
             "dips_series_geometry": ([_vp, u32, u32, u32, P(u64), P(u64), P(u64)], st),
+            "dips_alt_params_default": ([P(DipsAltParams)], st),
+            "dips_alt_create": ([P(DipsAltParams), u32, u32, st, P(_vp)], st),
+            "dips_alt_destroy": ([_vp], None),
+            "dips_alt_last_error": ([_vp], ctypes.c_char_p),
+            "dips_alt_set_stream": ([_vp, _vp], st),
+            "dips_alt_synchronize": ([_vp], st),
+            "dips_alt_send_frame": ([_vp, _u8p, ctypes.c_size_t, st, _u8p, ctypes.c_size_t], st),
+            "dips_alt_send_frames": ([_vp, _u8p, u32, _u8p, _u8p], st),
+            "dips_alt_run": ([_vp, _u8p, u32, _vp, u32, _u8p], st),
+            "dips_alt_snapshot_texture": ([_vp, _u8p, ctypes.c_size_t], st),
+            "dips_alt_kernel_time": ([_vp, P(ctypes.c_double), P(u64)], st),
+            "dips_alt_kernel_time_reset": ([_vp], st),
         }
         del i32, f32
         for name, (args, res) in sig.items():
@@ -153,5 +177,13 @@ def check(status: int, handle=None) -> int:
     if status < 0:
         lib = load()
         msg = lib.dips_last_error(handle)
+        raise DipsError(status, msg.decode() if msg else "")
+    return status
+
+
+def check_alt(status: int, handle=None) -> int:
+    if status < 0:
+        lib = load()
+        msg = lib.dips_alt_last_error(handle)
         raise DipsError(status, msg.decode() if msg else "")
     return status

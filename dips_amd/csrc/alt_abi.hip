@@ -1,0 +1,478 @@
+// alt_abi.hip -- host side of the dips_alt operator's C ABI (include/dips_hip.h,
+// "dips_alt operator").  The handle plays DiPsCompute
+// (dips_alt/src/dips_compute/mod.rs:243-267: texture slots, texture_index,
+// snapshot texture, output) plus the loop state of run_dips_on_file
+// (dips_alt/src/lib.rs:566-567: index, overall_frame).  No exception leaves
+// this file; every entry point returns a dips_status.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/dips_hip.h"
+#include "dips_kernels.h"
+#include "host_buffers.h"
+
+namespace {
+
+using dips_host::DevBuf;
+using dips_host::HostPinned;
+
+std::mutex g_alt_err_mu;
+std::string g_alt_create_err;
+
+constexpr uint64_t kFrameCount = 2;  // FRAME_COUNT, dips_alt/src/lib.rs:36
+
+}  // namespace
+
+struct dips_alt_handle {
+    dips_alt_params p{};
+    int device = 0;
+    int cu_count = 0;
+    uint32_t width = 0, height = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    DevBuf slots[dips::kAltMaxTextures];  // input_textures (mod.rs:279-301)
+    DevBuf snap[2];                       // snapshot texture (.r), double-buffered for the batch kernel
+    int cur = 0;                          // snap[cur] is the snapshot texture
+    uint64_t sent = 0;                    // frames sent; texture_index = sent % N (mod.rs:494, 523)
+    uint64_t index = 0, overall = 0;      // run_dips_on_file loop state (lib.rs:566-567)
+
+    DevBuf out1, stage_frames, stage_out, meta;
+    HostPinned io;
+    std::vector<uint8_t> meta_host;
+    hipEvent_t meta_done = nullptr;
+    bool meta_pending = false;
+    int occupancy = 0;
+
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    std::vector<hipEvent_t> ev_free;
+    double t_ms = 0.0;
+    uint64_t t_launches = 0;
+
+    size_t frame_bytes() const { return (size_t)width * height * 4u; }
+    size_t n_px() const { return (size_t)width * height; }
+};
+
+namespace {
+
+dips_status fail(dips_alt_handle* h, dips_status st, const std::string& msg) {
+    if (h) h->err = msg;
+    return st;
+}
+
+dips_status hip_fail(dips_alt_handle* h, hipError_t e, const char* what) {
+    return fail(h, e == hipErrorOutOfMemory ? DIPS_ERR_NOMEM : DIPS_ERR_HIP,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define ALT_HIP(h, call)                                        \
+    do {                                                        \
+        hipError_t e_ = (call);                                 \
+        if (e_ != hipSuccess) return hip_fail((h), e_, #call); \
+    } while (0)
+
+dips_status bind(dips_alt_handle* h) {
+    if (!h) return DIPS_ERR_INVALID;
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
+    return DIPS_OK;
+}
+
+dips_status validate(const dips_alt_params* p, uint32_t w, uint32_t hgt, std::string* why) {
+    if (p->num_textures < 1 || p->num_textures > (uint32_t)dips::kAltMaxTextures) {
+        *why = "num_textures must be in [1, 16] (MAX_TEMPORAL_ARRAY_SIZE, dips_alt pre_compute_shader.wgsl:12)";
+        return DIPS_ERR_INVALID;
+    }
+    if (p->window_size < 1 || p->window_size > 11) {
+        *why = "window_size must be in [1, 11] (MAX_WIN_SIZE_SQUARE = 11*11, pre_compute_shader.wgsl:28)";
+        return DIPS_ERR_INVALID;
+    }
+    if (p->chroma_filter > 3u) {
+        *why = "chroma_filter must be 0..3 (dips_alt/src/dips_compute/mod.rs:158-165)";
+        return DIPS_ERR_INVALID;
+    }
+    if (!std::isfinite(p->sigmoid_horizontal_scalar)) {
+        *why = "sigmoid_horizontal_scalar must be finite";
+        return DIPS_ERR_INVALID;
+    }
+    if (w == 0 || hgt == 0) {
+        *why = "width and height must be non-zero";
+        return DIPS_ERR_INVALID;
+    }
+    if ((uint64_t)w * hgt * 4u >= (1ull << 31)) {
+        *why = "frame larger than 2 GiB";
+        return DIPS_ERR_INVALID;
+    }
+    return DIPS_OK;
+}
+
+hipEvent_t take_event(dips_alt_handle* h) {
+    if (!h->ev_free.empty()) {
+        hipEvent_t e = h->ev_free.back();
+        h->ev_free.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+bool fast_eligible(const dips_alt_handle* h, const uint8_t* frames, const uint8_t* out) {
+    auto a16 = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+    return h->p.num_textures == 2 && h->p.window_size == 1 && !(h->p.flags & DIPS_FLAG_FORCE_GENERIC) &&
+           h->n_px() % 4u == 0 && a16(frames) && a16(out);
+}
+
+// Slot k's content at global frame g (the latest frame G <= g with
+// G = k mod N): a batch frame if G >= sent, else the slot buffer.
+const uint8_t* slot_at(const dips_alt_handle* h, const uint8_t* frames, uint64_t g, uint32_t k) {
+    const uint64_t N = h->p.num_textures;
+    const uint64_t back = (g + N - k) % N;  // (g - k) mod N, k < N
+    if (back <= g && g - back >= h->sent) return frames + (size_t)(g - back - h->sent) * h->frame_bytes();
+    return h->slots[k].as<uint8_t>();
+}
+
+dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags, uint8_t* out,
+                     hipStream_t s) {
+    const void* k = dips::alt_batch_kernel_ptr((int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0);
+    if (!k) return fail(h, DIPS_ERR_INVALID, "no batch kernel for these parameters");
+    if (h->occupancy == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess || nb < 1) nb = 1;
+        h->occupancy = nb;
+    }
+    const uint64_t n_vec = h->n_px() / 4u;
+    const uint64_t n_tiles = (n_vec + 64u * dips::kUnrollAlt - 1) / (64u * dips::kUnrollAlt);
+    const uint64_t resident = (uint64_t)h->occupancy * 4u * (uint64_t)h->cu_count;
+    // chunks of >= 16 frames; enough (tile, chunk) items to fill the chip
+    uint64_t n_chunks = (resident + n_tiles - 1) / n_tiles;
+    n_chunks = std::min<uint64_t>(n_chunks, (n + 15u) / 16u);
+    n_chunks = std::max<uint64_t>(n_chunks, 1);
+    const uint32_t chunk = (uint32_t)((n + n_chunks - 1) / n_chunks);
+    n_chunks = (n + chunk - 1) / chunk;
+    if (n_tiles * n_chunks >= (1ull << 31)) return fail(h, DIPS_ERR_INVALID, "batch too large; split it");
+
+    // per-frame flags and per-chunk "last snapshot before the chunk"
+    const size_t flag_bytes = ((size_t)n + 3u) & ~(size_t)3u;
+    if (h->meta_pending) {
+        ALT_HIP(h, hipEventSynchronize(h->meta_done));
+        h->meta_pending = false;
+    }
+    h->meta_host.assign(flag_bytes + 4u * n_chunks, 0);
+    int32_t last = -1;
+    std::vector<int32_t> cs(n_chunks, -1);
+    for (uint32_t t = 0; t < n; ++t) {
+        if (t % chunk == 0) cs[t / chunk] = last;
+        const uint8_t f = flags && flags[t] ? 1 : 0;
+        h->meta_host[t] = f;
+        if (f) last = (int32_t)t;
+    }
+    std::memcpy(h->meta_host.data() + flag_bytes, cs.data(), 4u * n_chunks);
+    ALT_HIP(h, h->meta.ensure(h->meta_host.size()));
+    ALT_HIP(h, hipMemcpyAsync(h->meta.p, h->meta_host.data(), h->meta_host.size(), hipMemcpyHostToDevice, s));
+    ALT_HIP(h, hipEventRecord(h->meta_done, s));
+    h->meta_pending = true;
+
+    dips::AltBatchArgs a{};
+    a.frames = frames;
+    a.prev0 = h->slots[(h->sent + 1u) % 2u].as<uint8_t>();
+    a.snap_in = h->snap[h->cur].as<uint8_t>();
+    a.snap_out = h->snap[1 - h->cur].as<uint8_t>();
+    a.out = out;
+    a.flags = h->meta.as<uint8_t>();
+    a.chunk_snap = reinterpret_cast<const int32_t*>(h->meta.as<uint8_t>() + flag_bytes);
+    a.frame_bytes = (uint32_t)h->frame_bytes();
+    a.n_vec = (uint32_t)n_vec;
+    a.n_frames = n;
+    a.chunk = chunk;
+    a.n_chunks = (uint32_t)n_chunks;
+    a.n_tiles = (uint32_t)n_tiles;
+    a.last_snap = last;
+    a.scalar = h->p.sigmoid_horizontal_scalar;
+    const uint32_t blocks = (uint32_t)((n_tiles * n_chunks + 3u) / 4u);
+
+    const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
+        ALT_HIP(h, hipEventRecord(e0, s));
+    }
+    ALT_HIP(h, dips::launch_alt_batch(a, (int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0,
+                                      blocks, s));
+    if (timing) {
+        ALT_HIP(h, hipEventRecord(e1, s));
+        h->ev_pending.emplace_back(e0, e1);
+    }
+    if (last >= 0) h->cur = 1 - h->cur;
+    return DIPS_OK;
+}
+
+dips_status run_generic(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags, uint8_t* out,
+                        hipStream_t s) {
+    dips::AltArgs a{};
+    a.width = h->width;
+    a.height = h->height;
+    a.n_tex = h->p.num_textures;
+    a.window = h->p.window_size;
+    a.chroma = h->p.chroma_filter;
+    a.filter = h->p.filter_type;
+    a.scalar = h->p.sigmoid_horizontal_scalar;
+    a.colorize = h->p.colorize ? 1u : 0u;
+    a.snap = h->snap[h->cur].as<uint8_t>();
+    for (uint32_t t = 0; t < n; ++t) {
+        const uint64_t g = h->sent + t;
+        for (uint32_t k = 0; k < h->p.num_textures; ++k) a.slots[k] = slot_at(h, frames, g, k);
+        a.snapshot = flags && flags[t] ? 1u : 0u;
+        a.out = out + (size_t)t * h->frame_bytes();
+        ALT_HIP(h, dips::launch_alt_frame(a, s));
+    }
+    return DIPS_OK;
+}
+
+// n consecutive send_frame calls on device pointers, asynchronous on s.
+dips_status send_frames_device(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags,
+                               uint8_t* out, hipStream_t s) {
+    if (n == 0) return DIPS_OK;
+    dips_status st = fast_eligible(h, frames, out) ? run_fast(h, frames, n, flags, out, s)
+                                                   : run_generic(h, frames, n, flags, out, s);
+    if (st != DIPS_OK) return st;
+    // the texture slots now hold the batch's last N frames (write_texture, mod.rs:510-521)
+    const uint64_t N = h->p.num_textures;
+    const uint64_t end = h->sent + n;
+    const uint64_t beg = end > h->sent + N ? end - N : h->sent;
+    for (uint64_t G = std::max(beg, h->sent); G < end; ++G)
+        ALT_HIP(h, hipMemcpyAsync(h->slots[G % N].p, frames + (size_t)(G - h->sent) * h->frame_bytes(),
+                                  h->frame_bytes(), hipMemcpyDeviceToDevice, s));
+    h->sent = end;
+    return DIPS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+dips_status dips_alt_params_default(dips_alt_params* p) {
+    if (!p) return DIPS_ERR_INVALID;
+    std::memset(p, 0, sizeof(*p));
+    p->colorize = 1;
+    p->window_size = 1;
+    p->sigmoid_horizontal_scalar = 5.0f;
+    p->filter_type = DIPS_FILTER_SIGMOID;
+    p->chroma_filter = DIPS_CHROMA_NONE;
+    p->num_textures = (uint32_t)kFrameCount;
+    p->flags = 0;
+    return DIPS_OK;
+}
+
+dips_status dips_alt_create(const dips_alt_params* params, uint32_t width, uint32_t height, int device,
+                            dips_alt_handle** out) {
+    if (!out) return DIPS_ERR_INVALID;
+    *out = nullptr;
+    dips_alt_params p;
+    if (params) p = *params;
+    else dips_alt_params_default(&p);
+    std::string why;
+    if (validate(&p, width, height, &why) != DIPS_OK) {
+        std::lock_guard<std::mutex> lk(g_alt_err_mu);
+        g_alt_create_err = why;
+        return DIPS_ERR_INVALID;
+    }
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count <= 0 || device < 0 || device >= count) {
+        std::lock_guard<std::mutex> lk(g_alt_err_mu);
+        g_alt_create_err = std::string("no HIP device ") + std::to_string(device) + " (" +
+                           (e == hipSuccess ? std::to_string(count) + " visible" : hipGetErrorString(e)) + ")";
+        return DIPS_ERR_NODEVICE;
+    }
+    dips_alt_handle* h = new (std::nothrow) dips_alt_handle();
+    if (!h) return DIPS_ERR_NOMEM;
+    h->p = p;
+    h->device = device;
+    h->width = width;
+    h->height = height;
+    e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&h->cu_count, hipDeviceAttributeMultiprocessorCount, device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->meta_done, hipEventDisableTiming);
+    // wgpu zero-initialises textures: slots, snapshot and output start at 0
+    for (uint32_t k = 0; k < p.num_textures && e == hipSuccess; ++k) {
+        e = h->slots[k].ensure(h->frame_bytes());
+        if (e == hipSuccess) e = hipMemsetAsync(h->slots[k].p, 0, h->frame_bytes(), h->own_stream);
+    }
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+        e = h->snap[k].ensure(h->n_px());
+        if (e == hipSuccess) e = hipMemsetAsync(h->snap[k].p, 0, h->n_px(), h->own_stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(h->own_stream);
+    if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_alt_err_mu);
+        g_alt_create_err = std::string("HIP initialisation failed: ") + hipGetErrorString(e);
+        dips_alt_destroy(h);
+        return e == hipErrorOutOfMemory ? DIPS_ERR_NOMEM : DIPS_ERR_HIP;
+    }
+    h->stream = h->own_stream;
+    *out = h;
+    return DIPS_OK;
+}
+
+void dips_alt_destroy(dips_alt_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (auto& pr : h->ev_pending) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    for (auto e : h->ev_free) (void)hipEventDestroy(e);
+    if (h->meta_done) (void)hipEventDestroy(h->meta_done);
+    for (auto& s : h->slots) s.release();
+    for (auto& s : h->snap) s.release();
+    h->out1.release();
+    h->stage_frames.release();
+    h->stage_out.release();
+    h->meta.release();
+    h->io.release();
+    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    delete h;
+}
+
+const char* dips_alt_last_error(const dips_alt_handle* h) {
+    if (h) return h->err.c_str();
+    std::lock_guard<std::mutex> lk(g_alt_err_mu);
+    return g_alt_create_err.c_str();
+}
+
+dips_status dips_alt_set_stream(dips_alt_handle* h, void* stream) {
+    if (!h) return DIPS_ERR_INVALID;
+    h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+    return DIPS_OK;
+}
+
+dips_status dips_alt_synchronize(dips_alt_handle* h) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    ALT_HIP(h, hipStreamSynchronize(h->stream));
+    return DIPS_OK;
+}
+
+dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t len, int snapshot, uint8_t* out,
+                                size_t cap) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    const size_t fb = h->frame_bytes();
+    if (!frame || len != fb) return fail(h, DIPS_ERR_INVALID, "send_frame: len != width*height*4 (RGBA8, stride width*4)");
+    if (!out || cap < fb) return fail(h, DIPS_ERR_CAPACITY, "send_frame: output buffer smaller than width*height*4");
+    ALT_HIP(h, h->io.ensure(fb));
+    ALT_HIP(h, h->out1.ensure(fb));
+    ALT_HIP(h, hipStreamSynchronize(h->stream));
+    std::memcpy(h->io.p, frame, fb);
+    // queue.write_texture into slot texture_index, then texture_index += 1
+    const uint32_t N = h->p.num_textures;
+    uint8_t* slot = h->slots[h->sent % N].as<uint8_t>();
+    ALT_HIP(h, hipMemcpyAsync(slot, h->io.p, fb, hipMemcpyHostToDevice, h->stream));
+    h->sent += 1;
+    dips::AltArgs a{};
+    for (uint32_t k = 0; k < N; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
+    a.snap = h->snap[h->cur].as<uint8_t>();
+    a.out = h->out1.as<uint8_t>();
+    a.width = h->width;
+    a.height = h->height;
+    a.n_tex = N;
+    a.window = h->p.window_size;
+    a.chroma = h->p.chroma_filter;
+    a.filter = h->p.filter_type;
+    a.scalar = h->p.sigmoid_horizontal_scalar;
+    a.colorize = h->p.colorize ? 1u : 0u;
+    a.snapshot = snapshot ? 1u : 0u;
+    ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
+    // copy_texture_to_buffer + map_async + de-pad (mod.rs:597-643)
+    ALT_HIP(h, hipMemcpyAsync(h->io.p, h->out1.p, fb, hipMemcpyDeviceToHost, h->stream));
+    ALT_HIP(h, hipStreamSynchronize(h->stream));
+    std::memcpy(out, h->io.p, fb);
+    return DIPS_OK;
+}
+
+dips_status dips_alt_send_frames(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags,
+                                 uint8_t* out) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (n == 0) return DIPS_OK;
+    if (!frames || !out) return fail(h, DIPS_ERR_INVALID, "send_frames: null frames or output");
+    if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) return send_frames_device(h, frames, n, flags, out, h->stream);
+    const size_t total = h->frame_bytes() * (size_t)n;
+    ALT_HIP(h, h->stage_frames.ensure(total));
+    ALT_HIP(h, h->stage_out.ensure(total));
+    ALT_HIP(h, hipMemcpyAsync(h->stage_frames.p, frames, total, hipMemcpyHostToDevice, h->stream));
+    st = send_frames_device(h, h->stage_frames.as<uint8_t>(), n, flags, h->stage_out.as<uint8_t>(), h->stream);
+    if (st != DIPS_OK) return st;
+    ALT_HIP(h, hipMemcpyAsync(out, h->stage_out.p, total, hipMemcpyDeviceToHost, h->stream));
+    ALT_HIP(h, hipStreamSynchronize(h->stream));
+    return DIPS_OK;
+}
+
+dips_status dips_alt_run(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint64_t* markers,
+                         uint32_t n_markers, uint8_t* out) {
+    if (!h) return DIPS_ERR_INVALID;
+    if (n_markers && !markers) return fail(h, DIPS_ERR_INVALID, "run: null refresh markers");
+    std::vector<uint8_t> flags(n);
+    for (uint32_t t = 0; t < n; ++t) {
+        flags[t] = h->index == kFrameCount ? 1 : 0;  // match index { FRAME_COUNT => Some(()) } (lib.rs:636-639)
+        if (h->index <= kFrameCount) h->index += 1;  // lib.rs:662-664
+        h->overall += 1;                             // lib.rs:666
+        for (uint32_t k = 0; k < n_markers; ++k)     // refresh_markers.contains (lib.rs:668-670)
+            if (markers[k] == h->overall) {
+                h->index = 0;
+                break;
+            }
+    }
+    return dips_alt_send_frames(h, frames, n, flags.data(), out);
+}
+
+dips_status dips_alt_snapshot_texture(dips_alt_handle* h, uint8_t* out, size_t cap) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!out || cap < h->n_px()) return fail(h, DIPS_ERR_CAPACITY, "snapshot_texture: output smaller than width*height");
+    ALT_HIP(h, hipMemcpyAsync(out, h->snap[h->cur].p, h->n_px(), hipMemcpyDeviceToHost, h->stream));
+    ALT_HIP(h, hipStreamSynchronize(h->stream));
+    return DIPS_OK;
+}
+
+dips_status dips_alt_kernel_time(dips_alt_handle* h, double* total_ms, uint64_t* launches) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    for (auto& pr : h->ev_pending) {
+        ALT_HIP(h, hipEventSynchronize(pr.second));
+        float ms = 0.0f;
+        ALT_HIP(h, hipEventElapsedTime(&ms, pr.first, pr.second));
+        h->t_ms += ms;
+        h->t_launches += 1;
+        h->ev_free.push_back(pr.first);
+        h->ev_free.push_back(pr.second);
+    }
+    h->ev_pending.clear();
+    if (total_ms) *total_ms = h->t_ms;
+    if (launches) *launches = h->t_launches;
+    return DIPS_OK;
+}
+
+dips_status dips_alt_kernel_time_reset(dips_alt_handle* h) {
+    dips_status st = dips_alt_kernel_time(h, nullptr, nullptr);
+    if (st != DIPS_OK) return st;
+    h->t_ms = 0.0;
+    h->t_launches = 0;
+    return DIPS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,339 @@
+// alt_kernels.hip -- the dips_alt operator (DiPsCompute) on gfx950, SURVEY.md
+// s8f next-4: a snapshot reference, an N-slot temporal "median" and the
+// DIFF_SCALE epilogue (dips_alt/src/dips_compute/shaders/pre_compute_shader.wgsl,
+// host side dips_alt/src/dips_compute/mod.rs:498-646, driver loop
+// dips_alt/src/lib.rs:588-683).
+//
+//   alt_frame_kernel<N>   one send_frame dispatch (pre_compute_main :188-263)
+//                         for any N = num_textures in 1..16 and any spatial
+//                         window; W > 1 stages the intensity neighbourhood of
+//                         the 16x16 tile in LDS.
+//   alt_batch_kernel      a whole run of HBM-resident frames for N = 2, W = 1,
+//                         the configuration dips_alt runs (FRAME_COUNT = 2,
+//                         lib.rs:36; window_size 1, mod.rs:176-186).  A wave
+//                         owns a tile of pixels and walks a range of frames;
+//                         the previous frame's intensities and the snapshot
+//                         stay in registers, so a frame costs its 4 B/px read
+//                         plus the 4 B/px output write and nothing else.
+//
+// Numerics: the temporal sort of n values in a zero-filled 16-entry array,
+// element [n/2] (:212-227, :232, :238), is sorted(v + {0})[n/2] for n < 16
+// (one trailing zero inside the sorted range) and sorted(v)[8] for n = 16
+// (index 16 clamped to 15 by naga's Restrict policy).  Intensities are >= 0,
+// so for n = 2 it is min(v0, v1) and for n = 1 it is 0.
+#include "intensity_v2.h"
+
+namespace dips {
+
+namespace {
+
+constexpr int kTile = 16;
+constexpr int kMaxHalo = 5;                 // window <= 11
+constexpr int kLds = kTile + 2 * kMaxHalo;  // 26
+
+__device__ __forceinline__ float alt_texel_intensity(const uint8_t* img, uint64_t p, uint32_t chroma) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(img + 4 * p);
+    return intensity_rgb(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, chroma);
+}
+
+// Intensities of this workgroup's tile plus a halo of `halo` texels; texels
+// outside the frame are 0.0 (pre_compute_shader.wgsl:148-150).
+__device__ void alt_stage_tile(float (*tile)[kLds], const uint8_t* img, uint32_t w, uint32_t h, int halo,
+                               uint32_t chroma) {
+    const int ox = (int)(blockIdx.x * kTile) - halo;
+    const int oy = (int)(blockIdx.y * kTile) - halo;
+    const int span = kTile + 2 * halo;
+    for (int idx = threadIdx.y * kTile + threadIdx.x; idx < span * span; idx += kTile * kTile) {
+        const int ty = idx / span, tx = idx - ty * span;
+        const int gx = ox + tx, gy = oy + ty;
+        float v = 0.0f;
+        if (gx >= 0 && gy >= 0 && gx < (int)w && gy < (int)h) v = alt_texel_intensity(img, (uint64_t)gy * w + gx, chroma);
+        tile[ty][tx] = v;
+    }
+}
+
+// dips_alt spatial_median_filter for W > 1 (:141-184): the W^2-entry sort
+// holds the (2h)^2 window values (offsets [-h, h) on both axes) and
+// W^2 - (2h)^2 zeros; the result is element W^2/2 + 1.  All values are >= 0,
+// so that element is 0 while it falls among the zeros, otherwise the
+// (k - zeros)-th smallest window value.
+__device__ float alt_window_select(float (*tile)[kLds], int window) {
+    const int hw = window / 2;
+    const int side = 2 * hw;
+    const int n = side * side;
+    const int ws2 = window * window;
+    const int zeros = ws2 - n;
+    const int k = ws2 / 2 + 1;
+    if (k < zeros) return 0.0f;
+    const int kk = k - zeros;
+    const int tx = threadIdx.x, ty = threadIdx.y;
+    for (int c = 0; c < n; ++c) {
+        const float vc = tile[ty + c / side][tx + c % side];
+        int rank = 0;
+        for (int j = 0; j < n; ++j) {
+            const float vj = tile[ty + j / side][tx + j % side];
+            rank += (vj < vc || (vj == vc && j < c)) ? 1 : 0;
+        }
+        if (rank == kk) return vc;
+    }
+    return 0.0f;  // unreachable
+}
+
+// Element [n/2] of the sorted zero-padded temporal array (see file comment).
+template <int N>
+__device__ __forceinline__ float alt_temporal(const float (&v)[N]) {
+    if constexpr (N == 1) {
+        return 0.0f;
+    } else if constexpr (N == 2) {
+        return fminf(v[0], v[1]);
+    } else {
+        constexpr int kk = N == kAltMaxTextures ? N / 2 : N / 2 - 1;  // rank among v
+        float r = 0.0f;
+#pragma unroll
+        for (int c = 0; c < N; ++c) {
+            int rank = 0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) rank += (v[j] < v[c] || (v[j] == v[c] && j < c)) ? 1 : 0;
+            r = rank == kk ? v[c] : r;
+        }
+        return r;
+    }
+}
+
+__device__ __forceinline__ uint32_t gray_rgba(uint32_t s) { return s | (s << 8) | (s << 16) | (255u << 24); }
+
+template <int N>
+__global__ __launch_bounds__(256) void alt_frame_kernel(AltArgs a) {
+    __shared__ float tile[kLds][kLds];
+    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
+    const uint32_t y = blockIdx.y * kTile + threadIdx.y;
+    const bool inside = x < a.width && y < a.height;
+    const uint64_t p = (uint64_t)y * a.width + x;
+    float v[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        // median_array[k] = spatial_median_filter(coords, dims, k)
+        // (the generated array, dynamic_texture_array.rs:67-69)
+        if (a.window == 1) {
+            v[k] = inside ? alt_texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
+        } else {
+            __syncthreads();
+            alt_stage_tile(tile, a.slots[k], a.width, a.height, a.window / 2, a.chroma);
+            __syncthreads();
+            v[k] = inside ? alt_window_select(tile, a.window) : 0.0f;
+        }
+    }
+    if (!inside) return;
+    const float med = alt_temporal<N>(v);
+    uint32_t o;
+    if (a.snapshot) {
+        // snapshot == 1: store the intensity into the snapshot and the output
+        // texture (:231-235)
+        const uint32_t s = unorm_store(med);
+        a.snap[p] = (uint8_t)s;
+        o = gray_rgba(s);
+    } else {
+        // textureLoad(snapshot_texture).r - median, then map / filter /
+        // DIFF_SCALE / colour (:237-261)
+        o = visual_epilogue(unorm_load(a.snap[p]) - med, a.filter, a.scalar, a.colorize != 0u);
+    }
+    *reinterpret_cast<uint32_t*>(a.out + 4 * p) = o;
+}
+
+// ---------------------------------------------------------------------------
+// Batch kernel (N = 2, W = 1, RGBA8)
+// ---------------------------------------------------------------------------
+
+template <int U>
+struct AltTile {
+    uint32_t voff[U];  // byte offset of the lane's vec u inside a frame
+};
+
+template <int CH, int U>
+__device__ __forceinline__ void alt_intensity(const uint8_t* frame, uint32_t fb, const AltTile<U>& tl,
+                                              f32x2 (&dst)[U][2]) {
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(frame, fb);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        uint32_t d[4];
+        load_vec<4>(r, tl.voff[u], d);
+        St2 s;
+        derive_v2<4, CH>(d, s);
+        dst[u][0] = s.i[0];
+        dst[u][1] = s.i[1];
+    }
+}
+
+template <int CH, int FILT, int COL, int U>
+__global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (item >= a.n_tiles * a.n_chunks) return;
+    const uint32_t c = item / a.n_tiles;
+    const uint32_t tile = item - c * a.n_tiles;
+    const uint32_t t0 = c * a.chunk;
+    const uint32_t t1 = min(t0 + a.chunk, a.n_frames);
+    const uint32_t fb = a.frame_bytes;
+    AltTile<U> tl;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        // vecs past the frame end read as 0 and their stores are dropped
+        // (buffer range checking), so a ragged last tile needs no branch
+        const uint32_t vec = (tile * U + (uint32_t)u) * 64u + lane;
+        tl.voff[u] = vec < a.n_vec ? vec * 16u : 0x80000000u;
+    }
+
+    // intensities of the previous frame (slot (g+1) mod 2 holds it)
+    f32x2 prev[U][2];
+    alt_intensity<CH, U>(t0 == 0 ? a.prev0 : a.frames + (uint64_t)(t0 - 1) * fb, fb, tl, prev);
+
+    // snapshot bytes in force at t0: the batch's last snapshot before t0,
+    // recomputed from its two frames, or the snapshot texture
+    uint32_t snapb[U];
+    const int32_t s = a.chunk_snap[c];
+    if (s < 0) {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.snap_in, a.n_vec * 4u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) snapb[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, tl.voff[u] >> 2, 0, 0);
+    } else {
+        f32x2 is[U][2], ip[U][2];
+        alt_intensity<CH, U>(a.frames + (uint64_t)s * fb, fb, tl, is);
+        alt_intensity<CH, U>(s == 0 ? a.prev0 : a.frames + (uint64_t)(s - 1) * fb, fb, tl, ip);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint32_t b = 0;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const f32x2 m = __builtin_elementwise_min(is[u][k], ip[u][k]) * (f32x2){kI2sToI, kI2sToI};
+                b |= unorm_store(m.x) << (16 * k);
+                b |= unorm_store(m.y) << (16 * k + 8);
+            }
+            snapb[u] = b;
+        }
+    }
+    float snapf[U][4];
+    auto unpack_snap = [&]() {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) snapf[u][q] = unorm_load((snapb[u] >> (8 * q)) & 0xFFu);
+    };
+    unpack_snap();
+
+    auto load_frame = [&](uint32_t t, uint32_t (&d)[U][4]) {
+        const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)t * fb, fb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_vec<4>(r, tl.voff[u], d[u]);
+    };
+
+    auto process = [&](uint32_t t, const uint32_t (&d)[U][4]) {
+        const bool snap_now = a.flags[t] != 0;  // wave-uniform (scalar load)
+        const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (uint64_t)t * fb, fb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            St2 n;
+            derive_v2<4, CH>(d[u], n);
+            float med[4];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const f32x2 m = __builtin_elementwise_min(n.i[k], prev[u][k]) * (f32x2){kI2sToI, kI2sToI};
+                med[2 * k] = m.x;
+                med[2 * k + 1] = m.y;
+                prev[u][k] = n.i[k];
+            }
+            uint32_t o[4];
+            if (snap_now) {
+                uint32_t b = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t sq = unorm_store(med[q]);
+                    b |= sq << (8 * q);
+                    o[q] = gray_rgba(sq);
+                }
+                snapb[u] = b;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    o[q] = visual_epilogue(snapf[u][q] - med[q], (uint32_t)FILT, a.scalar, COL != 0);
+            }
+            store_vec<4>(ro, tl.voff[u], o);
+        }
+        if (snap_now) unpack_snap();
+    };
+
+    // two frames in flight per wave: frame t+1 loads while t is processed
+    uint32_t buf[2][U][4];
+    uint32_t t = t0;
+    load_frame(t, buf[0]);
+    while (true) {
+        if (t + 1 < t1) load_frame(t + 1, buf[1]);
+        process(t, buf[0]);
+        if (++t >= t1) break;
+        if (t + 1 < t1) load_frame(t + 1, buf[0]);
+        process(t, buf[1]);
+        if (++t >= t1) break;
+    }
+
+    if (a.last_snap >= (int32_t)t0 && a.last_snap < (int32_t)t1) {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(a.snap_out, a.n_vec * 4u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) __builtin_amdgcn_raw_buffer_store_b32(snapb[u], rs, tl.voff[u] >> 2, 0, 0);
+    }
+}
+
+template <int N>
+hipError_t launch_frame_n(const AltArgs& a, hipStream_t s) {
+    dim3 grid((a.width + kTile - 1) / kTile, (a.height + kTile - 1) / kTile);
+    hipLaunchKernelGGL(alt_frame_kernel<N>, grid, dim3(kTile, kTile), 0, s, a);
+    return hipGetLastError();
+}
+
+template <int CH, int FILT>
+const void* batch_ptr_fc(bool colorize) {
+    return colorize ? reinterpret_cast<const void*>(&alt_batch_kernel<CH, FILT, 1, kUnrollAlt>)
+                    : reinterpret_cast<const void*>(&alt_batch_kernel<CH, FILT, 0, kUnrollAlt>);
+}
+
+template <int CH>
+const void* batch_ptr_c(int filter, bool colorize) {
+    switch (filter) {
+        case 0: return batch_ptr_fc<CH, 0>(colorize);
+        case 1: return batch_ptr_fc<CH, 1>(colorize);
+        default: return batch_ptr_fc<CH, 255>(colorize);  // any other code: identity (:249)
+    }
+}
+
+}  // namespace
+
+hipError_t launch_alt_frame(const AltArgs& a, hipStream_t s) {
+    switch (a.n_tex) {
+#define DIPS_ALT_N(NV) \
+    case NV: return launch_frame_n<NV>(a, s);
+        DIPS_ALT_N(1) DIPS_ALT_N(2) DIPS_ALT_N(3) DIPS_ALT_N(4) DIPS_ALT_N(5) DIPS_ALT_N(6) DIPS_ALT_N(7)
+        DIPS_ALT_N(8) DIPS_ALT_N(9) DIPS_ALT_N(10) DIPS_ALT_N(11) DIPS_ALT_N(12) DIPS_ALT_N(13)
+        DIPS_ALT_N(14) DIPS_ALT_N(15) DIPS_ALT_N(16)
+#undef DIPS_ALT_N
+        default: return hipErrorInvalidValue;
+    }
+}
+
+const void* alt_batch_kernel_ptr(int chroma, int filter, bool colorize) {
+    switch (chroma) {
+        case 0: return batch_ptr_c<0>(filter, colorize);
+        case 1: return batch_ptr_c<1>(filter, colorize);
+        case 2: return batch_ptr_c<2>(filter, colorize);
+        case 3: return batch_ptr_c<3>(filter, colorize);
+        default: return nullptr;
+    }
+}
+
+hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool colorize, uint32_t blocks,
+                            hipStream_t s) {
+    const void* k = alt_batch_kernel_ptr(chroma, filter, colorize);
+    if (!k || blocks == 0) return hipErrorInvalidValue;
+    AltBatchArgs args = a;
+    void* params[] = {&args};
+    return hipLaunchKernel(k, dim3(blocks), dim3(256), params, 0, s);
+}
+
+}  // namespace dips

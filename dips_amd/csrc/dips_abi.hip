@@ -21,53 +21,12 @@
 
 #include "../../include/dips_hip.h"
 #include "dips_kernels.h"
+#include "host_buffers.h"
 
 namespace {
 
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t n) {
-        if (n <= cap) return hipSuccess;
-        if (p) {
-            hipError_t e = hipFree(p);
-            p = nullptr;
-            cap = 0;
-            if (e != hipSuccess) return e;
-        }
-        hipError_t e = hipMalloc(&p, n);
-        if (e == hipSuccess) cap = n;
-        return e;
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-    template <typename T> T* as() const { return static_cast<T*>(p); }
-};
-
-struct HostPinned {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t n) {
-        if (n <= cap) return hipSuccess;
-        if (p) {
-            (void)hipHostFree(p);
-            p = nullptr;
-            cap = 0;
-        }
-        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
-        if (e == hipSuccess) cap = n;
-        return e;
-    }
-    void release() {
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-    uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
-};
+using dips_host::DevBuf;
+using dips_host::HostPinned;
 
 std::mutex g_err_mu;
 std::string g_create_err;

@@ -75,6 +75,43 @@ struct CompatArgs {
     uint32_t colorize;
 };
 
+// dips_alt DiPsCompute (alt_kernels.hip).
+constexpr int kAltMaxTextures = 16;  // MAX_TEMPORAL_ARRAY_SIZE (dips_alt pre_compute_shader.wgsl:12)
+constexpr int kUnrollAlt = 2;        // vecs (4 px) per lane of alt_batch_kernel
+
+struct AltArgs {                     // one send_frame dispatch
+    const uint8_t* slots[kAltMaxTextures];  // RGBA8 contents of the N texture slots
+    uint8_t* snap;                   // snapshot texture, one byte (.r) per pixel
+    uint8_t* out;                    // RGBA8 output texture
+    uint32_t width, height;
+    uint32_t n_tex;
+    int32_t window;
+    uint32_t chroma, filter;
+    float scalar;
+    uint32_t colorize;
+    uint32_t snapshot;
+};
+
+struct AltBatchArgs {                // a run of frames, N = 2, W = 1
+    const uint8_t* frames;           // n_frames x frame_bytes (RGBA8)
+    const uint8_t* prev0;            // slot holding the frame before frames[0]
+    const uint8_t* snap_in;          // snapshot bytes before the batch
+    uint8_t* snap_out;               // snapshot bytes after the batch's last snapshot
+    uint8_t* out;                    // n_frames x frame_bytes (RGBA8)
+    const uint8_t* flags;            // device: n_frames snapshot flags
+    const int32_t* chunk_snap;       // device: per chunk, last snapshot frame before it or -1
+    uint32_t frame_bytes;
+    uint32_t n_vec;                  // 4-pixel vecs per frame
+    uint32_t n_frames, chunk, n_chunks, n_tiles;
+    int32_t last_snap;               // last snapshot frame of the batch or -1
+    float scalar;
+};
+
+hipError_t launch_alt_frame(const AltArgs& a, hipStream_t s);
+const void* alt_batch_kernel_ptr(int chroma, int filter, bool colorize);
+hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool colorize, uint32_t blocks,
+                            hipStream_t s);
+
 int pixels_per_vec(int channels);
 int fast_unroll(int channels);
 const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map);

@@ -181,6 +181,79 @@ dips_status dips_series_geometry(dips_handle *h, uint32_t width, uint32_t height
 /* Library ABI version (DIPS_ABI_VERSION). */
 int dips_abi_version(void);
 
+/* ------------------------------------------------------------------------
+ * dips_alt operator.  The dips_alt crate's GPU
+ * operator is DiPsCompute (dips_alt/src/dips_compute/mod.rs:243-647):
+ * new(num_textures, textures_width, textures_height, window, device, queue,
+ * properties) and send_frame(frame, snapshot, surface) -> Vec<u8>, driven by
+ * the frame loop of run_dips_on_file (dips_alt/src/lib.rs:554-690).  The
+ * reference's constructor takes (rows, cols) in that order (lib.rs:596-603);
+ * this ABI takes width = columns, height = rows.  Frames are RGBA8, stride
+ * width*4 (mod.rs:510-521).
+ * ------------------------------------------------------------------------ */
+
+/* DiPsProperties of dips_alt (dips_alt/src/dips_compute/mod.rs:167-186) plus
+ * the operator's texture count. */
+typedef struct dips_alt_params {
+    uint8_t colorize;                /* COLORIZE; default 1 (mod.rs:179) */
+    int32_t window_size;             /* WINDOW_SIZE; 1..11; default 1 (mod.rs:180) */
+    float sigmoid_horizontal_scalar; /* SIGMOID_HORIZONTAL_SCALAR; default 5.0 (mod.rs:181) */
+    uint32_t filter_type;            /* DIPS_FILTER_SIGMOID (default) / _INVERSE_SIGMOID;
+                                        any other code: no filter (shader default branch) */
+    uint32_t chroma_filter;          /* DIPS_CHROMA_*: All = NONE (default), Red, Green, Blue */
+    uint32_t num_textures;           /* NUM_TEXTURES, 1..16; default FRAME_COUNT = 2 (lib.rs:36) */
+    uint32_t flags;                  /* DIPS_FLAG_DEVICE_PTRS, _TIME_KERNEL, _FORCE_GENERIC */
+} dips_alt_params;
+
+typedef struct dips_alt_handle dips_alt_handle;
+
+/* Fill `p` with DiPsProperties::default() (mod.rs:176-186), num_textures 2. */
+dips_status dips_alt_params_default(dips_alt_params *p);
+
+/* Replaces DiPsCompute::new (dips_alt/src/dips_compute/mod.rs:270-496):
+ * texture slots, snapshot texture and output, all zero-initialised. */
+dips_status dips_alt_create(const dips_alt_params *params, uint32_t width, uint32_t height, int device,
+                            dips_alt_handle **out);
+
+/* Replaces Drop of DiPsCompute. */
+void dips_alt_destroy(dips_alt_handle *h);
+
+/* Last error message for `h` (or the last creation failure if h == NULL). */
+const char *dips_alt_last_error(const dips_alt_handle *h);
+
+/* Run subsequent work on `stream` (a hipStream_t; NULL = the handle's own). */
+dips_status dips_alt_set_stream(dips_alt_handle *h, void *stream);
+dips_status dips_alt_synchronize(dips_alt_handle *h);
+
+/* Replaces DiPsCompute::send_frame (mod.rs:498-646): writes the frame into
+ * texture slot texture_index, advances it, runs pre_compute_main with the
+ * snapshot uniform = (snapshot != 0) and copies the RGBA8 output texture
+ * (width*height*4 bytes) to `out_rgba`.  Host pointers always. */
+dips_status dips_alt_send_frame(dips_alt_handle *h, const uint8_t *frame_rgba, size_t len, int snapshot,
+                                uint8_t *out_rgba, size_t cap);
+
+/* `n_frames` consecutive send_frame calls in one pass: frames n_frames x
+ * width*height*4, snapshot_flags (host, n_frames bytes, NULL = none) the
+ * per-frame snapshot argument, out n_frames x width*height*4.  With
+ * DIPS_FLAG_DEVICE_PTRS frames/out are device pointers and the call is
+ * asynchronous on the handle's stream. */
+dips_status dips_alt_send_frames(dips_alt_handle *h, const uint8_t *frames, uint32_t n_frames,
+                                 const uint8_t *snapshot_flags, uint8_t *out);
+
+/* The frame loop of run_dips_on_file (lib.rs:588-683) minus OpenCV decode /
+ * encode: snapshot while index == FRAME_COUNT, index saturating, a refresh
+ * marker equal to the running 1-based frame count resets index to 0.  The
+ * loop state persists across calls, so a video may be fed in pieces. */
+dips_status dips_alt_run(dips_alt_handle *h, const uint8_t *frames, uint32_t n_frames,
+                         const uint64_t *refresh_markers, uint32_t n_markers, uint8_t *out);
+
+/* Copy the snapshot texture's .r channel (width*height bytes, host). */
+dips_status dips_alt_snapshot_texture(dips_alt_handle *h, uint8_t *out_gray, size_t cap);
+
+/* Kernel timing of the batch kernel (DIPS_FLAG_TIME_KERNEL), as dips_kernel_time. */
+dips_status dips_alt_kernel_time(dips_alt_handle *h, double *total_ms, uint64_t *launches);
+dips_status dips_alt_kernel_time_reset(dips_alt_handle *h);
+
 #ifdef __cplusplus
 }
 #endif

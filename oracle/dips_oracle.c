@@ -541,3 +541,185 @@ int dips_oracle_cs_start_texture(const dips_oracle_cs *cs, uint8_t *out) {
     memcpy(out, cs->start, (size_t)cs->width * cs->height * 4);
     return 1;
 }
+
+/* ------------------------------------------------------------------ */
+/* dips_alt DiPsCompute (next-4 of SURVEY.md s8f)                      */
+/* ------------------------------------------------------------------ */
+
+#define O_ALT_MAX_TEX 16 /* MAX_TEMPORAL_ARRAY_SIZE, dips_alt pre_compute_shader.wgsl:12 */
+
+struct dips_oracle_alt {
+    uint32_t n_tex;          /* num_textures, dips_alt/src/dips_compute/mod.rs:270-279 */
+    uint32_t width, height;  /* texture extent (mod.rs:283-287: width = cols) */
+    uint8_t colorize;
+    int32_t window;
+    float scalar;            /* SIGMOID_HORIZONTAL_SCALAR */
+    uint32_t filter, chroma;
+    uint8_t *slots[O_ALT_MAX_TEX]; /* input_textures, zero-initialised (wgpu) */
+    uint8_t *snap;           /* snapshot_texture (.r channel), zero-initialised */
+    uint32_t tex_idx;        /* texture_index: UCircularIndex(0, n), mod.rs:494 */
+};
+
+dips_oracle_alt *dips_oracle_alt_new(uint32_t n_tex, uint32_t width, uint32_t height,
+                                     uint8_t colorize, int32_t window, float scalar,
+                                     uint32_t filter, uint32_t chroma) {
+    if (n_tex < 1 || n_tex > O_ALT_MAX_TEX || width == 0 || height == 0) return NULL;
+    if (window < 1 || window > 11 || chroma > 3) return NULL;
+    dips_oracle_alt *a = (dips_oracle_alt *)calloc(1, sizeof(*a));
+    if (!a) return NULL;
+    a->n_tex = n_tex;
+    a->width = width;
+    a->height = height;
+    a->colorize = colorize ? 1 : 0;
+    a->window = window;
+    a->scalar = scalar;
+    a->filter = filter;
+    a->chroma = chroma;
+    const size_t fb = (size_t)width * height * 4;
+    for (uint32_t k = 0; k < n_tex; ++k) {
+        a->slots[k] = (uint8_t *)calloc(fb, 1);
+        if (!a->slots[k]) { dips_oracle_alt_free(a); return NULL; }
+    }
+    a->snap = (uint8_t *)calloc((size_t)width * height, 1);
+    if (!a->snap) { dips_oracle_alt_free(a); return NULL; }
+    return a;
+}
+
+void dips_oracle_alt_free(dips_oracle_alt *a) {
+    if (!a) return;
+    for (uint32_t k = 0; k < O_ALT_MAX_TEX; ++k) free(a->slots[k]);
+    free(a->snap);
+    free(a);
+}
+
+/* spatial_median_filter of dips_alt (dips_alt pre_compute_shader.wgsl:134-186):
+ * the (2h)^2 offsets in [-h, h) are filled (out-of-frame = 0), the rest of the
+ * 121-entry array is zero, a bubble sort over the first W^2 entries (all
+ * indices in bounds for W <= 11, unlike dips' W^2 + 1), result [W^2/2 + 1]. */
+static float o_alt_spatial(const uint8_t *img, uint32_t w, uint32_t h, uint32_t x, uint32_t y,
+                           int window, int chroma) {
+    const uint8_t *px = img + ((size_t)y * w + x) * 4;
+    if (window == 1) return o_intensity_rgb(px[0], px[1], px[2], chroma); /* :135-139 */
+    float a[121];
+    memset(a, 0, sizeof(a));
+    const int hw = window / 2;
+    for (int i = -hw; i < hw; ++i) {
+        for (int j = -hw; j < hw; ++j) {
+            float color;
+            const int xi = (int)x + i, yj = (int)y + j;
+            if (xi >= (int)w || yj >= (int)h || xi < 0 || yj < 0) color = 0.0f;
+            else {
+                const uint8_t *q = img + ((size_t)yj * w + (size_t)xi) * 4;
+                color = o_intensity_rgb(q[0], q[1], q[2], chroma);
+            }
+            a[(i + hw) + window * (j + hw)] = color;
+        }
+    }
+    const int ws2 = window * window;
+    for (int i = 0; i < ws2 - 1; ++i) {
+        int swapped = 0;
+        for (int j = 0; j < ws2 - 1; ++j) {
+            if (a[j] > a[j + 1]) {
+                const float tmp = a[j];
+                a[j] = a[j + 1];
+                a[j + 1] = tmp;
+                swapped = 1;
+            }
+        }
+        if (!swapped) break;
+    }
+    return a[ws2 / 2 + 1];
+}
+
+/* The temporal sort of dips_alt pre_compute_main (pre_compute_shader.wgsl:200,
+ * 212-227, 232, 238): a 16-entry zero-initialised array holding the n
+ * filtered values, n bubble passes over j < n comparing [j] and [j+1]
+ * (index 16 clamped to 15 by naga's Restrict policy when n = 16), element
+ * [n/2].  For n < 16 the sort covers one trailing zero. */
+float dips_oracle_alt_temporal(const float *v, uint32_t n) {
+    float a[O_ALT_MAX_TEX];
+    memset(a, 0, sizeof(a));
+    for (uint32_t i = 0; i < n; ++i) a[i] = v[i];
+    for (uint32_t i = 0; i < n; ++i) {
+        int swapped = 0;
+        for (uint32_t j = 0; j < n; ++j) {
+            const uint32_t j1 = j + 1 > O_ALT_MAX_TEX - 1 ? O_ALT_MAX_TEX - 1 : j + 1;
+            if (a[j] > a[j1]) {
+                const float tmp = a[j];
+                a[j] = a[j1];
+                a[j1] = tmp;
+                swapped = 1;
+            }
+        }
+        if (!swapped) break;
+    }
+    return a[n / 2];
+}
+
+/* DiPsCompute::send_frame (dips_alt/src/dips_compute/mod.rs:498-646) with the
+ * compute pass pre_compute_main (pre_compute_shader.wgsl:188-263); returns the
+ * RGBA8 output texture (width*height*4).  `snapshot` != 0 is the Some(())
+ * case: the uniform is 1 for this dispatch only (mod.rs:525-528, 617-620). */
+int dips_oracle_alt_send_frame(dips_oracle_alt *a, const uint8_t *rgba, int snapshot,
+                               uint8_t *out) {
+    if (!a || !rgba || !out) return -1;
+    const uint32_t w = a->width, h = a->height;
+    const size_t fb = (size_t)w * h * 4;
+    memcpy(a->slots[a->tex_idx], rgba, fb);    /* queue.write_texture, :510-521 */
+    a->tex_idx = (a->tex_idx + 1) % a->n_tex;  /* texture_index += 1, :523 */
+    for (uint32_t y = 0; y < h; ++y) {
+        for (uint32_t x = 0; x < w; ++x) {
+            const size_t p = (size_t)y * w + x;
+            float m[O_ALT_MAX_TEX];
+            for (uint32_t k = 0; k < a->n_tex; ++k) /* array generator, dynamic_texture_array.rs:67-69 */
+                m[k] = o_alt_spatial(a->slots[k], w, h, x, y, a->window, (int)a->chroma);
+            const float med = dips_oracle_alt_temporal(m, a->n_tex);
+            uint8_t *o = out + p * 4;
+            if (snapshot) { /* :231-235 */
+                const uint8_t s = dips_oracle_q(med);
+                a->snap[p] = s;
+                o[0] = o[1] = o[2] = s;
+                o[3] = 255;
+                continue;
+            }
+            const float original = dips_oracle_u(a->snap[p]); /* :237 */
+            float diff = original - med;
+            diff = diff * ((0.5f - -0.5f) / (1.0f - -1.0f)); /* map(), :100-108, 240 */
+            if (a->filter == 0) diff = o_sigmoid(diff, a->scalar);
+            else if (a->filter == 1) diff = o_inv_sigmoid(diff, a->scalar);
+            diff *= 5.0f; /* DIFF_SCALE, :26, 252 */
+            float rgb[3];
+            if (a->colorize) {
+                if (diff < 0.0f) o_hsl(0.0f, fabsf(diff), 0.5f, rgb);
+                else o_hsl(120.0f, diff, 0.5f, rgb);
+            } else {
+                rgb[0] = rgb[1] = rgb[2] = 0.5f - diff;
+            }
+            o[0] = dips_oracle_q(rgb[0]);
+            o[1] = dips_oracle_q(rgb[1]);
+            o[2] = dips_oracle_q(rgb[2]);
+            o[3] = 255;
+        }
+    }
+    return 0;
+}
+
+/* The frame loop of run_dips_on_file (dips_alt/src/lib.rs:588-683) without
+ * the OpenCV decode / encode: snapshot when index == FRAME_COUNT (2), index
+ * saturates at FRAME_COUNT + 1, and a refresh marker equal to the 1-based
+ * frame count resets index to 0.  Writes n_frames outputs. */
+int dips_oracle_alt_run(dips_oracle_alt *a, const uint8_t *frames, uint32_t n_frames,
+                        const uint64_t *markers, uint32_t n_markers, uint8_t *out) {
+    if (!a) return -1;
+    const size_t fb = (size_t)a->width * a->height * 4;
+    uint64_t index = 0, overall = 0;
+    for (uint32_t t = 0; t < n_frames; ++t) {
+        int rc = dips_oracle_alt_send_frame(a, frames + (size_t)t * fb, index == 2, out + (size_t)t * fb);
+        if (rc) return rc;
+        if (index <= 2) index += 1;
+        overall += 1;
+        for (uint32_t k = 0; k < n_markers; ++k)
+            if (markers[k] == overall) { index = 0; break; }
+    }
+    return 0;
+}

@@ -71,6 +71,20 @@ int  dips_oracle_cs_dispatch(dips_oracle_cs *cs, uint8_t *out_rgba);
 int  dips_oracle_cs_start_texture(const dips_oracle_cs *cs, uint8_t *out_rgba);
 void dips_oracle_cs_free(dips_oracle_cs *cs);
 
+/* dips_alt DiPsCompute emulation (dips_alt/src/dips_compute/mod.rs:243-647,
+ * shader dips_alt/src/dips_compute/shaders/pre_compute_shader.wgsl).
+ * width = texture columns, height = rows; n_tex = num_textures (1..16). */
+typedef struct dips_oracle_alt dips_oracle_alt;
+dips_oracle_alt *dips_oracle_alt_new(uint32_t n_tex, uint32_t width, uint32_t height,
+                                     uint8_t colorize, int32_t window, float scalar,
+                                     uint32_t filter, uint32_t chroma);
+float dips_oracle_alt_temporal(const float *v, uint32_t n);
+int  dips_oracle_alt_send_frame(dips_oracle_alt *a, const uint8_t *rgba, int snapshot,
+                                uint8_t *out_rgba);
+int  dips_oracle_alt_run(dips_oracle_alt *a, const uint8_t *frames, uint32_t n_frames,
+                         const uint64_t *markers, uint32_t n_markers, uint8_t *out);
+void dips_oracle_alt_free(dips_oracle_alt *a);
+
 #ifdef __cplusplus
 }
 #endif

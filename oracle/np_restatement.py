@@ -295,3 +295,80 @@ class ComputeState:
         orig = U_LUT[self.start[..., 0]]
         diff = (orig - med).astype(F32)
         return epilogue(diff, self.filter, self.k, self.colorize)
+
+
+# --------------------------------------------------------------------------
+# dips_alt DiPsCompute (dips_alt/src/dips_compute/mod.rs:243-647,
+# dips_alt/src/dips_compute/shaders/pre_compute_shader.wgsl)
+# --------------------------------------------------------------------------
+
+def alt_spatial(img: np.ndarray, window: int, chroma: int) -> np.ndarray:
+    """dips_alt spatial_median_filter (:134-186): the (2h)^2 window values and
+    W^2 - (2h)^2 zeros sorted, element W^2/2 + 1 (no +1 entry, unlike dips)."""
+    I = intensity(img[..., :3], chroma, gray=False)
+    if window == 1:
+        return I
+    h, w = I.shape
+    hw = window // 2
+    size = window * window
+    shifted = []
+    for i in range(-hw, hw):        # x offset
+        for j in range(-hw, hw):    # y offset
+            ys, xs = np.arange(h) + j, np.arange(w) + i
+            ok = ((ys >= 0) & (ys < h))[:, None] & ((xs >= 0) & (xs < w))[None, :]
+            sub = I[np.clip(ys, 0, h - 1)][:, np.clip(xs, 0, w - 1)]
+            shifted.append(np.where(ok, sub, F32(0.0)).astype(F32))
+    vals = np.stack(shifted, axis=-1)
+    pad = np.zeros((h, w, size - vals.shape[-1]), dtype=F32)
+    return np.sort(np.concatenate([vals, pad], axis=-1), axis=-1)[..., size // 2 + 1].astype(F32)
+
+
+def alt_temporal(stack: np.ndarray) -> np.ndarray:
+    """pre_compute_main's sort (:212-227) of the n filtered values inside a
+    zero-filled 16-entry array, element n/2: for n < 16 the sort spans one
+    trailing zero, for n = 16 (index 16 clamped) it is the plain sort."""
+    n = stack.shape[-1]
+    if n < 16:
+        stack = np.concatenate([stack, np.zeros(stack.shape[:-1] + (1,), dtype=F32)], axis=-1)
+    return np.sort(stack, axis=-1)[..., n // 2].astype(F32)
+
+
+class AltCompute:
+    """numpy twin of DiPsCompute::send_frame (mod.rs:498-646)."""
+
+    def __init__(self, num_textures, width, height, colorize=True, window=1, scalar=5.0,
+                 filter_type=0, chroma=0):
+        self.n = int(num_textures)
+        self.w, self.h = int(width), int(height)
+        self.colorize = bool(colorize)
+        self.window = int(window)
+        self.k = float(np.float32(scalar))
+        self.filter = int(filter_type)
+        self.chroma = int(chroma)
+        self.slots = [np.zeros((self.h, self.w, 4), np.uint8) for _ in range(self.n)]
+        self.snap = np.zeros((self.h, self.w), np.uint8)
+        self.idx = 0
+
+    def send_frame(self, frame, snapshot=False):
+        self.slots[self.idx] = np.asarray(frame, np.uint8).reshape(self.h, self.w, 4).copy()
+        self.idx = (self.idx + 1) % self.n
+        med = alt_temporal(np.stack([alt_spatial(s, self.window, self.chroma) for s in self.slots],
+                                    axis=-1))
+        if snapshot:
+            s = q(med)
+            self.snap = s
+            return np.stack([s, s, s, np.full_like(s, 255)], axis=-1)
+        diff = (U_LUT[self.snap] - med).astype(F32)
+        return epilogue(diff, self.filter, self.k, self.colorize)
+
+    def run(self, frames, markers=()):
+        """run_dips_on_file's loop (dips_alt/src/lib.rs:588-683)."""
+        index, overall, outs = 0, 0, []
+        for f in frames:
+            outs.append(self.send_frame(f, snapshot=(index == 2)))
+            if index <= 2:
+                index += 1
+            overall += 1
+            if overall in markers:
+                index = 0
+        return np.stack(outs) if outs else np.zeros((0, self.h, self.w, 4), np.uint8)

@@ -70,6 +70,19 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     lib.dips_oracle_cs_start_texture.restype = ctypes.c_int
     lib.dips_oracle_cs_free.argtypes = [ctypes.c_void_p]
     lib.dips_oracle_cs_free.restype = None
+    lib.dips_oracle_alt_new.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint8, ctypes.c_int32, ctypes.c_float,
+                                        ctypes.c_uint32, ctypes.c_uint32]
+    lib.dips_oracle_alt_new.restype = ctypes.c_void_p
+    lib.dips_oracle_alt_temporal.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_uint32]
+    lib.dips_oracle_alt_temporal.restype = ctypes.c_float
+    lib.dips_oracle_alt_send_frame.argtypes = [ctypes.c_void_p, _u8p, ctypes.c_int, _u8p]
+    lib.dips_oracle_alt_send_frame.restype = ctypes.c_int
+    lib.dips_oracle_alt_run.argtypes = [ctypes.c_void_p, _u8p, ctypes.c_uint32, _u64p,
+                                        ctypes.c_uint32, _u8p]
+    lib.dips_oracle_alt_run.restype = ctypes.c_int
+    lib.dips_oracle_alt_free.argtypes = [ctypes.c_void_p]
+    lib.dips_oracle_alt_free.restype = None
     if path == os.path.join(_HERE, "libdips_oracle.so"):
         _LIB = lib
     return lib
@@ -161,3 +174,50 @@ def frame_callback(width: int, height: int, frame: np.ndarray, compute: ComputeS
     compute.add_texture(width, height, frame)
     out = compute.dispatch()
     return out if out is not None else np.array(frame, dtype=np.uint8, copy=True).reshape(height, width, 4)
+
+
+class AltCompute:
+    """Oracle twin of dips_alt's DiPsCompute (dips_alt/src/dips_compute/mod.rs:243-647).
+    width = frame columns, height = rows (natural order; the reference's
+    constructor takes (rows, cols), lib.rs:596-603)."""
+
+    def __init__(self, num_textures: int, width: int, height: int, colorize: bool = True,
+                 window: int = 1, scalar: float = 5.0, filter_type: int = 0, chroma: int = 0):
+        self._lib = load()
+        self._h = self._lib.dips_oracle_alt_new(num_textures, width, height, 1 if colorize else 0,
+                                                window, ctypes.c_float(scalar), filter_type, chroma)
+        if not self._h:
+            raise ValueError("invalid DiPsCompute parameters")
+        self.width, self.height = width, height
+
+    def send_frame(self, frame: np.ndarray, snapshot: bool = False) -> np.ndarray:
+        frame = np.ascontiguousarray(frame, dtype=np.uint8)
+        assert frame.size == self.width * self.height * 4
+        out = np.zeros((self.height, self.width, 4), dtype=np.uint8)
+        rc = self._lib.dips_oracle_alt_send_frame(self._h, _p(frame), 1 if snapshot else 0, _p(out))
+        if rc != 0:
+            raise ValueError(f"send_frame rc={rc}")
+        return out
+
+    def run(self, frames: np.ndarray, markers=()) -> np.ndarray:
+        """run_dips_on_file's frame loop (dips_alt/src/lib.rs:588-683)."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        n = frames.shape[0]
+        out = np.zeros_like(frames)
+        mk = np.ascontiguousarray(np.asarray(list(markers), dtype=np.uint64))
+        rc = self._lib.dips_oracle_alt_run(self._h, _p(frames), n, _p(mk, _u64p), mk.size, _p(out))
+        if rc != 0:
+            raise ValueError(f"alt run rc={rc}")
+        return out
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._lib.dips_oracle_alt_free(h)
+            self._h = None
+
+
+def alt_temporal(values, lib: Optional[ctypes.CDLL] = None) -> float:
+    lib = lib or load()
+    v = np.ascontiguousarray(np.asarray(values, dtype=np.float32))
+    return float(lib.dips_oracle_alt_temporal(v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), v.size))
