@@ -6,6 +6,7 @@ mirror of the reference crate's operator surface (dips/src/lib.rs,
 dips/src/gpu/mod.rs) plus the batch difference-series operator and the
 frame-range sharding over RCCL (dips_amd.shard).
 """
+from . import alt  # dips_alt crate surface (DiPsCompute, run_dips_on_file loop)
 from ._lib import DipsError, DipsLibraryError, LIB_PATH, load as load_library
 from .api import (ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, DiPsProperties,
                   FrameCallbackNotSpecifiedError, Mode, PixelFormat, Series,

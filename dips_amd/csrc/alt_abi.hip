@@ -143,7 +143,8 @@ const uint8_t* slot_at(const dips_alt_handle* h, const uint8_t* frames, uint64_t
 
 dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags, uint8_t* out,
                      hipStream_t s) {
-    const void* k = dips::alt_batch_kernel_ptr((int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0);
+    const bool fast = dips::alt_fast_epilogue_ok(h->p.filter_type, h->p.sigmoid_horizontal_scalar);
+    const void* k = dips::alt_batch_kernel_ptr((int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0, fast);
     if (!k) return fail(h, DIPS_ERR_INVALID, "no batch kernel for these parameters");
     if (h->occupancy == 0) {
         int nb = 0;
@@ -198,6 +199,7 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
     a.n_tiles = (uint32_t)n_tiles;
     a.last_snap = last;
     a.scalar = h->p.sigmoid_horizontal_scalar;
+    a.kneg_half = -h->p.sigmoid_horizontal_scalar * 0.5f;
     const uint32_t blocks = (uint32_t)((n_tiles * n_chunks + 3u) / 4u);
 
     const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
@@ -209,7 +211,7 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
         ALT_HIP(h, hipEventRecord(e0, s));
     }
     ALT_HIP(h, dips::launch_alt_batch(a, (int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0,
-                                      blocks, s));
+                                      fast, blocks, s));
     if (timing) {
         ALT_HIP(h, hipEventRecord(e1, s));
         h->ev_pending.emplace_back(e0, e1);

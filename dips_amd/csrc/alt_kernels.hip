@@ -21,6 +21,7 @@
 // (one trailing zero inside the sorted range) and sorted(v)[8] for n = 16
 // (index 16 clamped to 15 by naga's Restrict policy).  Intensities are >= 0,
 // so for n = 2 it is min(v0, v1) and for n = 1 it is 0.
+#include "epilogue_fast.h"
 #include "intensity_v2.h"
 
 namespace dips {
@@ -164,7 +165,15 @@ __device__ __forceinline__ void alt_intensity(const uint8_t* frame, uint32_t fb,
     }
 }
 
-template <int CH, int FILT, int COL, int U>
+// exact u(c) = c / 255 without a division (series_common.h, exhaustively checked)
+__device__ __forceinline__ float unorm_fma(uint32_t c) {
+    const float f = (float)c;
+    return __builtin_fmaf(f, kUnormHi, f * kUnormLo);
+}
+
+// FAST: the branch-free epilogue of epilogue_fast.h (sigmoid with |k| <= 160,
+// or no filter); otherwise the specification's visual_epilogue.
+template <int CH, int FILT, int COL, bool FAST, int U>
 __global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -216,7 +225,7 @@ __global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) snapf[u][q] = unorm_load((snapb[u] >> (8 * q)) & 0xFFu);
+            for (int q = 0; q < 4; ++q) snapf[u][q] = unorm_fma((snapb[u] >> (8 * q)) & 0xFFu);
     };
     unpack_snap();
 
@@ -253,8 +262,12 @@ __global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
                 snapb[u] = b;
             } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    o[q] = visual_epilogue(snapf[u][q] - med[q], (uint32_t)FILT, a.scalar, COL != 0);
+                for (int q = 0; q < 4; ++q) {
+                    if constexpr (FAST)
+                        o[q] = epilogue_fast<FILT, COL != 0>(snapf[u][q] - med[q], a.kneg_half);
+                    else
+                        o[q] = visual_epilogue(snapf[u][q] - med[q], (uint32_t)FILT, a.scalar, COL != 0);
+                }
             }
             store_vec<4>(ro, tl.voff[u], o);
         }
@@ -288,18 +301,18 @@ hipError_t launch_frame_n(const AltArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int CH, int FILT>
+template <int CH, int FILT, bool FAST>
 const void* batch_ptr_fc(bool colorize) {
-    return colorize ? reinterpret_cast<const void*>(&alt_batch_kernel<CH, FILT, 1, kUnrollAlt>)
-                    : reinterpret_cast<const void*>(&alt_batch_kernel<CH, FILT, 0, kUnrollAlt>);
+    return colorize ? reinterpret_cast<const void*>(&alt_batch_kernel<CH, FILT, 1, FAST, kUnrollAlt>)
+                    : reinterpret_cast<const void*>(&alt_batch_kernel<CH, FILT, 0, FAST, kUnrollAlt>);
 }
 
 template <int CH>
-const void* batch_ptr_c(int filter, bool colorize) {
+const void* batch_ptr_c(int filter, bool colorize, bool fast) {
     switch (filter) {
-        case 0: return batch_ptr_fc<CH, 0>(colorize);
-        case 1: return batch_ptr_fc<CH, 1>(colorize);
-        default: return batch_ptr_fc<CH, 255>(colorize);  // any other code: identity (:249)
+        case 0: return fast ? batch_ptr_fc<CH, 0, true>(colorize) : batch_ptr_fc<CH, 0, false>(colorize);
+        case 1: return batch_ptr_fc<CH, 1, false>(colorize);
+        default: return batch_ptr_fc<CH, 255, true>(colorize);  // any other code: identity (:249)
     }
 }
 
@@ -317,19 +330,19 @@ hipError_t launch_alt_frame(const AltArgs& a, hipStream_t s) {
     }
 }
 
-const void* alt_batch_kernel_ptr(int chroma, int filter, bool colorize) {
+const void* alt_batch_kernel_ptr(int chroma, int filter, bool colorize, bool fast) {
     switch (chroma) {
-        case 0: return batch_ptr_c<0>(filter, colorize);
-        case 1: return batch_ptr_c<1>(filter, colorize);
-        case 2: return batch_ptr_c<2>(filter, colorize);
-        case 3: return batch_ptr_c<3>(filter, colorize);
+        case 0: return batch_ptr_c<0>(filter, colorize, fast);
+        case 1: return batch_ptr_c<1>(filter, colorize, fast);
+        case 2: return batch_ptr_c<2>(filter, colorize, fast);
+        case 3: return batch_ptr_c<3>(filter, colorize, fast);
         default: return nullptr;
     }
 }
 
-hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool colorize, uint32_t blocks,
+hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool colorize, bool fast, uint32_t blocks,
                             hipStream_t s) {
-    const void* k = alt_batch_kernel_ptr(chroma, filter, colorize);
+    const void* k = alt_batch_kernel_ptr(chroma, filter, colorize, fast);
     if (!k || blocks == 0) return hipErrorInvalidValue;
     AltBatchArgs args = a;
     void* params[] = {&args};

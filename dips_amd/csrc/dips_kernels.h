@@ -104,13 +104,23 @@ struct AltBatchArgs {                // a run of frames, N = 2, W = 1
     uint32_t n_vec;                  // 4-pixel vecs per frame
     uint32_t n_frames, chunk, n_chunks, n_tiles;
     int32_t last_snap;               // last snapshot frame of the batch or -1
-    float scalar;
+    float scalar;                    // SIGMOID_HORIZONTAL_SCALAR k
+    float kneg_half;                 // -k / 2 (fast epilogue)
 };
 
 hipError_t launch_alt_frame(const AltArgs& a, hipStream_t s);
-const void* alt_batch_kernel_ptr(int chroma, int filter, bool colorize);
-hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool colorize, uint32_t blocks,
+// fast: the branch-free epilogue (alt_fast_epilogue_ok)
+const void* alt_batch_kernel_ptr(int chroma, int filter, bool colorize, bool fast);
+hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool colorize, bool fast, uint32_t blocks,
                             hipStream_t s);
+// the fast epilogue's preconditions (epilogue_fast.h): sigmoid with a scalar
+// k of |k| <= 160 (0 or |k| >= 2^-60 so -k/2 is exact), or no filter
+inline bool alt_fast_epilogue_ok(uint32_t filter, float k) {
+    if (filter == 1u) return false;
+    if (filter != 0u) return true;
+    const float a = k < 0.0f ? -k : k;
+    return a <= 160.0f && (a == 0.0f || a >= 0x1p-60f);
+}
 
 int pixels_per_vec(int channels);
 int fast_unroll(int channels);
