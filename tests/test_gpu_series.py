@@ -139,6 +139,65 @@ def test_synth_device_bit_exact(c):
     assert np.array_equal(dst.cpu().numpy(), want)
 
 
+def test_8k_threshold_config_matches_oracle():
+    """BASELINE.json configs[4]: 7680x4320 RGB8, the f32 intensity path with
+    a threshold (tau = 8/255), overall and per-frame, against the oracle."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    w, h, n = 7680, 4320, 4
+    dev = torch.empty((n, h, w, 3), dtype=torch.uint8, device="cuda")
+    for mode in (Mode.Overall, Mode.PerFrame):
+        op = DiffSeriesOperator(PixelFormat.RGB8, mode, 8 / 255, 0)
+        try:
+            op.synth_device(dev, w, h, 0xD1B5, 9996)
+            ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+            op.run_device(dev, ser)
+            torch.cuda.synchronize()
+            host = dev.cpu().numpy()
+            out4, si, _ = oracle.series(host, mode=int(mode), tau=8 / 255, nthreads=8)
+            got = ser.cpu().numpy().view(np.uint64)
+            assert np.array_equal(got, out4)
+            np.testing.assert_allclose(np.ldexp(got[:, 3].astype(np.float64), -32), si, rtol=SI_RTOL)
+        finally:
+            op.close()
+
+
+def test_1080p_overall_full_batch_properties():
+    """BASELINE.json configs[1] at full size (1920x1080 RGB8, 1000 frames,
+    'overall'): the series of the whole batch equals the concatenation of two
+    half batches against the same reference (frame 0) and of a per-frame run
+    whose reference is the halo frame; frame 0's entry is zero; the first
+    frames equal the oracle."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    w, h, n = 1920, 1080, 1000
+    dev = torch.empty((n, h, w, 3), dtype=torch.uint8, device="cuda")
+    op = DiffSeriesOperator(PixelFormat.RGB8, Mode.Overall, 8 / 255, 0)
+    pf = DiffSeriesOperator(PixelFormat.RGB8, Mode.PerFrame, 8 / 255, 0)
+    try:
+        op.synth_device(dev, w, h, 0xD1B5, 0)
+        full = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+        op.run_device(dev, full)
+        a = torch.zeros((500, 4), dtype=torch.int64, device="cuda")
+        b = torch.zeros((500, 4), dtype=torch.int64, device="cuda")
+        op.run_device(dev[:500], a, ref=dev[0])
+        op.run_device(dev[500:], b, ref=dev[0])
+        p_full = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+        p_half = torch.zeros((500, 4), dtype=torch.int64, device="cuda")
+        pf.run_device(dev, p_full)
+        pf.run_device(dev[500:], p_half, ref=dev[499])
+        torch.cuda.synchronize()
+        assert torch.equal(full, torch.cat([a, b]))
+        assert torch.equal(p_full[500:], p_half)
+        assert not full[0].any() and not p_full[0].any()
+        host = dev[:3].cpu().numpy()
+        out4, _, _ = oracle.series(host, mode=0, tau=8 / 255, nthreads=8)
+        assert np.array_equal(full[:3].cpu().numpy().view(np.uint64), out4)
+    finally:
+        op.close()
+        pf.close()
+
+
 def test_device_path_matches_host_path():
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
