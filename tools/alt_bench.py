@@ -35,7 +35,9 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cpu-frames", type=int, default=3)
+    ap.add_argument("--cpu-frames", type=int, default=10)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "alt_pmc_traffic.json"),
+                    help="HBM traffic per launch measured by profiles/collect_alt_pmc.sh")
     args = ap.parse_args()
 
     import torch
@@ -81,6 +83,12 @@ def main():
 
     algo = F * W * H * 8
     achieved = algo / (kernel_ms / 1e3) / 1e9
+    traffic, traffic_src = None, None
+    if os.path.exists(args.pmc_json):
+        with open(args.pmc_json) as f:
+            pmc = json.load(f)
+        if (pmc.get("width"), pmc.get("height"), pmc.get("frames")) == (W, H, F):
+            traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), pmc.get("source")
     print(json.dumps({
         "metric": "dips_alt frames/s + achieved HBM GB/s, 4K RGBA8",
         "value": round(F * args.steps / elapsed, 2), "unit": "frames/s", "n_gpus": 1,
@@ -89,7 +97,9 @@ def main():
         "config": {"workload": f"{W}x{H} RGBA8, {F} frames, dips_alt run loop, FRAME_COUNT=2, default "
                                "DiPsProperties (colorize, window 1, sigmoid, scalar 5)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel": "alt_batch_kernel<0,0,1,2>",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     **({"traffic_source": traffic_src} if traffic_src else {}),
+                     "kernel": "alt_batch_kernel<0,0,1,true,2>",
                      "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": algo},
         "cpu_baseline": {"value": round(n_cpu / cpu_s, 4), "unit": "frames/s", "cores": 1, "kind": "port",
                          "sample": f"first {n_cpu} frames, oracle/dips_oracle.c DiPsCompute, {cpu_s:.2f} s",

@@ -11,35 +11,42 @@ import os
 import sys
 
 
-def per_dispatch(d, counter):
+def per_dispatch(d, counter, kernel):
     vals = []
     for f in glob.glob(os.path.join(d, counter, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "series_v2_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     return vals
 
 
 def main():
+    # usage: pmc_to_json.py DIR FRAMES MODE OUT [KERNEL BYTES_PER_FRAME]
     d, frames, mode, out = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
-    fetch = per_dispatch(d, "FETCH_SIZE")
-    write = per_dispatch(d, "WRITE_SIZE")
+    kernel = sys.argv[5] if len(sys.argv) > 5 else "series_v2_kernel"
+    W, H = 3840, 2160
+    bpf = int(sys.argv[6]) if len(sys.argv) > 6 else W * H * 3
+    fetch = per_dispatch(d, "FETCH_SIZE", kernel)
+    write = per_dispatch(d, "WRITE_SIZE", kernel)
     if not fetch or not write:
-        raise SystemExit(f"no series_v2_kernel rows (fetch {len(fetch)}, write {len(write)})")
-    fk = sum(fetch) / len(fetch)
-    wk = sum(write) / len(write)
-    W, H, C = 3840, 2160, 3
-    algo = frames * W * H * C
+        raise SystemExit(f"no {kernel} rows (fetch {len(fetch)}, write {len(write)})")
+    # the largest dispatches are the timed full-batch launches (a run may also
+    # hold short parity-check launches of the same kernel)
+    full_f = [v for v in fetch if v >= 0.5 * max(fetch)]
+    full_w = [v for v in write if v >= 0.5 * max(write)]
+    fk = sum(full_f) / len(full_f)
+    wk = sum(full_w) / len(full_w)
+    algo = frames * bpf
     res = {
-        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on bench.py, "
-                  "series_v2_kernel dispatches; FETCH_SIZE x2 (gfx950 wide-stream correction)",
+        "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), {kernel} full-batch "
+                  "dispatches; FETCH_SIZE x2 (gfx950 wide-stream correction)",
         "width": W, "height": H, "frames": frames, "mode": mode,
         "fetch_kib_raw": fk, "write_kib": wk,
         "read_bytes_per_launch": 2 * fk * 1024, "write_bytes_per_launch": wk * 1024,
         "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
         "algorithmic_bytes_per_launch": algo,
         "traffic_over_algorithmic": (2 * fk * 1024 + wk * 1024) / algo,
-        "dispatches": [len(fetch), len(write)],
+        "dispatches": [len(full_f), len(full_w)],
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
