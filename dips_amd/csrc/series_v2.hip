@@ -70,6 +70,8 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
             // (a wave-uniform skip of this exact sum when no lane has a pixel
             // above the threshold measured slower: if-converted by hipcc, or
             // as a forced branch it costs registers and occupancy)
+            // (the lane-predicated form `if (s0) si += a0` compiles to an
+            // unconditional add and two 32-bit selects of the f64: slower)
             si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
         }
         if constexpr (PF) st[u] = n;

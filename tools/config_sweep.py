@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""config_sweep.py -- every BASELINE.json config on one MI355X (the per-GPU
+slice of the multi-GPU ones), HBM-resident synthetic frames, timed with the
+library's hipEvents around the series kernel.  One JSON line per config plus
+a parity spot check of the first frames against the oracle.
+
+Run on the GPU box: python tools/config_sweep.py [--steps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# (name, width, height, channels, frames per GPU, mode, tau)
+CONFIGS = [
+    ("configs[0] 640x480 gray8, 300 frames, overall", 640, 480, 1, 300, 0, 0.0),
+    ("configs[1] 1920x1080 RGB8, 1000 frames, overall", 1920, 1080, 3, 1000, 0, 8 / 255),
+    ("configs[2] 3840x2160 RGB8, 5000 frames, per-frame", 3840, 2160, 3, 5000, 1, 8 / 255),
+    ("configs[3] 3840x2160 RGB8, 40000/8 frames per GPU, overall", 3840, 2160, 3, 5000, 0, 8 / 255),
+    ("configs[4] 7680x4320 RGB8, 10000/8 frames per GPU, f32 threshold", 7680, 4320, 3, 1250, 0, 8 / 255),
+    ("extra: 3840x2160 RGBA8, 3750 frames, per-frame", 3840, 2160, 4, 3750, 1, 8 / 255),
+    ("extra: 3840x2160 gray8, 15000 frames, per-frame", 3840, 2160, 1, 15000, 1, 8 / 255),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    from oracle import oracle
+
+    dev = torch.device("cuda", 0)
+    for name, W, H, C, F, mode, tau in CONFIGS:
+        shape = (F, H, W) if C == 1 else (F, H, W, C)
+        frames = torch.empty(shape, dtype=torch.uint8, device=dev)
+        op = DiffSeriesOperator(PixelFormat(C), Mode(mode), tau, time_kernel=True)
+        op.synth_device(frames, W, H, 0xD1B5, 0)
+        series = torch.zeros((F, 4), dtype=torch.int64, device=dev)
+        op.run_device(frames, series)
+        torch.cuda.synchronize()
+        op.kernel_time(reset=True)
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            op.run_device(frames, series)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t) / args.steps
+        kms, n = op.kernel_time()
+        kms /= max(n, 1)
+        host = frames[:3].cpu().numpy()
+        want, _, _ = oracle.series(host, mode=mode, tau=tau, nthreads=8)
+        ok = bool(np.array_equal(series[:3].cpu().numpy().view(np.uint64), want))
+        fb = W * H * C
+        print(json.dumps({"config": name, "frames_per_s": round(F / wall, 1),
+                          "kernel_ms": round(kms, 4), "kernel_GBps": round(F * fb / (kms / 1e3) / 1e9, 1),
+                          "frac_of_8TBps": round(F * fb / (kms / 1e3) / 8e12, 4),
+                          "first_frames_match_oracle": ok}), flush=True)
+        op.close()
+        del frames, series
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
