@@ -29,9 +29,10 @@
 namespace dips {
 
 // SJ from the intensity difference: 255 * |dI2| = |dJ| + err, |err| < 1.1e-4
-// (u() rounds up by < 2^-24, the sum and difference round by <= 2^-24 each),
-// so the per-lane f32 sum of |dI2s| * 255 * 2^-22 (exact multiplier, <= 8 px x
-// 510 < 4096: rounding < 2^-13 per add) is within 0.002 of the integer SJ.
+// (u() rounds up by < 2^-24, the sum and difference round by <= 2^-24 each;
+// exhaustive in tests/test_oracle.py), so the per-lane f32 sum of
+// |dI2s| * 255 * 2^-22 (exact multiplier, 16 px x 510 < 8192: rounding
+// <= 2^-11 per add) is within 0.01 of the integer SJ.
 constexpr float kSjMul = 255.0f / 4194304.0f;
 
 // One frame of one tile: accumulate against the reference state `st`
