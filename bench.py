@@ -127,7 +127,7 @@ def main():
 
     # Reference frame of the rank's first frame ('overall': broadcast once per
     # job, the reference is fixed; 'per-frame': the halo frame, exchanged
-    # every step by dips_amd.shard.exchange_halo).
+    # every step by dips_amd.shard.per_frame_overlapped).
     if mode == Mode.Overall:
         if rank == 0:
             ref.copy_(frames[0])
@@ -139,10 +139,12 @@ def main():
 
     def step():
         if mode == Mode.Overall:
-            r = ref
+            compute(frames, ref, series)
+        elif world == 1:
+            compute(frames, None, series)
         else:
-            r = shard.exchange_halo(frames, ref)
-        compute(frames, r, series)
+            # the halo transfer overlaps the compute of frames 1..F-1
+            shard.per_frame_overlapped(frames, ref, series, compute)
         return gather(series)
 
     final = None
@@ -161,7 +163,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t
     kms, launches = op.kernel_time()
-    tt = torch.tensor([elapsed, kms / max(launches, 1)], dtype=torch.float64, device=dev)
+    # series-kernel time per step (one launch per step, two when the halo
+    # overlap splits a per-frame batch at N > 1)
+    tt = torch.tensor([elapsed, kms / args.steps], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed_max, kernel_ms = float(tt[0]), float(tt[1])

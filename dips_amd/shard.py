@@ -59,6 +59,38 @@ def exchange_halo(local_frames: torch.Tensor, halo: torch.Tensor, group=None) ->
     return halo if rank > 0 else None
 
 
+def start_halo(local_frames: torch.Tensor, halo: torch.Tensor, group=None) -> List:
+    """Asynchronous form of exchange_halo: posts the send of this rank's last
+    frame and the receive of rank-1's last frame, returns the work handles
+    (empty on a single rank).  Frames 1.. of the shard do not depend on the
+    halo, so their compute can run while the transfer is in flight."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return []
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    ops = []
+    if rank + 1 < world and local_frames.shape[0] > 0:
+        ops.append(dist.P2POp(dist.isend, local_frames[-1].contiguous(), rank + 1, group))
+    if rank > 0:
+        ops.append(dist.P2POp(dist.irecv, halo, rank - 1, group))
+    return dist.batch_isend_irecv(ops) if ops else []
+
+
+def per_frame_overlapped(local_frames: torch.Tensor, halo: torch.Tensor, series: torch.Tensor,
+                         compute: Callable[[torch.Tensor, Optional[torch.Tensor], torch.Tensor], None],
+                         group=None) -> None:
+    """'per-frame' batch with the halo transfer hidden behind the compute of
+    frames 1..n-1 (each against its local predecessor); frame 0 is computed
+    against the received halo (or itself on rank 0) once the transfer lands."""
+    works = start_halo(local_frames, halo, group)
+    n = local_frames.shape[0]
+    if n > 1:
+        compute(local_frames[1:], local_frames[0], series[1:])
+    for w in works:
+        w.wait()
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    compute(local_frames[:1], halo if rank > 0 else None, series[:1])
+
+
 class SeriesGather:
     """Reassemble the per-rank series on rank 0 with one gather.
 

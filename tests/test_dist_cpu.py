@@ -33,7 +33,7 @@ def _oracle_compute(mode, tau):
     return compute
 
 
-def _worker(rank, world, port, n_total, mode, tau, result_q):
+def _worker(rank, world, port, n_total, mode, tau, result_q, overlapped=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -46,23 +46,30 @@ def _worker(rank, world, port, n_total, mode, tau, result_q):
         if mode == 0:
             reference = torch.from_numpy(all_frames[0].copy()) if rank == 0 else torch.empty_like(local[0])
             shard.broadcast_reference(reference)
-        full = shard.sharded_series(local, per_frame=(mode == 1), n_total=n_total,
-                                    compute=_oracle_compute(mode, tau), reference=reference)
+        if overlapped:
+            # bench.py's per-frame step: halo transfer behind frames 1..n-1
+            series = torch.zeros((local.shape[0], shard.SERIES_COLS), dtype=torch.int64)
+            halo = torch.empty_like(local[0])
+            shard.per_frame_overlapped(local, halo, series, _oracle_compute(mode, tau))
+            full = shard.SeriesGather(n_total, torch.device("cpu"))(series)
+        else:
+            full = shard.sharded_series(local, per_frame=(mode == 1), n_total=n_total,
+                                        compute=_oracle_compute(mode, tau), reference=reference)
         if rank == 0:
             result_q.put(full.numpy().copy())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode,overlapped", [(0, False), (1, False), (1, True)])
 @pytest.mark.parametrize("n_total", [7, 8])
-def test_sharded_equals_single(mode, n_total):
+def test_sharded_equals_single(mode, overlapped, n_total):
     from oracle import oracle
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, mode, 2 / 255, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, mode, 2 / 255, q, overlapped))
              for r in range(world)]
     for p in procs:
         p.start()
