@@ -179,9 +179,12 @@ class ComputeState:
     """Drop-in for dips/src/gpu/mod.rs ComputeState on a HIP device."""
 
     def __init__(self, colorize: bool, spatial_window_size: int, sensitivity: float,
-                 filter_type: DiPsFilter, chroma_filter: ChromaFilter, device: int = 0):
+                 filter_type: DiPsFilter, chroma_filter: ChromaFilter, device: int = 0,
+                 time_kernel: bool = False):
         self._hd = _Handle(_params(colorize, spatial_window_size, sensitivity, filter_type,
-                                   chroma_filter, fmt=PixelFormat.RGBA8), device)
+                                   chroma_filter, fmt=PixelFormat.RGBA8,
+                                   flags=_lib.FLAG_TIME_KERNEL if time_kernel else 0), device)
+        self._dev: Optional[_Handle] = None
         self._w = 0
         self._h = 0
 
@@ -201,6 +204,52 @@ class ComputeState:
         r = self._hd.check(self._hd._lib.dips_dispatch(self._hd.ptr, out.ctypes.data, out.nbytes))
         return out if r == 1 else None
 
+    def frame_callback_batch(self, width: int, height: int, frames) -> np.ndarray:
+        """len(frames) consecutive frame_callback calls (dips/src/lib.rs:233-246)
+        in one pass over HBM (dips_frame_callback_batch); frames [N, H, W, 4]."""
+        a = _as_u8(frames)
+        if a.size % (width * height * 4) != 0:
+            raise ValueError("frames must be [N, height, width, 4] RGBA8")
+        n = a.size // (width * height * 4)
+        out = np.empty((n, height, width, 4), dtype=np.uint8)
+        self._hd.check(self._hd._lib.dips_frame_callback_batch(self._hd.ptr, width, height, a.ctypes.data, n,
+                                                               out.ctypes.data))
+        self._w, self._h = width, height
+        return out
+
+    def frame_callback_batch_device(self, frames, out, stream=None) -> None:
+        """Device form: uint8 HIP tensors [N, H, W, 4], asynchronous on the
+        tensor's current stream.  Keeps its own ComputeState, separate from
+        the host-pointer calls of this object."""
+        n, h, w = int(frames.shape[0]), int(frames.shape[1]), int(frames.shape[2])
+        if tuple(frames.shape) != (n, h, w, 4) or tuple(out.shape) != tuple(frames.shape):
+            raise ValueError("frames/out must be [N, H, W, 4] uint8 tensors")
+        for t in (frames, out):
+            if not t.is_cuda or not t.is_contiguous():
+                raise ValueError("device path needs contiguous HIP tensors")
+        if self._dev is None:
+            p = DipsParams()
+            ctypes.memmove(ctypes.byref(p), ctypes.byref(self._hd.params), ctypes.sizeof(p))
+            p.flags |= _lib.FLAG_DEVICE_PTRS
+            self._dev = _Handle(p, self._hd.device)
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device).cuda_stream
+        lib = self._dev._lib
+        self._dev.check(lib.dips_set_stream(self._dev.ptr, ctypes.c_void_p(int(stream))))
+        self._dev.check(lib.dips_frame_callback_batch(self._dev.ptr, w, h, frames.data_ptr(), n, out.data_ptr()))
+
+    def kernel_time(self, reset: bool = False) -> Tuple[float, int]:
+        """hipEvent time of the batch kernel on the device handle (time_kernel=True)."""
+        ms, cnt = ctypes.c_double(), ctypes.c_uint64()
+        hd = self._dev
+        if hd is None:
+            return 0.0, 0
+        hd.check(hd._lib.dips_kernel_time(hd.ptr, ctypes.byref(ms), ctypes.byref(cnt)))
+        if reset:
+            hd.check(hd._lib.dips_kernel_time_reset(hd.ptr))
+        return ms.value, cnt.value
+
     def start_texture(self) -> Optional[np.ndarray]:
         out = np.empty((self._h, self._w, 4), dtype=np.uint8)
         r = self._hd.check(self._hd._lib.dips_start_texture(self._hd.ptr, out.ctypes.data, out.nbytes))
@@ -208,6 +257,8 @@ class ComputeState:
 
     def close(self) -> None:
         self._hd.close()
+        if self._dev is not None:
+            self._dev.close()
 
 
 def frame_callback(width: int, height: int, frame_data, compute: ComputeState) -> np.ndarray:
@@ -221,16 +272,32 @@ def frame_callback(width: int, height: int, frame_data, compute: ComputeState) -
 
 
 def perform_dips_frames(properties: DiPsProperties, frames: Iterable, width: int, height: int,
-                        device: int = 0) -> Iterator[np.ndarray]:
+                        device: int = 0, batch: int = 0) -> Iterator[np.ndarray]:
     """perform_dips (dips/src/lib.rs:252-257) minus the GStreamer decode
     front-end (out of scope): runs the frame callback over an iterable of
-    RGBA8 frames and yields the callback's outputs in order."""
+    RGBA8 frames and yields the callback's outputs in order.  With the
+    default callback and batch > 0, frames are grouped `batch` at a time
+    through dips_frame_callback_batch (same outputs, one device pass each)."""
     cs = ComputeState(properties.colorize_, properties.spatial_window_size_,
                       properties.sensitivity_, properties.filter_type_,
                       properties.chroma_filter_, device)
-    cb = properties.get_frame_callback() or frame_callback
-    for f in frames:
-        yield cb(width, height, f, cs)
+    cb = properties.get_frame_callback()
+    try:
+        if cb is None and batch > 0:
+            pending = []
+            for f in frames:
+                pending.append(np.asarray(f, dtype=np.uint8).reshape(height, width, 4))
+                if len(pending) == batch:
+                    yield from cs.frame_callback_batch(width, height, np.stack(pending))
+                    pending = []
+            if pending:
+                yield from cs.frame_callback_batch(width, height, np.stack(pending))
+            return
+        cb = cb or frame_callback
+        for f in frames:
+            yield cb(width, height, f, cs)
+    finally:
+        cs.close()
 
 
 # ---------------------------------------------------------------------------

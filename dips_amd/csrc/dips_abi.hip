@@ -8,6 +8,7 @@
 // dips_last_error().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -67,6 +68,10 @@ struct dips_handle {
     uint32_t uniform_idx = 0;  // starting_index uniform (bind_groups.rs:317-321)
     DevBuf slots[4], raw, start, out;
     HostPinned io;
+    uint64_t added = 0;       // frames added so far (global frame index of the next one)
+    DevBuf slots_alt[4];      // second ring for the multi-chunk batch kernel (swapped in after it)
+    DevBuf cb_frames, cb_out; // host-pointer staging of dips_frame_callback_batch
+    int cb_occupancy = 0;
 };
 
 namespace {
@@ -320,6 +325,9 @@ void dips_destroy(dips_handle* h) {
     h->stage_series.release();
     h->stage_map.release();
     for (auto& s : h->slots) s.release();
+    for (auto& s : h->slots_alt) s.release();
+    h->cb_frames.release();
+    h->cb_out.release();
     h->raw.release();
     h->start.release();
     h->out.release();
@@ -352,9 +360,14 @@ dips_status dips_synchronize(dips_handle* h) {
 // dips-compat ComputeState
 // ---------------------------------------------------------------------------
 
-dips_status dips_add_texture(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frame, size_t len) {
-    dips_status st = bind(h);
-    if (st != DIPS_OK) return st;
+}  // extern "C"
+
+namespace {
+
+// ComputeState::add_texture (dips/src/gpu/mod.rs:170-216) from a host frame
+// (through the pinned staging buffer) or a device frame (D2D).
+dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frame, size_t len,
+                             bool device_src) {
     if (!frame || width == 0 || height == 0) return fail(h, DIPS_ERR_INVALID, "add_texture: empty frame");
     const size_t fb = (size_t)width * height * 4u;
     if (len != fb) return fail(h, DIPS_ERR_INVALID, "add_texture: len != width*height*4 (RGBA8, stride width*4)");
@@ -369,12 +382,18 @@ dips_status dips_add_texture(dips_handle* h, uint32_t width, uint32_t height, co
         h->width = width;
         h->height = height;
     }
-    // upload through the pinned staging buffer (one PCIe transfer)
-    DIPS_HIP(h, hipStreamSynchronize(h->stream));
-    std::memcpy(h->io.p, frame, fb);
+    const uint8_t* src = frame;
+    hipMemcpyKind kind = hipMemcpyDeviceToDevice;
+    if (!device_src) {
+        // upload through the pinned staging buffer (one PCIe transfer)
+        DIPS_HIP(h, hipStreamSynchronize(h->stream));
+        std::memcpy(h->io.p, frame, fb);
+        src = h->io.bytes();
+        kind = hipMemcpyHostToDevice;
+    }
     if (!h->main_init) {
         // VecDeque phase (dips/src/gpu/mod.rs:171-177): frames 0..3 fill slots 0..3
-        DIPS_HIP(h, hipMemcpyAsync(h->slots[h->n_queued].p, h->io.p, fb, hipMemcpyHostToDevice, h->stream));
+        DIPS_HIP(h, hipMemcpyAsync(h->slots[h->n_queued].p, src, fb, kind, h->stream));
         h->n_queued += 1;
         if (h->n_queued == 4) {
             // PreComputeBindGroups::initialize + run_precompute_pipeline (:178-188)
@@ -393,17 +412,18 @@ dips_status dips_add_texture(dips_handle* h, uint32_t width, uint32_t height, co
         }
     } else {
         // update_temporal_texture (bind_groups.rs:407-427)
-        DIPS_HIP(h, hipMemcpyAsync(h->slots[h->ring_idx].p, h->io.p, fb, hipMemcpyHostToDevice, h->stream));
+        DIPS_HIP(h, hipMemcpyAsync(h->slots[h->ring_idx].p, src, fb, kind, h->stream));
         h->uniform_idx = h->ring_idx;
         h->ring_idx = (h->ring_idx + 1u) % 4u;
     }
-    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    h->added += 1;
+    if (!device_src) DIPS_HIP(h, hipStreamSynchronize(h->stream));
     return DIPS_OK;
 }
 
-int dips_dispatch(dips_handle* h, uint8_t* out, size_t cap) {
-    dips_status st = bind(h);
-    if (st != DIPS_OK) return st;
+// ComputeState::dispatch (dips/src/gpu/mod.rs:306-397) into `out`: a host
+// buffer (synchronous readback) or a device buffer (asynchronous).
+int dispatch_impl(dips_handle* h, uint8_t* out, size_t cap, bool device_dst) {
     if (!h->main_init) return 0;  // None (dips/src/gpu/mod.rs:394-396)
     const size_t fb = (size_t)h->width * h->height * 4u;
     if (!out) return fail(h, DIPS_ERR_INVALID, "dispatch: null output");
@@ -411,7 +431,7 @@ int dips_dispatch(dips_handle* h, uint8_t* out, size_t cap) {
     dips::CompatArgs a{};
     for (int k = 0; k < 4; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
     a.start = h->start.as<uint8_t>();
-    a.out = h->out.as<uint8_t>();
+    a.out = device_dst ? out : h->out.as<uint8_t>();
     a.width = h->width;
     a.height = h->height;
     a.newest = h->uniform_idx;
@@ -427,10 +447,130 @@ int dips_dispatch(dips_handle* h, uint8_t* out, size_t cap) {
         a.raw = h->raw.as<uint8_t>();
     }
     DIPS_HIP(h, dips::launch_compat_main(a, h->stream));
+    if (device_dst) return 1;
     DIPS_HIP(h, hipMemcpyAsync(h->io.p, h->out.p, fb, hipMemcpyDeviceToHost, h->stream));
     DIPS_HIP(h, hipStreamSynchronize(h->stream));
     std::memcpy(out, h->io.p, fb);
     return 1;
+}
+
+// frame_callback over frames[0..n) (device pointers), asynchronous: the
+// first frames of the stream one by one (start texture, unquantised ring),
+// then the steady state (global frame >= 7, W = 1) in one batch kernel.
+dips_status frame_callback_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames, uint32_t n,
+                                  uint8_t* out) {
+    const size_t fb = (size_t)width * height * 4u;
+    uint32_t t = 0;
+    for (; t < n && (h->added < 7 || h->p.spatial_window_size != 1); ++t) {
+        dips_status st = add_texture_impl(h, width, height, frames + (size_t)t * fb, fb, true);
+        if (st != DIPS_OK) return st;
+        const int r = dispatch_impl(h, out + (size_t)t * fb, fb, true);
+        if (r < 0) return (dips_status)r;
+        if (r == 0)  // frame_data.to_vec() (dips/src/lib.rs:244)
+            DIPS_HIP(h, hipMemcpyAsync(out + (size_t)t * fb, frames + (size_t)t * fb, fb, hipMemcpyDeviceToDevice,
+                                       h->stream));
+    }
+    if (t == n) return DIPS_OK;
+    if (width != h->width || height != h->height)
+        return fail(h, DIPS_ERR_INVALID, "frame_callback_batch: frame size changed after the first frame");
+    const uint8_t* bf = frames + (size_t)t * fb;
+    uint8_t* bo = out + (size_t)t * fb;
+    const uint32_t m = n - t;
+    const uint64_t npx = (uint64_t)width * height;
+    auto a16 = [](const void* q) { return ((uintptr_t)q & 15u) == 0; };
+    if (npx % 4u != 0 || fb >= (1ull << 31) || !a16(bf) || !a16(bo)) {
+        for (; t < n; ++t) {  // shapes the batch kernel does not take: frame by frame
+            dips_status st = add_texture_impl(h, width, height, frames + (size_t)t * fb, fb, true);
+            if (st != DIPS_OK) return st;
+            const int r = dispatch_impl(h, out + (size_t)t * fb, fb, true);
+            if (r < 0) return (dips_status)r;
+        }
+        return DIPS_OK;
+    }
+    const bool fast = dips::alt_fast_epilogue_ok(h->p.filter_type, h->p.sensitivity);
+    const void* k = dips::compat_batch_kernel_ptr((int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0,
+                                                  fast);
+    if (!k) return fail(h, DIPS_ERR_INVALID, "no batch kernel for these parameters");
+    if (h->cb_occupancy == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess || nb < 1) nb = 1;
+        h->cb_occupancy = nb;
+    }
+    const uint64_t n_vec = npx / 4u;
+    const uint64_t U = dips::kUnrollCompatBatch;
+    const uint64_t n_tiles = (n_vec + 64u * U - 1) / (64u * U);
+    const uint64_t resident = (uint64_t)h->cb_occupancy * 4u * (uint64_t)h->cu_count;
+    uint64_t n_chunks = (resident + n_tiles - 1) / n_tiles;
+    n_chunks = std::min<uint64_t>(n_chunks, (m + 15u) / 16u);
+    n_chunks = std::max<uint64_t>(n_chunks, 1);
+    const uint32_t chunk = (uint32_t)((m + n_chunks - 1) / n_chunks);
+    n_chunks = (m + chunk - 1) / chunk;
+    if (n_tiles * n_chunks >= (1ull << 31)) return fail(h, DIPS_ERR_INVALID, "batch too large; split it");
+
+    dips::CompatBatchArgs a{};
+    a.frames = bf;
+    a.out = bo;
+    a.start = h->start.as<uint8_t>();
+    const uint32_t r0 = h->ring_idx;  // slot of the batch's first frame
+    for (uint32_t j = 0; j < 3; ++j) a.pre[j] = h->slots[(r0 + 3u - j) % 4u].as<uint8_t>();
+    // with several chunks the last one would overwrite ring slots the first
+    // one still reads: write the new ring into the second set and swap
+    const bool swap = n_chunks > 1;
+    if (swap)
+        for (auto& sb : h->slots_alt) DIPS_HIP(h, sb.ensure(fb));
+    for (uint32_t j = 0; j < 4; ++j) {
+        a.post[j] = nullptr;
+        if (j < m) {
+            const uint32_t slot = (uint32_t)((r0 + (uint64_t)(m - 1 - j)) % 4u);
+            a.post[j] = (swap ? h->slots_alt[slot] : h->slots[slot]).as<uint8_t>();
+        }
+    }
+    a.frame_bytes = (uint32_t)fb;
+    a.n_vec = (uint32_t)n_vec;
+    a.n_frames = m;
+    a.chunk = chunk;
+    a.n_chunks = (uint32_t)n_chunks;
+    a.n_tiles = (uint32_t)n_tiles;
+    a.k = h->p.sensitivity;
+    a.kneg_half = -h->p.sensitivity * 0.5f;
+    const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
+        DIPS_HIP(h, hipEventRecord(e0, h->stream));
+    }
+    DIPS_HIP(h, dips::launch_compat_batch(a, (int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0, fast,
+                                          (uint32_t)((n_tiles * n_chunks + 3u) / 4u), h->stream));
+    if (timing) {
+        DIPS_HIP(h, hipEventRecord(e1, h->stream));
+        h->ev_pending.emplace_back(e0, e1);
+    }
+    if (swap) {
+        // m >= 16: all four slots were rewritten
+        for (int j = 0; j < 4; ++j) std::swap(h->slots[j], h->slots_alt[j]);
+    }
+    h->ring_idx = (uint32_t)((r0 + (uint64_t)m) % 4u);
+    h->uniform_idx = (h->ring_idx + 3u) % 4u;
+    h->added += m;
+    return DIPS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+dips_status dips_add_texture(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frame, size_t len) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    return add_texture_impl(h, width, height, frame, len, false);
+}
+
+int dips_dispatch(dips_handle* h, uint8_t* out, size_t cap) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    return dispatch_impl(h, out, cap, false);
 }
 
 int dips_frame_callback(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frame, size_t len,
@@ -442,6 +582,25 @@ int dips_frame_callback(dips_handle* h, uint32_t width, uint32_t height, const u
     const int r = dips_dispatch(h, out, cap);
     if (r == 0) std::memcpy(out, frame, len);  // frame_data.to_vec() (dips/src/lib.rs:244)
     return r;
+}
+
+dips_status dips_frame_callback_batch(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
+                                      uint32_t n_frames, uint8_t* out) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (n_frames == 0) return DIPS_OK;
+    if (!frames || !out || width == 0 || height == 0)
+        return fail(h, DIPS_ERR_INVALID, "frame_callback_batch: null or empty argument");
+    if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) return frame_callback_device(h, width, height, frames, n_frames, out);
+    const size_t total = (size_t)width * height * 4u * n_frames;
+    DIPS_HIP(h, h->cb_frames.ensure(total));
+    DIPS_HIP(h, h->cb_out.ensure(total));
+    DIPS_HIP(h, hipMemcpyAsync(h->cb_frames.p, frames, total, hipMemcpyHostToDevice, h->stream));
+    st = frame_callback_device(h, width, height, h->cb_frames.as<uint8_t>(), n_frames, h->cb_out.as<uint8_t>());
+    if (st != DIPS_OK) return st;
+    DIPS_HIP(h, hipMemcpyAsync(out, h->cb_out.p, total, hipMemcpyDeviceToHost, h->stream));
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    return DIPS_OK;
 }
 
 int dips_start_texture(dips_handle* h, uint8_t* out, size_t cap) {

@@ -75,6 +75,24 @@ struct CompatArgs {
     uint32_t colorize;
 };
 
+// dips ComputeState over a batch in steady state (compat_batch.hip).
+struct CompatBatchArgs {
+    const uint8_t* frames;   // n_frames x frame_bytes (RGBA8)
+    uint8_t* out;            // n_frames x frame_bytes (RGBA8)
+    const uint8_t* start;    // start texture (RGBA8 gray, R = S)
+    const uint8_t* pre[3];   // ring slots of the frames before frames[0] (gray texels): t-1, t-2, t-3
+    uint8_t* post[4];        // ring slots that receive frames n-1 .. n-4 as gray texels (null: none)
+    uint32_t frame_bytes;
+    uint32_t n_vec;          // 4-pixel vecs per frame
+    uint32_t n_frames, chunk, n_chunks, n_tiles;
+    float k;                 // sensitivity (SIGMOID_HORIZONTAL_SCALAR)
+    float kneg_half;         // -k / 2
+};
+constexpr int kUnrollCompatBatch = 2;
+const void* compat_batch_kernel_ptr(int chroma, int filter, bool colorize, bool fast);
+hipError_t launch_compat_batch(const CompatBatchArgs& a, int chroma, int filter, bool colorize, bool fast,
+                               uint32_t blocks, hipStream_t s);
+
 // dips_alt DiPsCompute (alt_kernels.hip).
 constexpr int kAltMaxTextures = 16;  // MAX_TEMPORAL_ARRAY_SIZE (dips_alt pre_compute_shader.wgsl:12)
 constexpr int kUnrollAlt = 2;        // vecs (4 px) per lane of alt_batch_kernel

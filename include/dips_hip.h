@@ -130,6 +130,17 @@ int dips_dispatch(dips_handle *h, uint8_t *out_rgba, size_t cap);
 int dips_frame_callback(dips_handle *h, uint32_t width, uint32_t height,
                         const uint8_t *frame_rgba, size_t len, uint8_t *out, size_t cap);
 
+/* `n_frames` consecutive frame_callback calls (dips/src/lib.rs:233-246) in
+ * one pass: frames and out are n_frames x width*height*4 RGBA8; out[t] is
+ * the visualisation, or the passthrough copy for the stream's first three
+ * frames.  The first frames of a stream (start texture, unquantised ring)
+ * and spatial windows W > 1 run frame by frame; the steady state (W = 1,
+ * from the stream's 8th frame) runs as one HBM-streaming kernel.  With
+ * DIPS_FLAG_DEVICE_PTRS both are device pointers and the call is
+ * asynchronous on the handle's stream; otherwise host pointers. */
+dips_status dips_frame_callback_batch(dips_handle *h, uint32_t width, uint32_t height, const uint8_t *frames,
+                                      uint32_t n_frames, uint8_t *out);
+
 /* Copy the start texture (RGBA8 gray, pre_compute_shader.wgsl:92-132) built
  * at the 4th frame.  Returns 1 if available, 0 if not yet built. */
 int dips_start_texture(dips_handle *h, uint8_t *out_rgba, size_t cap);

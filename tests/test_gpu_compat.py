@@ -107,3 +107,85 @@ def test_rejects_bad_input():
             cs.add_texture(8, 8, np.zeros((8, 7, 4), np.uint8))
     finally:
         cs.close()
+
+
+# ---------------------------------------------------------------------------
+# dips_frame_callback_batch: the steady-state batch kernel (compat_batch.hip)
+# ---------------------------------------------------------------------------
+
+def _oracle_callbacks(frames, params):
+    ref = oracle.ComputeState(*params)
+    h, w = frames.shape[1], frames.shape[2]
+    return np.stack([oracle.frame_callback(w, h, f, ref) for f in frames])
+
+
+BATCH_PARAMS = list(itertools.product([False, True], [1, 3], [5.0, 0.7, 200.0], [255, 0, 1], [0, 2]))
+
+
+@pytest.mark.parametrize("colorize,window,sens,filt,chroma", BATCH_PARAMS)
+def test_frame_callback_batch_matches_oracle(colorize, window, sens, filt, chroma):
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+    params = (colorize, window, sens, filt, chroma)
+    for (w, h), pieces in [((64, 48), [40]), ((64, 48), [3, 5, 32]), ((37, 21), [10, 30])]:
+        frames = _frames(w, h, 40, 21 + window + filt)
+        frames[20] = frames[19]
+        want = _oracle_callbacks(frames, params)
+        cs = ComputeState(colorize, window, sens, DiPsFilter(filt), ChromaFilter(chroma))
+        try:
+            outs, s = [], 0
+            for k in pieces:
+                outs.append(cs.frame_callback_batch(w, h, frames[s:s + k]))
+                s += k
+        finally:
+            cs.close()
+        got = np.concatenate(outs)
+        assert np.array_equal(got, want), ((w, h), pieces, np.argwhere(got != want)[:4])
+
+
+def test_frame_callback_batch_multi_chunk_and_mixed_calls():
+    """A small frame (4 tiles) over 150 frames runs as ~10 frame chunks (the
+    second ring set and the chunk-start rebuild from HBM); per-frame calls
+    before and after a batch see the same ComputeState."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
+    w, h = 64, 32
+    frames = _frames(w, h, 180, 77)
+    params = (True, 1, 5.0, 0, 0)
+    want = _oracle_callbacks(frames, params)
+    cs = ComputeState(True, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+    try:
+        got = [frame_callback(w, h, frames[t], cs) for t in range(9)]
+        got += list(cs.frame_callback_batch(w, h, frames[9:159]))
+        got += [frame_callback(w, h, frames[t], cs) for t in range(159, 165)]
+        got += list(cs.frame_callback_batch(w, h, frames[165:]))
+    finally:
+        cs.close()
+    assert np.array_equal(np.stack(got), want)
+
+
+def test_frame_callback_batch_device_4k():
+    import torch
+    from dips_amd import ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, PixelFormat
+    w, h, n = 3840, 2160, 24
+    dev = torch.empty((n, h, w, 4), dtype=torch.uint8, device="cuda")
+    op = DiffSeriesOperator(PixelFormat.RGBA8)
+    try:
+        op.synth_device(dev, w, h, 0xD1B5, 0)
+    finally:
+        op.close()
+    out = torch.empty_like(dev)
+    cs = ComputeState(False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
+    try:
+        cs.frame_callback_batch_device(dev, out)
+        torch.cuda.synchronize()
+        host = dev.cpu().numpy()
+        got = out.cpu().numpy()
+    finally:
+        cs.close()
+    ref = oracle.ComputeState(False, 1, 5.0, 255, 0)
+    for t in range(10):
+        assert np.array_equal(oracle.frame_callback(w, h, host[t], ref), got[t]), t
+    cs2 = ComputeState(False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
+    try:
+        assert np.array_equal(cs2.frame_callback_batch(w, h, host), got)
+    finally:
+        cs2.close()

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""compat_bench.py -- measurement of the dips ComputeState over a batch
+(dips_frame_callback_batch, compat_batch.hip): 3840x2160 RGBA8 synthetic
+frames resident in HBM (the appsink caps are RGBA, dips/src/frame_extractor.rs:
+141-148), frame_callback semantics with the default DiPsProperties (gray,
+window 1, Unfiltered; dips/src/lib.rs:74-86) or colour + sigmoid.  A step =
+one batch pass over frames that are all in the steady state (the stream's
+first 7 frames are fed once before timing).  Algorithmic HBM bytes per frame
+= W*H*4 read + W*H*4 written.  Prints one JSON line per property set.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+HBM_PEAK_GBS = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=1000)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+    from dips_amd import ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, PixelFormat
+    from oracle import oracle
+
+    W, H, F = 3840, 2160, args.frames
+    dev = torch.device("cuda", 0)
+    frames = torch.empty((F, H, W, 4), dtype=torch.uint8, device=dev)
+    op = DiffSeriesOperator(PixelFormat.RGBA8)
+    op.synth_device(frames, W, H, 0xD1B5, 0)
+    op.close()
+    out = torch.empty_like(frames)
+    for name, props in [("default (gray, Unfiltered)", (False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)),
+                        ("colorize + sigmoid k=5", (True, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_))]:
+        cs = ComputeState(*props, time_kernel=True)
+        cs.frame_callback_batch_device(frames[:7], out[:7])  # warm-up frames of the stream
+        for _ in range(args.warmup):
+            cs.frame_callback_batch_device(frames, out)
+        torch.cuda.synchronize()
+        cs.kernel_time(reset=True)
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            cs.frame_callback_batch_device(frames, out)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t
+        kms, launches = cs.kernel_time()
+        kernel_ms = kms / max(launches, 1)
+        cs.close()
+        # parity spot check: a fresh stream over the first 10 frames
+        cs2 = ComputeState(*props)
+        o2 = torch.empty_like(frames[:10])
+        cs2.frame_callback_batch_device(frames[:10], o2)
+        torch.cuda.synchronize()
+        cs2.close()
+        host = frames[:10].cpu().numpy()
+        ref = oracle.ComputeState(props[0], props[1], props[2], int(props[3]), int(props[4]))
+        want = np.stack([oracle.frame_callback(W, H, f, ref) for f in host])
+        algo = F * W * H * 8
+        achieved = algo / (kernel_ms / 1e3) / 1e9
+        print(json.dumps({
+            "metric": "dips ComputeState batch frames/s + achieved HBM GB/s, 4K RGBA8", "properties": name,
+            "value": round(F * args.steps / elapsed, 2), "unit": "frames/s", "kernel_ms": round(kernel_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": algo},
+            "first_10_frames_match_oracle": bool(np.array_equal(o2.cpu().numpy(), want)),
+        }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
