@@ -18,6 +18,7 @@
 #include "../../include/dips_hip.h"
 #include "dips_kernels.h"
 #include "host_buffers.h"
+#include "host_stream.h"
 
 namespace {
 
@@ -46,11 +47,15 @@ struct dips_alt_handle {
     uint64_t sent = 0;                    // frames sent; texture_index = sent % N (mod.rs:494, 523)
     uint64_t index = 0, overall = 0;      // run_dips_on_file loop state (lib.rs:566-567)
 
-    DevBuf out1, stage_frames, stage_out, meta;
+    DevBuf out1, meta;
+    dips_host::StreamPipe pipe;  // host-pointer feed of dips_alt_send_frames
     HostPinned io;
-    std::vector<uint8_t> meta_host;
-    hipEvent_t meta_done = nullptr;
-    bool meta_pending = false;
+    HostPinned meta_pin[2];  // per-batch flags + chunk table, pinned so the upload stays asynchronous
+    hipEvent_t meta_done[2] = {nullptr, nullptr};
+    hipEvent_t meta_free = nullptr;     // the last batch kernel that read the device table
+    hipStream_t meta_stream = nullptr;  // uploads of the table
+    bool meta_pending[2] = {false, false};
+    int meta_turn = 0;
     int occupancy = 0;
 
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
@@ -162,26 +167,41 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
     n_chunks = (n + chunk - 1) / chunk;
     if (n_tiles * n_chunks >= (1ull << 31)) return fail(h, DIPS_ERR_INVALID, "batch too large; split it");
 
-    // per-frame flags and per-chunk "last snapshot before the chunk"
+    // per-frame flags and per-chunk "last snapshot before the chunk", staged
+    // in one of two pinned buffers (reused once its previous upload is done)
     const size_t flag_bytes = ((size_t)n + 3u) & ~(size_t)3u;
-    if (h->meta_pending) {
-        ALT_HIP(h, hipEventSynchronize(h->meta_done));
-        h->meta_pending = false;
+    const size_t meta_bytes = flag_bytes + 4u * n_chunks;
+    const int mb = h->meta_turn;
+    h->meta_turn ^= 1;
+    if (h->meta_pending[mb]) {
+        ALT_HIP(h, hipEventSynchronize(h->meta_done[mb]));
+        h->meta_pending[mb] = false;
     }
-    h->meta_host.assign(flag_bytes + 4u * n_chunks, 0);
+    ALT_HIP(h, h->meta_pin[mb].ensure(meta_bytes));
+    uint8_t* meta_host = h->meta_pin[mb].bytes();
+    std::memset(meta_host, 0, meta_bytes);
     int32_t last = -1;
     std::vector<int32_t> cs(n_chunks, -1);
     for (uint32_t t = 0; t < n; ++t) {
         if (t % chunk == 0) cs[t / chunk] = last;
         const uint8_t f = flags && flags[t] ? 1 : 0;
-        h->meta_host[t] = f;
+        meta_host[t] = f;
         if (f) last = (int32_t)t;
     }
-    std::memcpy(h->meta_host.data() + flag_bytes, cs.data(), 4u * n_chunks);
-    ALT_HIP(h, h->meta.ensure(h->meta_host.size()));
-    ALT_HIP(h, hipMemcpyAsync(h->meta.p, h->meta_host.data(), h->meta_host.size(), hipMemcpyHostToDevice, s));
-    ALT_HIP(h, hipEventRecord(h->meta_done, s));
-    h->meta_pending = true;
+    std::memcpy(meta_host + flag_bytes, cs.data(), 4u * n_chunks);
+    if (meta_bytes > h->meta.cap) {
+        ALT_HIP(h, hipStreamSynchronize(s));  // the old table may still be read by a queued kernel
+        ALT_HIP(h, hipStreamSynchronize(h->meta_stream));
+        ALT_HIP(h, h->meta.ensure(meta_bytes));
+    }
+    // on its own idle stream: a small host-to-device copy queued behind
+    // other work on `s` can hold the host until `s` drains (measured: it
+    // serialised the pipelined host feed)
+    ALT_HIP(h, hipStreamWaitEvent(h->meta_stream, h->meta_free, 0));
+    ALT_HIP(h, hipMemcpyAsync(h->meta.p, meta_host, meta_bytes, hipMemcpyHostToDevice, h->meta_stream));
+    ALT_HIP(h, hipEventRecord(h->meta_done[mb], h->meta_stream));
+    ALT_HIP(h, hipStreamWaitEvent(s, h->meta_done[mb], 0));
+    h->meta_pending[mb] = true;
 
     dips::AltBatchArgs a{};
     a.frames = frames;
@@ -216,6 +236,7 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
         ALT_HIP(h, hipEventRecord(e1, s));
         h->ev_pending.emplace_back(e0, e1);
     }
+    ALT_HIP(h, hipEventRecord(h->meta_free, s));  // the next table upload waits for this kernel
     if (last >= 0) h->cur = 1 - h->cur;
     return DIPS_OK;
 }
@@ -253,9 +274,22 @@ dips_status send_frames_device(dips_alt_handle* h, const uint8_t* frames, uint32
     const uint64_t N = h->p.num_textures;
     const uint64_t end = h->sent + n;
     const uint64_t beg = end > h->sent + N ? end - N : h->sent;
-    for (uint64_t G = std::max(beg, h->sent); G < end; ++G)
-        ALT_HIP(h, hipMemcpyAsync(h->slots[G % N].p, frames + (size_t)(G - h->sent) * h->frame_bytes(),
-                                  h->frame_bytes(), hipMemcpyDeviceToDevice, s));
+    const size_t fb = h->frame_bytes();
+    const bool vec = fb % 16u == 0 && ((uintptr_t)frames & 15u) == 0;
+    dips::CopyFramesArgs ca{};
+    ca.n16 = fb / 16u;
+    uint32_t nc = 0;
+    for (uint64_t G = std::max(beg, h->sent); G < end; ++G) {
+        const uint8_t* src = frames + (size_t)(G - h->sent) * fb;
+        if (vec && N <= 2) {
+            ca.src[nc] = src;
+            ca.dst[nc] = h->slots[G % N].as<uint8_t>();
+            ++nc;
+        } else {
+            ALT_HIP(h, hipMemcpyAsync(h->slots[G % N].p, src, fb, hipMemcpyDeviceToDevice, s));
+        }
+    }
+    ALT_HIP(h, dips::launch_copy_frames(ca, nc, s));
     h->sent = end;
     return DIPS_OK;
 }
@@ -307,7 +341,10 @@ dips_status dips_alt_create(const dips_alt_params* params, uint32_t width, uint3
     e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&h->cu_count, hipDeviceAttributeMultiprocessorCount, device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->meta_done, hipEventDisableTiming);
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&h->meta_done[k], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->meta_free, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(h->meta_free, h->own_stream);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->meta_stream, hipStreamNonBlocking);
     // wgpu zero-initialises textures: slots, snapshot and output start at 0
     for (uint32_t k = 0; k < p.num_textures && e == hipSuccess; ++k) {
         e = h->slots[k].ensure(h->frame_bytes());
@@ -338,12 +375,16 @@ void dips_alt_destroy(dips_alt_handle* h) {
         (void)hipEventDestroy(pr.second);
     }
     for (auto e : h->ev_free) (void)hipEventDestroy(e);
-    if (h->meta_done) (void)hipEventDestroy(h->meta_done);
+    if (h->meta_stream) (void)hipStreamSynchronize(h->meta_stream);
+    for (auto& ev : h->meta_done)
+        if (ev) (void)hipEventDestroy(ev);
+    if (h->meta_free) (void)hipEventDestroy(h->meta_free);
+    if (h->meta_stream) (void)hipStreamDestroy(h->meta_stream);
+    for (auto& mp : h->meta_pin) mp.release();
     for (auto& s : h->slots) s.release();
     for (auto& s : h->snap) s.release();
     h->out1.release();
-    h->stage_frames.release();
-    h->stage_out.release();
+    h->pipe.release();
     h->meta.release();
     h->io.release();
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -413,13 +454,21 @@ dips_status dips_alt_send_frames(dips_alt_handle* h, const uint8_t* frames, uint
     if (n == 0) return DIPS_OK;
     if (!frames || !out) return fail(h, DIPS_ERR_INVALID, "send_frames: null frames or output");
     if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) return send_frames_device(h, frames, n, flags, out, h->stream);
-    const size_t total = h->frame_bytes() * (size_t)n;
-    ALT_HIP(h, h->stage_frames.ensure(total));
-    ALT_HIP(h, h->stage_out.ensure(total));
-    ALT_HIP(h, hipMemcpyAsync(h->stage_frames.p, frames, total, hipMemcpyHostToDevice, h->stream));
-    st = send_frames_device(h, h->stage_frames.as<uint8_t>(), n, flags, h->stage_out.as<uint8_t>(), h->stream);
-    if (st != DIPS_OK) return st;
-    ALT_HIP(h, hipMemcpyAsync(out, h->stage_out.p, total, hipMemcpyDeviceToHost, h->stream));
+    // host frames: pipelined upload / batch kernel / download, ~256 MiB chunks
+    const size_t fb = h->frame_bytes();
+    const uint64_t chunk = std::max<uint64_t>(1, (256ull << 20) / fb);
+    uint64_t done = 0;
+    int fst = 0;
+    ALT_HIP(h, dips_host::run_stream_pipe(
+                   h->pipe, h->stream, n, fb, fb, chunk, frames, out,
+                   [&](const uint8_t* din, uint8_t* dout, uint64_t m) {
+                       const int r = (int)send_frames_device(h, din, (uint32_t)m, flags ? flags + done : nullptr,
+                                                             dout, h->stream);
+                       done += m;
+                       return r;
+                   },
+                   &fst));
+    if (fst < 0) return (dips_status)fst;
     ALT_HIP(h, hipStreamSynchronize(h->stream));
     return DIPS_OK;
 }

@@ -349,4 +349,26 @@ hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool 
     return hipLaunchKernel(k, dim3(blocks), dim3(256), params, 0, s);
 }
 
+// Ring-slot refresh after a batch (write_texture, dips_alt mod.rs:510-521):
+// up to two frame copies in one launch on the compute stream.  A
+// device-to-device hipMemcpyAsync is an SDMA job, queued on the same copy
+// engines as the pipelined PCIe feed; as a kernel it takes a few microseconds
+// of HBM time instead.
+__global__ __launch_bounds__(256) void copy_frames_kernel(CopyFramesArgs a) {
+    const uint32_t j = blockIdx.y;
+    const uint4* __restrict__ src = reinterpret_cast<const uint4*>(a.src[j]);
+    uint4* __restrict__ dst = reinterpret_cast<uint4*>(a.dst[j]);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < a.n16; i += (uint64_t)gridDim.x * 256u)
+        dst[i] = src[i];
+}
+
+hipError_t launch_copy_frames(const CopyFramesArgs& a, uint32_t count, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    if (count > 2) return hipErrorInvalidValue;
+    const uint64_t want = (a.n16 + 255u) / 256u;
+    const uint32_t bx = (uint32_t)(want < 2048u ? (want == 0 ? 1u : want) : 2048u);
+    hipLaunchKernelGGL(copy_frames_kernel, dim3(bx, count), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 }  // namespace dips

@@ -23,11 +23,13 @@
 #include "../../include/dips_hip.h"
 #include "dips_kernels.h"
 #include "host_buffers.h"
+#include "host_stream.h"
 
 namespace {
 
 using dips_host::DevBuf;
 using dips_host::HostPinned;
+using dips_host::staged_copy;
 
 std::mutex g_err_mu;
 std::string g_create_err;
@@ -70,7 +72,7 @@ struct dips_handle {
     HostPinned io;
     uint64_t added = 0;       // frames added so far (global frame index of the next one)
     DevBuf slots_alt[4];      // second ring for the multi-chunk batch kernel (swapped in after it)
-    DevBuf cb_frames, cb_out; // host-pointer staging of dips_frame_callback_batch
+    dips_host::StreamPipe pipe;  // host-pointer feed of dips_frame_callback_batch
     int cb_occupancy = 0;
 };
 
@@ -326,8 +328,7 @@ void dips_destroy(dips_handle* h) {
     h->stage_map.release();
     for (auto& s : h->slots) s.release();
     for (auto& s : h->slots_alt) s.release();
-    h->cb_frames.release();
-    h->cb_out.release();
+    h->pipe.release();
     h->raw.release();
     h->start.release();
     h->out.release();
@@ -592,13 +593,17 @@ dips_status dips_frame_callback_batch(dips_handle* h, uint32_t width, uint32_t h
     if (!frames || !out || width == 0 || height == 0)
         return fail(h, DIPS_ERR_INVALID, "frame_callback_batch: null or empty argument");
     if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) return frame_callback_device(h, width, height, frames, n_frames, out);
-    const size_t total = (size_t)width * height * 4u * n_frames;
-    DIPS_HIP(h, h->cb_frames.ensure(total));
-    DIPS_HIP(h, h->cb_out.ensure(total));
-    DIPS_HIP(h, hipMemcpyAsync(h->cb_frames.p, frames, total, hipMemcpyHostToDevice, h->stream));
-    st = frame_callback_device(h, width, height, h->cb_frames.as<uint8_t>(), n_frames, h->cb_out.as<uint8_t>());
-    if (st != DIPS_OK) return st;
-    DIPS_HIP(h, hipMemcpyAsync(out, h->cb_out.p, total, hipMemcpyDeviceToHost, h->stream));
+    // host frames: pipelined upload / batch kernel / download, ~256 MiB chunks
+    const size_t fb = (size_t)width * height * 4u;
+    const uint64_t chunk = std::max<uint64_t>(1, (256ull << 20) / fb);
+    int fst = 0;
+    DIPS_HIP(h, dips_host::run_stream_pipe(
+                    h->pipe, h->stream, n_frames, fb, fb, chunk, frames, out,
+                    [&](const uint8_t* din, uint8_t* dout, uint64_t m) {
+                        return (int)frame_callback_device(h, width, height, din, (uint32_t)m, dout);
+                    },
+                    &fst));
+    if (fst < 0) return (dips_status)fst;
     DIPS_HIP(h, hipStreamSynchronize(h->stream));
     return DIPS_OK;
 }
@@ -656,30 +661,6 @@ dips_status dips_diff_series(dips_handle* h, uint32_t width, uint32_t height, co
     if (map) DIPS_HIP(h, hipMemcpyAsync(map, map_dev, total, hipMemcpyDeviceToHost, h->stream));
     DIPS_HIP(h, hipStreamSynchronize(h->stream));
     return DIPS_OK;
-}
-
-// Host -> pinned staging copy split over several threads: one thread's
-// memcpy from pageable memory runs well below the PCIe DMA rate.
-static void staged_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
-    const size_t kMinPerThread = 8u << 20;
-    unsigned nt = std::thread::hardware_concurrency();
-    nt = nt == 0 ? 1u : (nt > 8u ? 8u : nt);
-    if (bytes < 2 * kMinPerThread || nt == 1) {
-        std::memcpy(dst, src, bytes);
-        return;
-    }
-    if ((size_t)nt > bytes / kMinPerThread) nt = (unsigned)(bytes / kMinPerThread);
-    const size_t per = (bytes / nt + 63) & ~(size_t)63;
-    std::vector<std::thread> pool;
-    pool.reserve(nt - 1);
-    for (unsigned i = 1; i < nt; ++i) {
-        const size_t o = per * i;
-        if (o >= bytes) break;
-        const size_t len = o + per <= bytes ? per : bytes - o;
-        pool.emplace_back([=]() { std::memcpy(dst + o, src + o, len); });
-    }
-    std::memcpy(dst, src, per < bytes ? per : bytes);
-    for (auto& t : pool) t.join();
 }
 
 dips_status dips_diff_series_streamed(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* host_frames,

@@ -127,6 +127,13 @@ struct AltBatchArgs {                // a run of frames, N = 2, W = 1
 };
 
 hipError_t launch_alt_frame(const AltArgs& a, hipStream_t s);
+
+struct CopyFramesArgs {
+    const uint8_t* src[2];
+    uint8_t* dst[2];
+    uint64_t n16;  // 16-byte words per frame (16-byte aligned frames)
+};
+hipError_t launch_copy_frames(const CopyFramesArgs& a, uint32_t count, hipStream_t s);
 // fast: the branch-free epilogue (alt_fast_epilogue_ok)
 const void* alt_batch_kernel_ptr(int chroma, int filter, bool colorize, bool fast);
 hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool colorize, bool fast, uint32_t blocks,

@@ -1,0 +1,151 @@
+// host_stream.h -- pipelined host-memory feed for the batch operators
+// (internal to libdips_hip.so): frames in pageable host memory are copied
+// into pinned buffers by several threads, DMA'd to HBM on an upload stream,
+// processed on the compute stream and DMA'd back on a download stream, two
+// chunks in flight, so the PCIe transfers in both directions, the host copies
+// and the kernels overlap.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "host_buffers.h"
+
+namespace dips_host {
+
+// Host copy split over up to 8 threads (one thread's memcpy from pageable
+// memory runs well below the PCIe DMA rate).
+inline void staged_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
+    const size_t kMinPerThread = 8u << 20;
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt == 0 ? 1u : (nt > 8u ? 8u : nt);
+    if (bytes < 2 * kMinPerThread || nt == 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    if ((size_t)nt > bytes / kMinPerThread) nt = (unsigned)(bytes / kMinPerThread);
+    const size_t per = (bytes / nt + 63) & ~(size_t)63;
+    std::vector<std::thread> pool;
+    pool.reserve(nt - 1);
+    for (unsigned i = 1; i < nt; ++i) {
+        const size_t o = per * i;
+        if (o >= bytes) break;
+        const size_t len = o + per <= bytes ? per : bytes - o;
+        pool.emplace_back([=]() { std::memcpy(dst + o, src + o, len); });
+    }
+    std::memcpy(dst, src, per < bytes ? per : bytes);
+    for (auto& t : pool) t.join();
+}
+
+struct StreamPipe {
+    HostPinned pin_in[2], pin_out[2];
+    DevBuf dev_in[2], dev_out[2];
+    hipStream_t up = nullptr, down = nullptr;
+    hipEvent_t uploaded[2] = {nullptr, nullptr}, computed[2] = {nullptr, nullptr},
+               downloaded[2] = {nullptr, nullptr};
+
+    hipError_t init() {
+        if (up) return hipSuccess;
+        hipError_t e = hipStreamCreateWithFlags(&up, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&down, hipStreamNonBlocking);
+        for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+            e = hipEventCreateWithFlags(&uploaded[i], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&computed[i], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&downloaded[i], hipEventDisableTiming);
+        }
+        return e;
+    }
+    void release() {
+        if (up) (void)hipStreamSynchronize(up);
+        if (down) (void)hipStreamSynchronize(down);
+        for (int i = 0; i < 2; ++i) {
+            pin_in[i].release();
+            pin_out[i].release();
+            dev_in[i].release();
+            dev_out[i].release();
+            if (uploaded[i]) (void)hipEventDestroy(uploaded[i]);
+            if (computed[i]) (void)hipEventDestroy(computed[i]);
+            if (downloaded[i]) (void)hipEventDestroy(downloaded[i]);
+            uploaded[i] = computed[i] = downloaded[i] = nullptr;
+        }
+        if (up) (void)hipStreamDestroy(up);
+        if (down) (void)hipStreamDestroy(down);
+        up = down = nullptr;
+    }
+};
+
+// Process n items of `ib` input and `ob` output bytes each from host `in` to
+// host `out`, `chunk` items at a time: fn(dev_in, dev_out, count) enqueues the
+// compute of one chunk on `compute` (chunks in order) and returns 0 or a
+// negative status.  Returns hipSuccess, or the first HIP error (*fn_status
+// receives a negative fn result).
+template <typename Fn>
+hipError_t run_stream_pipe(StreamPipe& p, hipStream_t compute, uint64_t n, size_t ib, size_t ob, uint64_t chunk,
+                           const uint8_t* in, uint8_t* out, Fn&& fn, int* fn_status) {
+    *fn_status = 0;
+    hipError_t e = p.init();
+    if (e != hipSuccess) return e;
+    if (chunk == 0 || chunk > n) chunk = n;
+    for (int i = 0; i < 2; ++i) {
+        if ((e = p.pin_in[i].ensure(ib * chunk)) != hipSuccess) return e;
+        if ((e = p.pin_out[i].ensure(ob * chunk)) != hipSuccess) return e;
+        if ((e = p.dev_in[i].ensure(ib * chunk)) != hipSuccess) return e;
+        if ((e = p.dev_out[i].ensure(ob * chunk)) != hipSuccess) return e;
+    }
+    const uint64_t n_chunks = (n + chunk - 1) / chunk;
+    static const bool trace = std::getenv("DIPS_PIPE_TRACE") != nullptr;
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    auto count_of = [&](uint64_t k) { return (k + 1) * chunk <= n ? chunk : n - k * chunk; };
+    for (uint64_t k = 0; k <= n_chunks; ++k) {
+        if (k < n_chunks) {
+            const int b = (int)(k & 1u);
+            const uint64_t m = count_of(k);
+            // pin_in[b] and dev_in[b] were last used by chunk k-2
+            const auto t0 = clk::now();
+            if (k >= 2 && (e = hipEventSynchronize(p.uploaded[b])) != hipSuccess) return e;
+            const auto t1 = clk::now();
+            staged_copy(p.pin_in[b].bytes(), in + k * chunk * ib, m * ib);
+            const auto t2 = clk::now();
+            if (k >= 2 && (e = hipStreamWaitEvent(p.up, p.computed[b], 0)) != hipSuccess) return e;
+            if ((e = hipMemcpyAsync(p.dev_in[b].p, p.pin_in[b].p, m * ib, hipMemcpyHostToDevice, p.up)) != hipSuccess)
+                return e;
+            if ((e = hipEventRecord(p.uploaded[b], p.up)) != hipSuccess) return e;
+            // dev_out[b] was last read by chunk k-2's download
+            if ((e = hipStreamWaitEvent(compute, p.uploaded[b], 0)) != hipSuccess) return e;
+            if (k >= 2 && (e = hipStreamWaitEvent(compute, p.downloaded[b], 0)) != hipSuccess) return e;
+            const int st = fn(p.dev_in[b].template as<uint8_t>(), p.dev_out[b].template as<uint8_t>(), m);
+            if (st < 0) {
+                *fn_status = st;
+                return hipSuccess;
+            }
+            if ((e = hipEventRecord(p.computed[b], compute)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(p.down, p.computed[b], 0)) != hipSuccess) return e;
+            if ((e = hipMemcpyAsync(p.pin_out[b].p, p.dev_out[b].p, m * ob, hipMemcpyDeviceToHost, p.down)) != hipSuccess)
+                return e;
+            if ((e = hipEventRecord(p.downloaded[b], p.down)) != hipSuccess) return e;
+            if (trace)
+                std::fprintf(stderr, "pipe chunk %llu: wait_up %.2f copy_in %.2f enqueue %.2f ms\n",
+                             (unsigned long long)k, ms(t0, t1), ms(t1, t2), ms(t2, clk::now()));
+        }
+        if (k >= 1) {  // chunk k-1's results to the caller while chunk k runs
+            const int b = (int)((k - 1) & 1u);
+            const auto t0 = clk::now();
+            if ((e = hipEventSynchronize(p.downloaded[b])) != hipSuccess) return e;
+            const auto t1 = clk::now();
+            staged_copy(out + (k - 1) * chunk * ob, p.pin_out[b].bytes(), count_of(k - 1) * ob);
+            if (trace)
+                std::fprintf(stderr, "pipe chunk %llu: wait_down %.2f copy_out %.2f ms\n", (unsigned long long)(k - 1),
+                             ms(t0, t1), ms(t1, clk::now()));
+        }
+    }
+    return hipSuccess;
+}
+
+}  // namespace dips_host
