@@ -454,9 +454,9 @@ dips_status dips_alt_send_frames(dips_alt_handle* h, const uint8_t* frames, uint
     if (n == 0) return DIPS_OK;
     if (!frames || !out) return fail(h, DIPS_ERR_INVALID, "send_frames: null frames or output");
     if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) return send_frames_device(h, frames, n, flags, out, h->stream);
-    // host frames: pipelined upload / batch kernel / download, ~256 MiB chunks
+    // host frames: pipelined upload / batch kernel / download in chunks
     const size_t fb = h->frame_bytes();
-    const uint64_t chunk = std::max<uint64_t>(1, (256ull << 20) / fb);
+    const uint64_t chunk = dips_host::feed_chunk_frames(fb);
     uint64_t done = 0;
     int fst = 0;
     ALT_HIP(h, dips_host::run_stream_pipe(

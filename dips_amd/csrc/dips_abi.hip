@@ -593,9 +593,9 @@ dips_status dips_frame_callback_batch(dips_handle* h, uint32_t width, uint32_t h
     if (!frames || !out || width == 0 || height == 0)
         return fail(h, DIPS_ERR_INVALID, "frame_callback_batch: null or empty argument");
     if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) return frame_callback_device(h, width, height, frames, n_frames, out);
-    // host frames: pipelined upload / batch kernel / download, ~256 MiB chunks
+    // host frames: pipelined upload / batch kernel / download in chunks
     const size_t fb = (size_t)width * height * 4u;
-    const uint64_t chunk = std::max<uint64_t>(1, (256ull << 20) / fb);
+    const uint64_t chunk = dips_host::feed_chunk_frames(fb);
     int fst = 0;
     DIPS_HIP(h, dips_host::run_stream_pipe(
                     h->pipe, h->stream, n_frames, fb, fb, chunk, frames, out,

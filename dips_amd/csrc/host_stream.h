@@ -43,6 +43,20 @@ inline void staged_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
     for (auto& t : pool) t.join();
 }
 
+// Frames per pipelined chunk: ~256 MiB (two chunks in flight per direction
+// keep both PCIe directions and the kernel busy); DIPS_FEED_CHUNK_BYTES
+// overrides the byte budget (the tests use it to force many ragged chunks
+// at small frame sizes).
+inline uint64_t feed_chunk_frames(size_t frame_bytes) {
+    uint64_t budget = 256ull << 20;
+    if (const char* e = std::getenv("DIPS_FEED_CHUNK_BYTES")) {
+        const unsigned long long v = std::strtoull(e, nullptr, 10);
+        if (v > 0) budget = v;
+    }
+    const uint64_t n = budget / (frame_bytes ? frame_bytes : 1);
+    return n ? n : 1;
+}
+
 struct StreamPipe {
     HostPinned pin_in[2], pin_out[2];
     DevBuf dev_in[2], dev_out[2];

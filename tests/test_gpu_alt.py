@@ -174,3 +174,22 @@ def test_rejects_bad_input():
             c.send_frame(np.zeros((8, 7, 4), np.uint8))
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("chunk_frames", [1, 4, 9])
+def test_run_host_feed_chunks(monkeypatch, chunk_frames):
+    """Host frames go through the pipelined feed in chunks; with a few frames
+    per chunk (ragged last chunk, refresh markers and snapshots falling on
+    chunk edges) the loop's outputs equal the oracle's."""
+    from dips_amd.alt import DiPsRunner
+    w, h = 32, 24
+    monkeypatch.setenv("DIPS_FEED_CHUNK_BYTES", str(chunk_frames * w * h * 4))
+    frames = _frames(w, h, 50, 40 + chunk_frames)
+    markers = [4, 9, 10, 27, 36]
+    want = oracle.AltCompute(2, w, h, True, 1, 5.0, 0, 0).run(frames, markers)
+    r = DiPsRunner(h, w, _props(True, 1, 5.0, 0, 0), markers)
+    try:
+        got = np.concatenate([r(frames[:13]), r(frames[13:])])
+    finally:
+        r.close()
+    assert np.array_equal(got, want), np.argwhere(got != want)[:4]

@@ -189,3 +189,22 @@ def test_frame_callback_batch_device_4k():
         assert np.array_equal(cs2.frame_callback_batch(w, h, host), got)
     finally:
         cs2.close()
+
+
+@pytest.mark.parametrize("chunk_frames", [1, 3, 7])
+def test_frame_callback_batch_host_feed_chunks(monkeypatch, chunk_frames):
+    """The host-pointer batch is fed through the pipelined upload / kernel /
+    download in chunks (two in flight); forced down to a few frames per chunk
+    with a ragged last chunk, the outputs stay those of the oracle."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+    w, h = 64, 48
+    monkeypatch.setenv("DIPS_FEED_CHUNK_BYTES", str(chunk_frames * w * h * 4))
+    frames = _frames(w, h, 61, 5 + chunk_frames)
+    params = (True, 1, 5.0, 0, 0)
+    want = _oracle_callbacks(frames, params)
+    cs = ComputeState(True, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+    try:
+        got = np.concatenate([cs.frame_callback_batch(w, h, frames[:5]), cs.frame_callback_batch(w, h, frames[5:])])
+    finally:
+        cs.close()
+    assert np.array_equal(got, want), np.argwhere(got != want)[:4]
