@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--mode", choices=["per-frame", "overall"], default="per-frame")
     ap.add_argument("--tau", type=float, default=8.0 / 255.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true",
+                    help="rank 0 recomputes the series of all N*F frames in one single-device launch "
+                         "and requires the gathered series to equal it (functional check of the N>1 path)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU work of the cpu_baseline sample")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -104,7 +107,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local)  # one rank per GPU (RCCL rejects two ranks on one device)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
@@ -176,6 +179,16 @@ def main():
         assert final.shape == (world * F, 4)
         if mode == Mode.PerFrame:
             assert final[0].sum() == 0  # frame 0 against itself
+        if args.check:
+            # the same N*F frames in one launch on one device (small sizes only)
+            allf = torch.empty((world * F, H, W, C), dtype=torch.uint8, device=dev)
+            op.synth_device(allf, W, H, SEED, 0)
+            one = torch.zeros((world * F, 4), dtype=torch.int64, device=dev)
+            op.run_device(allf, one, ref=None if mode == Mode.PerFrame else allf[0])
+            torch.cuda.synchronize()
+            assert np.array_equal(final, one.cpu().numpy().view(np.uint64)), "gathered series != single-device series"
+            log(f"check: gathered series of {world}x{F} frames equals the single-device series")
+            del allf, one
         waves, tiles, pbytes = op.geometry(W, H, F)
         algo_bytes = F * fb  # each frame read once per launch
         achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
