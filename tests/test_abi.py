@@ -31,6 +31,15 @@ def test_header_functions_exported():
     assert lib.dips_abi_version() == 1
 
 
+def test_integration_binds_every_entry_point():
+    """INTEGRATION.md's Rust extern blocks name every function the header
+    declares (the binding a maintainer adds is complete)."""
+    with open(os.path.join(ROOT, "INTEGRATION.md")) as f:
+        doc = f.read()
+    missing = [n for n in _lib.header_functions() if f"fn {n}(" not in doc]
+    assert not missing, missing
+
+
 def test_library_is_gfx950_code_object():
     with open(_lib.LIB_PATH, "rb") as f:
         blob = f.read()
