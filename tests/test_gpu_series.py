@@ -216,3 +216,26 @@ def test_device_path_matches_host_path():
             assert np.array_equal(got, out4)
         finally:
             op.close()
+
+
+@pytest.mark.parametrize("c", [1, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_long_batch_segments_match_oracle(c, mode):
+    """A small frame over thousands of frames: every resident wave walks a
+    multi-frame segment (the unrolled 4-frame ring, the tail and segments
+    that start mid-tile or cross into the next tile), the last tile is
+    ragged.  Every frame's entry and the full byte map equal the oracle."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    w, h = 80, 36  # 2880 px: 2.8 RGB tiles of 1024 px, 1.4 gray tiles of 2048 px
+    n = 20011 if c == 1 else 8009
+    frames = _frames(c, w, h, n, 40 + c + mode, "random")
+    for chroma, tau in [(0, 8 / 255), (1, 0.0)] if c != 1 else [(0, 8 / 255), (0, 0.0)]:
+        op = DiffSeriesOperator(PixelFormat(c), Mode(mode), tau, chroma)
+        try:
+            got, gmap = op(frames, want_map=True)
+            got_nomap, _ = op(frames)
+        finally:
+            op.close()
+        out4, si, dmap = oracle.series(frames, mode=mode, chroma=chroma, tau=tau, want_map=True, nthreads=8)
+        _check(got, out4, si, gmap, dmap)
+        _check(got_nomap, out4, si)
