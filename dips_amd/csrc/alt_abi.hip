@@ -49,6 +49,7 @@ struct dips_alt_handle {
 
     DevBuf out1, meta;
     dips_host::StreamPipe pipe;  // host-pointer feed of dips_alt_send_frames
+    dips_host::PieceEvents pieces;  // per-piece completion of send_frame's readback
     HostPinned io;
     HostPinned meta_pin[2];  // per-batch flags + chunk table, pinned so the upload stays asynchronous
     hipEvent_t meta_done[2] = {nullptr, nullptr};
@@ -385,6 +386,7 @@ void dips_alt_destroy(dips_alt_handle* h) {
     for (auto& s : h->snap) s.release();
     h->out1.release();
     h->pipe.release();
+    h->pieces.release();
     h->meta.release();
     h->io.release();
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -420,11 +422,11 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     ALT_HIP(h, h->io.ensure(fb));
     ALT_HIP(h, h->out1.ensure(fb));
     ALT_HIP(h, hipStreamSynchronize(h->stream));
-    std::memcpy(h->io.p, frame, fb);
     // queue.write_texture into slot texture_index, then texture_index += 1
+    // (through the pinned buffer in pieces: host copy and DMA overlapped)
     const uint32_t N = h->p.num_textures;
     uint8_t* slot = h->slots[h->sent % N].as<uint8_t>();
-    ALT_HIP(h, hipMemcpyAsync(slot, h->io.p, fb, hipMemcpyHostToDevice, h->stream));
+    ALT_HIP(h, dips_host::upload_via(slot, frame, fb, h->io.bytes(), h->stream));
     h->sent += 1;
     dips::AltArgs a{};
     for (uint32_t k = 0; k < N; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
@@ -441,9 +443,7 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     a.snapshot = snapshot ? 1u : 0u;
     ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
     // copy_texture_to_buffer + map_async + de-pad (mod.rs:597-643)
-    ALT_HIP(h, hipMemcpyAsync(h->io.p, h->out1.p, fb, hipMemcpyDeviceToHost, h->stream));
-    ALT_HIP(h, hipStreamSynchronize(h->stream));
-    std::memcpy(out, h->io.p, fb);
+    ALT_HIP(h, dips_host::download_via(out, h->out1.p, fb, h->io.bytes(), h->stream, h->pieces));
     return DIPS_OK;
 }
 

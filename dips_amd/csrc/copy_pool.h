@@ -1,0 +1,138 @@
+// copy_pool.h -- persistent host worker threads for the PCIe staging copies
+// (internal to libdips_hip.so).
+//
+// A single host thread copies pageable memory at a fraction of the PCIe DMA
+// rate, and creating threads per call costs tens of microseconds each, which
+// is too much for the per-frame operators (one 4K frame = 33 MB, ~0.6 ms of
+// DMA).  The pool keeps up to 7 workers parked on a condition variable;
+// run(n, fn) executes fn(0..n-1) on the workers and the calling thread and
+// returns when all are done.  One run at a time (a process-wide mutex): the
+// handles are not internally synchronised, but different handles may be
+// driven from different threads.  A child process created by fork() gets a
+// fresh pool (the parent's workers do not exist there).
+#pragma once
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace dips_host {
+
+class CopyPool {
+   public:
+    explicit CopyPool(unsigned workers) {
+        for (unsigned i = 0; i < workers; ++i) th_.emplace_back([this]() { loop(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    CopyPool(const CopyPool&) = delete;
+    CopyPool& operator=(const CopyPool&) = delete;
+
+    unsigned threads() const { return (unsigned)th_.size() + 1u; }
+
+    // fn(i) for every i in [0, n), spread over the workers and the caller.
+    void run(size_t n, const std::function<void(size_t)>& fn) {
+        if (n == 0) return;
+        std::lock_guard<std::mutex> one_run(run_mu_);
+        if (n == 1 || th_.empty()) {
+            for (size_t i = 0; i < n; ++i) fn(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &fn;
+            n_ = n;
+            next_.store(0, std::memory_order_relaxed);
+            busy_ = (unsigned)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain(fn, n);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this]() { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+
+    // The process-wide pool: min(8, hardware threads) - 1 workers.
+    static CopyPool& global() {
+        static std::mutex mu;
+        static CopyPool* pool = nullptr;
+        static pid_t owner = 0;
+        std::lock_guard<std::mutex> lk(mu);
+        if (!pool || owner != getpid()) {
+            // after fork() the parent's workers are gone: leak the copy the
+            // child inherited and start a new one
+            unsigned hw = std::thread::hardware_concurrency();
+            hw = hw == 0 ? 1u : std::min(hw, 8u);
+            pool = new CopyPool(hw - 1u);
+            owner = getpid();
+        }
+        return *pool;
+    }
+
+   private:
+    void drain(const std::function<void(size_t)>& fn, size_t n) {
+        for (size_t i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) fn(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(size_t)>* fn;
+            size_t n;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&]() { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                fn = fn_;
+                n = n_;
+            }
+            drain(*fn, n);
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (--busy_ == 0) done_cv_.notify_one();
+            }
+        }
+    }
+
+    std::vector<std::thread> th_;
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(size_t)>* fn_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    unsigned busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// Host copy in ~4 MiB pieces over the pool.
+inline void pool_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
+    const size_t kPiece = 4u << 20;
+    if (bytes < 2 * kPiece) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t n = (bytes + kPiece - 1) / kPiece;
+    CopyPool::global().run(n, [&](size_t i) {
+        const size_t o = i * kPiece;
+        std::memcpy(dst + o, src + o, std::min(kPiece, bytes - o));
+    });
+}
+
+}  // namespace dips_host

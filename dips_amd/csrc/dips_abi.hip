@@ -73,6 +73,7 @@ struct dips_handle {
     uint64_t added = 0;       // frames added so far (global frame index of the next one)
     DevBuf slots_alt[4];      // second ring for the multi-chunk batch kernel (swapped in after it)
     dips_host::StreamPipe pipe;  // host-pointer feed of dips_frame_callback_batch
+    dips_host::PieceEvents pieces;  // per-piece completion of the per-frame readback
     int cb_occupancy = 0;
 };
 
@@ -329,6 +330,7 @@ void dips_destroy(dips_handle* h) {
     for (auto& s : h->slots) s.release();
     for (auto& s : h->slots_alt) s.release();
     h->pipe.release();
+    h->pieces.release();
     h->raw.release();
     h->start.release();
     h->out.release();
@@ -383,18 +385,16 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
         h->width = width;
         h->height = height;
     }
-    const uint8_t* src = frame;
-    hipMemcpyKind kind = hipMemcpyDeviceToDevice;
-    if (!device_src) {
-        // upload through the pinned staging buffer (one PCIe transfer)
-        DIPS_HIP(h, hipStreamSynchronize(h->stream));
-        std::memcpy(h->io.p, frame, fb);
-        src = h->io.bytes();
-        kind = hipMemcpyHostToDevice;
-    }
+    // host frames go up through the pinned staging buffer in pieces (host
+    // copy and PCIe transfer overlapped); device frames are copied in HBM
+    auto put = [&](void* dst) -> hipError_t {
+        if (device_src) return hipMemcpyAsync(dst, frame, fb, hipMemcpyDeviceToDevice, h->stream);
+        const hipError_t e = hipStreamSynchronize(h->stream);  // the staging buffer is free again
+        return e != hipSuccess ? e : dips_host::upload_via(dst, frame, fb, h->io.bytes(), h->stream);
+    };
     if (!h->main_init) {
         // VecDeque phase (dips/src/gpu/mod.rs:171-177): frames 0..3 fill slots 0..3
-        DIPS_HIP(h, hipMemcpyAsync(h->slots[h->n_queued].p, src, fb, kind, h->stream));
+        DIPS_HIP(h, put(h->slots[h->n_queued].p));
         h->n_queued += 1;
         if (h->n_queued == 4) {
             // PreComputeBindGroups::initialize + run_precompute_pipeline (:178-188)
@@ -413,7 +413,7 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
         }
     } else {
         // update_temporal_texture (bind_groups.rs:407-427)
-        DIPS_HIP(h, hipMemcpyAsync(h->slots[h->ring_idx].p, src, fb, kind, h->stream));
+        DIPS_HIP(h, put(h->slots[h->ring_idx].p));
         h->uniform_idx = h->ring_idx;
         h->ring_idx = (h->ring_idx + 1u) % 4u;
     }
@@ -449,9 +449,9 @@ int dispatch_impl(dips_handle* h, uint8_t* out, size_t cap, bool device_dst) {
     }
     DIPS_HIP(h, dips::launch_compat_main(a, h->stream));
     if (device_dst) return 1;
-    DIPS_HIP(h, hipMemcpyAsync(h->io.p, h->out.p, fb, hipMemcpyDeviceToHost, h->stream));
-    DIPS_HIP(h, hipStreamSynchronize(h->stream));
-    std::memcpy(out, h->io.p, fb);
+    // readback (copy_texture_to_buffer + map, gpu/mod.rs:342-393) in pieces,
+    // each copied out as soon as its DMA lands
+    DIPS_HIP(h, dips_host::download_via(out, h->out.p, fb, h->io.bytes(), h->stream, h->pieces));
     return 1;
 }
 
@@ -581,7 +581,7 @@ int dips_frame_callback(dips_handle* h, uint32_t width, uint32_t height, const u
     dips_status st = dips_add_texture(h, width, height, frame, len);
     if (st != DIPS_OK) return st;
     const int r = dips_dispatch(h, out, cap);
-    if (r == 0) std::memcpy(out, frame, len);  // frame_data.to_vec() (dips/src/lib.rs:244)
+    if (r == 0) dips_host::pool_copy(out, frame, len);  // frame_data.to_vec() (dips/src/lib.rs:244)
     return r;
 }
 
