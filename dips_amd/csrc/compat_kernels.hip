@@ -30,9 +30,9 @@ __device__ __forceinline__ float texel_intensity(const uint8_t* img, uint64_t p,
 
 // Stage the intensity neighbourhood of this workgroup's tile.
 __device__ void stage_tile(float (*tile)[kLds], const uint8_t* img, uint32_t w, uint32_t h, int halo,
-                           uint32_t chroma) {
+                           uint32_t chroma, uint32_t y0 = 0) {
     const int ox = (int)(blockIdx.x * kTile) - halo;
-    const int oy = (int)(blockIdx.y * kTile) - halo;
+    const int oy = (int)(y0 + blockIdx.y * kTile) - halo;
     const int span = kTile + 2 * halo;
     for (int idx = threadIdx.y * kTile + threadIdx.x; idx < span * span; idx += kTile * kTile) {
         const int ty = idx / span, tx = idx - ty * span;
@@ -102,15 +102,16 @@ __global__ __launch_bounds__(256) void compat_precompute_kernel(CompatArgs a) {
 __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
     __shared__ float tile[kLds][kLds];
     const uint32_t x = blockIdx.x * kTile + threadIdx.x;
-    const uint32_t y = blockIdx.y * kTile + threadIdx.y;
-    const bool inside = x < a.width && y < a.height;
+    const uint32_t y = a.y0 + blockIdx.y * kTile + threadIdx.y;
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    const bool inside = x < a.width && y < yend;
     const uint64_t p = (uint64_t)y * a.width + x;
     float fi;
     if (a.window == 1) {
         if (!inside) return;
         fi = texel_intensity(a.raw, p, a.chroma);
     } else {
-        stage_tile(tile, a.raw, a.width, a.height, a.window / 2, a.chroma);
+        stage_tile(tile, a.raw, a.width, a.height, a.window / 2, a.chroma, a.y0);
         __syncthreads();
         if (!inside) return;
         fi = window_select(tile, a.window);
@@ -136,7 +137,9 @@ hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s) {
-    dim3 grid((a.width + kTile - 1) / kTile, (a.height + kTile - 1) / kTile);
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
+    dim3 grid((a.width + kTile - 1) / kTile, (yend - a.y0 + kTile - 1) / kTile);
     hipLaunchKernelGGL(compat_main_kernel, grid, dim3(kTile, kTile), 0, s, a);
     return hipGetLastError();
 }

@@ -9,8 +9,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -74,6 +76,8 @@ struct dips_handle {
     DevBuf slots_alt[4];      // second ring for the multi-chunk batch kernel (swapped in after it)
     dips_host::StreamPipe pipe;  // host-pointer feed of dips_frame_callback_batch
     dips_host::PieceEvents pieces;  // per-piece completion of the per-frame readback
+    dips_host::PieceEvents up_pieces;  // per-stripe upload completion (striped frame_callback)
+    HostPinned io_out;                 // readback staging of the striped frame_callback
     int cb_occupancy = 0;
 };
 
@@ -331,6 +335,8 @@ void dips_destroy(dips_handle* h) {
     for (auto& s : h->slots_alt) s.release();
     h->pipe.release();
     h->pieces.release();
+    h->up_pieces.release();
+    h->io_out.release();
     h->raw.release();
     h->start.release();
     h->out.release();
@@ -558,6 +564,75 @@ dips_status frame_callback_device(dips_handle* h, uint32_t width, uint32_t heigh
     return DIPS_OK;
 }
 
+// frame_callback in steady state (ComputeState initialised, W = 1, host
+// pointers): add_texture + dispatch with the frame cut into ~4 MiB row
+// stripes.  Stripe s is staged by the copy pool and DMA'd on copy_stream;
+// the main kernel of stripe s (W = 1 is per pixel) runs as soon as its rows
+// have landed and the stripe's readback follows on the compute stream, so
+// stripe s comes back while stripes s+1.. still go up (both PCIe directions
+// at once).  Same outputs and ring state as add_texture + dispatch.
+int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
+    const uint32_t W = h->width, H = h->height;
+    const size_t row = (size_t)W * 4u, fb = row * H;
+    const uint32_t rows = (uint32_t)std::max<size_t>(1, dips_host::piece_bytes() / row);
+    const uint32_t n_s = (H + rows - 1) / rows;
+    DIPS_HIP(h, h->io_out.ensure(fb));
+    DIPS_HIP(h, h->up_pieces.ensure(n_s));
+    DIPS_HIP(h, h->pieces.ensure(n_s));
+    // the previous call's transfers out of io / into io_out are complete
+    // once the compute stream (which waited for every upload) has drained
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    // update_temporal_texture (bind_groups.rs:407-427)
+    uint8_t* slot = h->slots[h->ring_idx].as<uint8_t>();
+    h->uniform_idx = h->ring_idx;
+    h->ring_idx = (h->ring_idx + 1u) % 4u;
+    h->added += 1;
+    uint8_t* pin_in = h->io.bytes();
+    std::atomic<int> err{(int)hipSuccess};
+    dips_host::CopyPool::global().run(n_s, [&](size_t si) {
+        const size_t o = si * rows * row, len = std::min<size_t>((size_t)rows * row, fb - o);
+        std::memcpy(pin_in + o, frame + o, len);
+        hipError_t e = hipMemcpyAsync(slot + o, pin_in + o, len, hipMemcpyHostToDevice, h->copy_stream);
+        if (e == hipSuccess) e = hipEventRecord(h->up_pieces.ev[si], h->copy_stream);
+        if (e != hipSuccess) err.store((int)e);
+    });
+    DIPS_HIP(h, (hipError_t)err.load());
+    dips::CompatArgs a{};
+    for (int k = 0; k < 4; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
+    a.start = h->start.as<uint8_t>();
+    a.out = h->out.as<uint8_t>();
+    a.raw = slot;  // W = 1: the per-pixel in-place filter is race free
+    a.width = W;
+    a.height = H;
+    a.newest = h->uniform_idx;
+    a.window = 1;
+    a.chroma = h->p.chroma_filter;
+    a.filter = h->p.filter_type;
+    a.sensitivity = h->p.sensitivity;
+    a.colorize = h->p.colorize ? 1u : 0u;
+    uint8_t* pin_out = h->io_out.bytes();
+    for (uint32_t si = 0; si < n_s; ++si) {
+        a.y0 = si * rows;
+        a.y1 = std::min(H, a.y0 + rows);
+        const size_t o = (size_t)a.y0 * row, len = (size_t)(a.y1 - a.y0) * row;
+        DIPS_HIP(h, hipStreamWaitEvent(h->stream, h->up_pieces.ev[si], 0));
+        DIPS_HIP(h, dips::launch_compat_main(a, h->stream));
+        DIPS_HIP(h, hipMemcpyAsync(pin_out + o, h->out.as<uint8_t>() + o, len, hipMemcpyDeviceToHost, h->stream));
+        DIPS_HIP(h, hipEventRecord(h->pieces.ev[si], h->stream));
+    }
+    dips_host::CopyPool::global().run(n_s, [&](size_t si) {
+        const hipError_t e = hipEventSynchronize(h->pieces.ev[si]);
+        if (e != hipSuccess) {
+            err.store((int)e);
+            return;
+        }
+        const size_t o = si * rows * row;
+        std::memcpy(out + o, pin_out + o, std::min<size_t>((size_t)rows * row, fb - o));
+    });
+    DIPS_HIP(h, (hipError_t)err.load());
+    return 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -578,6 +653,14 @@ int dips_frame_callback(dips_handle* h, uint32_t width, uint32_t height, const u
                         uint8_t* out, size_t cap) {
     if (!h) return DIPS_ERR_INVALID;
     if (!out || cap < len) return fail(h, DIPS_ERR_CAPACITY, "frame_callback: output buffer too small");
+    const char* striped_env = std::getenv("DIPS_CALLBACK_STRIPED");  // "0": plain add_texture + dispatch
+    if ((!striped_env || striped_env[0] != '0') && h->main_init && h->p.spatial_window_size == 1 &&
+        !(h->p.flags & DIPS_FLAG_DEVICE_PTRS) && frame &&
+        width == h->width && height == h->height && len == (size_t)width * height * 4u) {
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        return frame_callback_striped(h, frame, out);
+    }
     dips_status st = dips_add_texture(h, width, height, frame, len);
     if (st != DIPS_OK) return st;
     const int r = dips_dispatch(h, out, cap);

@@ -73,6 +73,7 @@ struct CompatArgs {
     uint32_t filter;
     float sensitivity;
     uint32_t colorize;
+    uint32_t y0, y1;         // compat_main: rows [y0, y1) only (y1 = 0: all rows)
 };
 
 // dips ComputeState over a batch in steady state (compat_batch.hip).

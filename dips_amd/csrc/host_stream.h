@@ -31,14 +31,11 @@ inline void staged_copy(uint8_t* dst, const uint8_t* src, size_t bytes) { pool_c
 // frame (1 / 2 / 4 / 8 MiB: 463 / 497-549 / 548-554 / 478-502 frames/s of
 // frame_callback); DIPS_PIECE_BYTES overrides it.
 inline size_t piece_bytes() {
-    static const size_t v = []() -> size_t {
-        if (const char* e = std::getenv("DIPS_PIECE_BYTES")) {
-            const unsigned long long b = std::strtoull(e, nullptr, 10);
-            if (b >= 4096) return (size_t)b;
-        }
-        return (size_t)4u << 20;
-    }();
-    return v;
+    if (const char* e = std::getenv("DIPS_PIECE_BYTES")) {
+        const unsigned long long b = std::strtoull(e, nullptr, 10);
+        if (b >= 64) return (size_t)b;
+    }
+    return (size_t)4u << 20;
 }
 
 // One frame host -> device through the pinned buffer `pin` (>= bytes): the

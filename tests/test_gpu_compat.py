@@ -208,3 +208,30 @@ def test_frame_callback_batch_host_feed_chunks(monkeypatch, chunk_frames):
     finally:
         cs.close()
     assert np.array_equal(got, want), np.argwhere(got != want)[:4]
+
+
+@pytest.mark.parametrize("colorize,sens,filt,chroma", [(False, 5.0, 255, 0), (True, 5.0, 0, 0), (True, 0.7, 1, 2)])
+@pytest.mark.parametrize("piece", ["rows3", "odd", "whole"])
+def test_frame_callback_striped_matches_oracle(monkeypatch, colorize, sens, filt, chroma, piece):
+    """Steady-state frame_callback goes through the striped path (upload,
+    per-stripe kernel and readback overlapped); with stripes of a few rows, a
+    ragged last stripe or one stripe, every output and the ring state equal
+    the oracle's add_texture + dispatch."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
+    w, h = 40, 29
+    row = w * 4
+    monkeypatch.setenv("DIPS_PIECE_BYTES", str({"rows3": 3 * row, "odd": 7 * row + 5, "whole": 1 << 22}[piece]))
+    frames = _frames(w, h, 16, 90 + filt)
+    cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter(chroma))
+    ref = oracle.ComputeState(colorize, 1, sens, filt, chroma)
+    try:
+        for k in range(16):
+            got = frame_callback(w, h, frames[k], cs)
+            want = oracle.frame_callback(w, h, frames[k], ref)
+            assert np.array_equal(got, want), (k, np.argwhere(got != want)[:4])
+        # per-call add_texture / dispatch after striped calls see the same ring
+        cs.add_texture(w, h, frames[3])
+        ref.add_texture(w, h, frames[3])
+        assert np.array_equal(cs.dispatch(), ref.dispatch())
+    finally:
+        cs.close()

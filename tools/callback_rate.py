@@ -36,15 +36,26 @@ def main():
     lib, hd = cs._hd._lib, cs._hd
     for t in range(8):  # warm-up: the VecDeque phase and the start texture
         hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes, out.ctypes.data, out.nbytes))
-    t0 = time.perf_counter()
-    for t in range(8, F):
-        hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes, out.ctypes.data, out.nbytes))
-    dt = time.perf_counter() - t0
+    # steady state, the striped call (default) and the plain add_texture +
+    # dispatch sequence alternating in rounds (same process, same box)
+    times = {"striped": 0.0, "plain": 0.0}
+    counts = {"striped": 0, "plain": 0}
+    for rnd in range(4):
+        for mode in ("striped", "plain"):
+            os.environ["DIPS_CALLBACK_STRIPED"] = "1" if mode == "striped" else "0"
+            t0 = time.perf_counter()
+            for t in range(8, F):
+                hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
+                                                 out.ctypes.data, out.nbytes))
+            times[mode] += time.perf_counter() - t0
+            counts[mode] += F - 8
+    os.environ.pop("DIPS_CALLBACK_STRIPED", None)
     cs.close()
-    n = F - 8
-    print(json.dumps({"operator": "dips frame_callback (add_texture + dispatch), one frame per call",
-                      "frames": n, "frames_per_s": round(n / dt, 1), "ms_per_frame": round(dt / n * 1e3, 3),
-                      "pcie_GBps_each_way": round(n * W * H * 4 / dt / 1e9, 1)}), flush=True)
+    for mode in ("striped", "plain"):
+        n, dt = counts[mode], times[mode]
+        print(json.dumps({"operator": f"dips frame_callback, one frame per call ({mode})",
+                          "frames": n, "frames_per_s": round(n / dt, 1), "ms_per_frame": round(dt / n * 1e3, 3),
+                          "pcie_GBps_each_way": round(n * W * H * 4 / dt / 1e9, 1)}), flush=True)
 
     c = DiPsCompute(2, H, W)
     ha = c._host
