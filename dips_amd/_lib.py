@@ -144,6 +144,7 @@ def load() -> ctypes.CDLL:
             "dips_dispatch": ([_vp, _u8p, ctypes.c_size_t], st),
             "dips_frame_callback": ([_vp, u32, u32, _u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t], st),
             "dips_start_texture": ([_vp, _u8p, ctypes.c_size_t], st),
+            "dips_compat_resume": ([_vp, u32, u32, _u8p, _u8p, u64], st),
             "dips_frame_callback_batch": ([_vp, u32, u32, _u8p, u32, _u8p], st),
             "dips_diff_series": ([_vp, u32, u32, _u8p, u32, _u8p, _vp, _u8p], st),
             "dips_series_si": ([P(SeriesEntry)], ctypes.c_double),

@@ -227,6 +227,12 @@ class ComputeState:
         for t in (frames, out):
             if not t.is_cuda or not t.is_contiguous():
                 raise ValueError("device path needs contiguous HIP tensors")
+        dv = self._device_handle(frames, stream)
+        dv.check(dv._lib.dips_frame_callback_batch(dv.ptr, w, h, frames.data_ptr(), n, out.data_ptr()))
+
+    def _device_handle(self, tensor, stream=None) -> "_Handle":
+        """The device-pointer twin handle (own ComputeState), bound to
+        `stream` (default: the tensor's current stream)."""
         if self._dev is None:
             p = DipsParams()
             ctypes.memmove(ctypes.byref(p), ctypes.byref(self._hd.params), ctypes.sizeof(p))
@@ -234,10 +240,39 @@ class ComputeState:
             self._dev = _Handle(p, self._hd.device)
         if stream is None:
             import torch
-            stream = torch.cuda.current_stream(frames.device).cuda_stream
-        lib = self._dev._lib
-        self._dev.check(lib.dips_set_stream(self._dev.ptr, ctypes.c_void_p(int(stream))))
-        self._dev.check(lib.dips_frame_callback_batch(self._dev.ptr, w, h, frames.data_ptr(), n, out.data_ptr()))
+            stream = torch.cuda.current_stream(tensor.device).cuda_stream
+        self._dev.check(self._dev._lib.dips_set_stream(self._dev.ptr, ctypes.c_void_p(int(stream))))
+        return self._dev
+
+    # -- frame-range sharding (3-frame halo + start texture) --
+    def resume(self, width: int, height: int, start, halo, t0: int) -> None:
+        """Continue as if frame_callback had seen global frames 0..t0-1
+        (t0 >= 7, window 1): `start` is the start texture of the handle that
+        saw frames 0..3, `halo` the raw RGBA8 frames t0-3..t0-1 ([3, H, W, 4])."""
+        s, hl = _as_u8(start), _as_u8(halo)
+        if s.size != width * height * 4 or hl.size != 3 * width * height * 4:
+            raise ValueError("start must be [H, W, 4] and halo [3, H, W, 4] RGBA8")
+        self._hd.check(self._hd._lib.dips_compat_resume(self._hd.ptr, width, height, s.ctypes.data,
+                                                        hl.ctypes.data, int(t0)))
+        self._w, self._h = width, height
+
+    def resume_device(self, start, halo, t0: int, stream=None) -> None:
+        """Device form of resume (uint8 HIP tensors), for the device handle
+        that frame_callback_batch_device drives."""
+        h, w = int(start.shape[0]), int(start.shape[1])
+        if tuple(start.shape) != (h, w, 4) or tuple(halo.shape) != (3, h, w, 4):
+            raise ValueError("start must be [H, W, 4] and halo [3, H, W, 4] uint8 tensors")
+        for t in (start, halo):
+            if not t.is_cuda or not t.is_contiguous():
+                raise ValueError("device path needs contiguous HIP tensors")
+        dv = self._device_handle(start, stream)
+        dv.check(dv._lib.dips_compat_resume(dv.ptr, w, h, start.data_ptr(), halo.data_ptr(), int(t0)))
+
+    def start_texture_device(self, out, stream=None) -> bool:
+        """The device handle's start texture into a uint8 HIP tensor [H, W, 4]
+        (asynchronous); False while it is not built yet."""
+        dv = self._device_handle(out, stream)
+        return dv.check(dv._lib.dips_start_texture(dv.ptr, out.data_ptr(), out.numel())) == 1
 
     def kernel_time(self, reset: bool = False) -> Tuple[float, int]:
         """hipEvent time of the batch kernel on the device handle (time_kernel=True)."""

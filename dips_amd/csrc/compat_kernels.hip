@@ -130,6 +130,23 @@ __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
     *reinterpret_cast<uint32_t*>(a.out + 4 * p) = visual_epilogue(diff, a.filter, a.sensitivity, a.colorize != 0u);
 }
 
+// A ring slot as frame_callback leaves it for a W = 1 frame: the gray texel
+// q(get_intensity(frame)) (dips_shader.wgsl:123-126, 187) -- the state
+// compat_main writes in place, rebuilt from a raw frame for resume.
+__global__ __launch_bounds__(256) void compat_gray_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                         uint64_t n_px, uint32_t chroma) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= n_px) return;
+    const uint32_t q = unorm_store(texel_intensity(src, p, chroma));
+    *reinterpret_cast<uint32_t*>(dst + 4 * p) = q | (q << 8) | (q << 16) | (255u << 24);
+}
+
+hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, uint32_t chroma, hipStream_t s) {
+    if (n_px == 0) return hipSuccess;
+    hipLaunchKernelGGL(compat_gray_kernel, dim3((uint32_t)((n_px + 255) / 256)), dim3(256), 0, s, src, dst, n_px, chroma);
+    return hipGetLastError();
+}
+
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s) {
     dim3 grid((a.width + kTile - 1) / kTile, (a.height + kTile - 1) / kTile);
     hipLaunchKernelGGL(compat_precompute_kernel, grid, dim3(kTile, kTile), 0, s, a);

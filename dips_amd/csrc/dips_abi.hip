@@ -668,6 +668,48 @@ int dips_frame_callback(dips_handle* h, uint32_t width, uint32_t height, const u
     return r;
 }
 
+dips_status dips_compat_resume(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* start_rgba,
+                               const uint8_t* halo, uint64_t t0) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!start_rgba || !halo || width == 0 || height == 0)
+        return fail(h, DIPS_ERR_INVALID, "compat_resume: null or empty argument");
+    if (t0 < 7) return fail(h, DIPS_ERR_INVALID, "compat_resume: t0 must be >= 7 (steady state of the ring)");
+    if (h->p.spatial_window_size != 1)
+        return fail(h, DIPS_ERR_INVALID, "compat_resume: only spatial_window_size 1 (the batch path) resumes");
+    const size_t fb = (size_t)width * height * 4u;
+    const bool dev = (h->p.flags & DIPS_FLAG_DEVICE_PTRS) != 0;
+    for (auto& sl : h->slots) DIPS_HIP(h, sl.ensure(fb));
+    DIPS_HIP(h, h->raw.ensure(fb));
+    DIPS_HIP(h, h->start.ensure(fb));
+    DIPS_HIP(h, h->out.ensure(fb));
+    DIPS_HIP(h, h->io.ensure(fb));
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    DIPS_HIP(h, hipMemcpyAsync(h->start.p, start_rgba, fb, kind, h->stream));
+    // slot (t0-1-j) mod 4 <- gray texel of frame t0-1-j (halo[2-j]); the
+    // raw frame goes through h->raw when it comes from the host
+    for (int j = 0; j < 3; ++j) {
+        const uint8_t* src = halo + (size_t)(2 - j) * fb;
+        if (!dev) {
+            DIPS_HIP(h, hipMemcpyAsync(h->raw.p, src, fb, hipMemcpyHostToDevice, h->stream));
+            src = h->raw.as<uint8_t>();
+        }
+        DIPS_HIP(h, dips::launch_compat_gray(src, h->slots[(t0 - 1 - (uint64_t)j) % 4u].as<uint8_t>(),
+                                             (uint64_t)width * height, h->p.chroma_filter, h->stream));
+    }
+    DIPS_HIP(h, hipMemsetAsync(h->slots[t0 % 4u].p, 0, fb, h->stream));
+    if (!dev) DIPS_HIP(h, hipStreamSynchronize(h->stream));  // host buffers are borrowed for the call only
+    h->width = width;
+    h->height = height;
+    h->n_queued = 4;
+    h->main_init = true;
+    h->ring_idx = (uint32_t)(t0 % 4u);
+    h->uniform_idx = (uint32_t)((t0 - 1) % 4u);
+    h->added = t0;
+    return DIPS_OK;
+}
+
 dips_status dips_frame_callback_batch(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
                                       uint32_t n_frames, uint8_t* out) {
     dips_status st = bind(h);
@@ -697,6 +739,10 @@ int dips_start_texture(dips_handle* h, uint8_t* out, size_t cap) {
     if (!h->main_init) return 0;
     const size_t fb = (size_t)h->width * h->height * 4u;
     if (!out || cap < fb) return fail(h, DIPS_ERR_CAPACITY, "start_texture: output buffer too small");
+    if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) {  // device destination, asynchronous on the stream
+        DIPS_HIP(h, hipMemcpyAsync(out, h->start.p, fb, hipMemcpyDeviceToDevice, h->stream));
+        return 1;
+    }
     DIPS_HIP(h, hipMemcpyAsync(h->io.p, h->start.p, fb, hipMemcpyDeviceToHost, h->stream));
     DIPS_HIP(h, hipStreamSynchronize(h->stream));
     std::memcpy(out, h->io.p, fb);

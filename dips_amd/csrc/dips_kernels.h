@@ -162,5 +162,6 @@ hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s);
+hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, uint32_t chroma, hipStream_t s);
 
 }  // namespace dips

@@ -123,6 +123,67 @@ class SeriesGather:
         return torch.cat([buf[: e - s] for buf, (s, e) in zip(self.recv, self.ranges)], dim=0)
 
 
+# ---------------------------------------------------------------------------
+# dips-compat ComputeState over frame ranges ("dips-compat T=4
+# needs a 3-frame halo").  Output frame t depends on the start texture S
+# (built from frames 0..3) and, through the temporal ring, on frames
+# t-3..t; so rank k > 0 needs S (broadcast once from rank 0) and the raw
+# frames s_k-3..s_k-1 (the last three of rank k-1), and resumes there
+# (ComputeState.resume / dips_compat_resume).
+# ---------------------------------------------------------------------------
+COMPAT_HALO = 3
+
+
+def start_compat_halo(local_frames: torch.Tensor, halo: torch.Tensor, group=None) -> List:
+    """Post the send of this rank's last 3 frames to rank+1 and the receive
+    of rank-1's last 3 frames into `halo` ([3, H, W, 4]); returns the works."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return []
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    ops = []
+    if rank + 1 < world:
+        if local_frames.shape[0] < COMPAT_HALO:
+            raise ValueError("every shard of the dips-compat path needs >= 3 frames")
+        ops.append(dist.P2POp(dist.isend, local_frames[-COMPAT_HALO:].contiguous(), rank + 1, group))
+    if rank > 0:
+        ops.append(dist.P2POp(dist.irecv, halo, rank - 1, group))
+    return dist.batch_isend_irecv(ops) if ops else []
+
+
+def compat_sharded(local_frames: torch.Tensor, t0: int, *,
+                   callback_batch: Callable[[torch.Tensor], torch.Tensor],
+                   start_texture: Callable[[torch.Tensor], None],
+                   resume: Callable[[torch.Tensor, torch.Tensor, int], None],
+                   start_buf: torch.Tensor, halo_buf: torch.Tensor, group=None) -> torch.Tensor:
+    """frame_callback over this rank's frames (global t0 .. t0+n-1) with the
+    outputs a single ComputeState would give.  Rank 0 starts from frame 0,
+    builds S at its 4th frame and broadcasts it; every other rank resumes
+    from S and the halo (t0 >= 7 there).  callback_batch(frames) returns the
+    outputs of consecutive frame_callback calls; start_texture(buf) fills S;
+    resume(S, halo, t0) sets the state.  Returns this rank's outputs."""
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    works = start_compat_halo(local_frames, halo_buf, group)
+    if rank == 0:
+        if t0 != 0:
+            raise ValueError("rank 0 owns the first frames")
+        head = callback_batch(local_frames[:4])  # frames 0..3: passthrough, then S
+        start_texture(start_buf)
+    if world > 1:
+        dist.broadcast(start_buf, src=0, group=group)
+    if rank == 0:
+        tail = callback_batch(local_frames[4:]) if local_frames.shape[0] > 4 else head[:0]
+        for w in works:
+            w.wait()
+        return torch.cat([head, tail])
+    if t0 < 7:
+        raise ValueError("ranks after the first must start at global frame >= 7")
+    for w in works:
+        w.wait()
+    resume(start_buf, halo_buf, t0)
+    return callback_batch(local_frames)
+
+
 def sharded_series(local_frames: torch.Tensor, *, per_frame: bool, n_total: int,
                    compute: Callable[[torch.Tensor, Optional[torch.Tensor], torch.Tensor], None],
                    reference: Optional[torch.Tensor] = None, group=None,

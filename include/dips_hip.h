@@ -145,6 +145,18 @@ dips_status dips_frame_callback_batch(dips_handle *h, uint32_t width, uint32_t h
  * at the 4th frame.  Returns 1 if available, 0 if not yet built. */
 int dips_start_texture(dips_handle *h, uint8_t *out_rgba, size_t cap);
 
+/* Frame-range sharding of the dips-compat path ("dips-compat
+ * T=4 needs a 3-frame halo"): put the handle in the state ComputeState has
+ * after frame_callback of global frames 0..t0-1 (dips/src/lib.rs:233-246;
+ * ring and start texture of dips/src/gpu/mod.rs:170-216, bind_groups.rs:
+ * 407-427), rebuilt from the start texture S (dips_start_texture of the
+ * handle that saw frames 0..3) and the raw RGBA8 frames t0-3, t0-2, t0-1
+ * (`halo`, 3 contiguous frames in that order).  Requires t0 >= 7 and
+ * spatial_window_size 1.  Device pointers with DIPS_FLAG_DEVICE_PTRS
+ * (asynchronous), host pointers otherwise. */
+dips_status dips_compat_resume(dips_handle *h, uint32_t width, uint32_t height,
+                               const uint8_t *start_rgba, const uint8_t *halo, uint64_t t0);
+
 /* North-star batch path: the per-frame difference series of `n_frames`
  * contiguous frames (each width*height*C bytes, C from params.format).
  *   ref: overall mode -> the reference frame (NULL = frames[0]);

@@ -465,6 +465,48 @@ int dips_oracle_cs_add_texture(dips_oracle_cs *cs, uint32_t width, uint32_t heig
     return 0;
 }
 
+int dips_oracle_cs_resume(dips_oracle_cs *cs, uint32_t width, uint32_t height, const uint8_t *start_rgba,
+                          const uint8_t *halo, uint64_t t0) {
+    /* After frame_callback of frames 0..t0-1 (t0 >= 7): pre/main bind groups
+     * initialised, start texture S, ring index t0 mod 4, and slot (t0-1-j)
+     * mod 4 holding frame t0-1-j as its own dispatch left it -- the gray
+     * texel q(spatial_median_filter(frame)) (dips_shader.wgsl:187) -- for
+     * j = 0, 1, 2.  The fourth slot is overwritten by the next add_texture
+     * before anything reads it; the VecDeque is not read after init. */
+    if (!cs || !start_rgba || !halo || width == 0 || height == 0 || t0 < 7) return -1;
+    const size_t fb = (size_t)width * height * 4;
+    for (int i = 0; i < O_T; ++i) { free(cs->queue[i]); free(cs->slots[i]); cs->queue[i] = cs->slots[i] = NULL; }
+    free(cs->start);
+    free(cs->scratch);
+    cs->start = (uint8_t *)malloc(fb);
+    cs->scratch = (uint8_t *)malloc(fb);
+    if (!cs->start || !cs->scratch) return -2;
+    for (int i = 0; i < O_T; ++i) {
+        cs->queue[i] = (uint8_t *)calloc(1, fb);
+        cs->slots[i] = (uint8_t *)calloc(1, fb);
+        if (!cs->queue[i] || !cs->slots[i]) return -2;
+    }
+    cs->width = width;
+    cs->height = height;
+    cs->n_queued = O_T;
+    cs->pre_init = cs->main_init = 1;
+    memcpy(cs->start, start_rgba, fb);
+    for (int j = 0; j < 3; ++j) {
+        const uint8_t *raw = halo + (size_t)(2 - j) * fb; /* frame t0-1-j */
+        uint8_t *sl = cs->slots[(t0 - 1 - (uint64_t)j) % O_T];
+        for (uint32_t y = 0; y < height; ++y)
+            for (uint32_t x = 0; x < width; ++x) {
+                const size_t p = (size_t)y * width + x;
+                const uint8_t q = dips_oracle_q(o_spatial(raw, width, height, x, y, cs->window, (int)cs->chroma));
+                sl[p * 4 + 0] = sl[p * 4 + 1] = sl[p * 4 + 2] = q;
+                sl[p * 4 + 3] = 255;
+            }
+    }
+    cs->ring_idx = (uint32_t)(t0 % O_T);
+    cs->uniform_idx = (uint32_t)((t0 - 1) % O_T);
+    return 0;
+}
+
 static float o_sigmoid(float x, float k) {
     /* dips_shader.wgsl:108-112 */
     return 1.0f / (1.0f + dips_oracle_expf(-k * x)) - 0.5f;

@@ -69,6 +69,11 @@ int  dips_oracle_cs_add_texture(dips_oracle_cs *cs, uint32_t width,
                                 uint32_t height, const uint8_t *rgba);
 int  dips_oracle_cs_dispatch(dips_oracle_cs *cs, uint8_t *out_rgba);
 int  dips_oracle_cs_start_texture(const dips_oracle_cs *cs, uint8_t *out_rgba);
+/* State after frames 0..t0-1 went through frame_callback (t0 >= 7), rebuilt
+ * from the start texture and the raw frames t0-3, t0-2, t0-1 (`halo`, in
+ * that order): the frame-range sharding of the dips-compat path. */
+int  dips_oracle_cs_resume(dips_oracle_cs *cs, uint32_t width, uint32_t height,
+                           const uint8_t *start_rgba, const uint8_t *halo, uint64_t t0);
 void dips_oracle_cs_free(dips_oracle_cs *cs);
 
 /* dips_alt DiPsCompute emulation (dips_alt/src/dips_compute/mod.rs:243-647,

@@ -64,6 +64,9 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     lib.dips_oracle_cs_add_texture.argtypes = [ctypes.c_void_p, ctypes.c_uint32,
                                                ctypes.c_uint32, _u8p]
     lib.dips_oracle_cs_add_texture.restype = ctypes.c_int
+    lib.dips_oracle_cs_resume.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_uint64]
+    lib.dips_oracle_cs_resume.restype = ctypes.c_int
     lib.dips_oracle_cs_dispatch.argtypes = [ctypes.c_void_p, _u8p]
     lib.dips_oracle_cs_dispatch.restype = ctypes.c_int
     lib.dips_oracle_cs_start_texture.argtypes = [ctypes.c_void_p, _u8p]
@@ -161,6 +164,17 @@ class ComputeState:
         out = np.zeros((self._hgt, self._w, 4), dtype=np.uint8)
         rc = self._lib.dips_oracle_cs_start_texture(self._h, _p(out))
         return out if rc == 1 else None
+
+    def resume(self, width: int, height: int, start: np.ndarray, halo: np.ndarray, t0: int) -> None:
+        """State after frame_callback of frames 0..t0-1 (t0 >= 7) from the
+        start texture and the raw frames t0-3..t0-1 (halo [3, H, W, 4])."""
+        start = np.ascontiguousarray(start, dtype=np.uint8)
+        halo = np.ascontiguousarray(halo, dtype=np.uint8)
+        assert start.size == width * height * 4 and halo.size == 3 * width * height * 4
+        rc = self._lib.dips_oracle_cs_resume(self._h, width, height, _p(start), _p(halo), int(t0))
+        if rc != 0:
+            raise ValueError(f"resume rc={rc}")
+        self._w, self._hgt = width, height
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -90,3 +90,64 @@ def test_frame_ranges_cover_and_balance():
             assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
             sizes = [e - s for s, e in r]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _compat_worker(rank, world, port, n_total, params, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle
+        w, h = 20, 12
+        rng = np.random.default_rng(77)
+        allf = rng.integers(0, 256, (n_total, h, w, 4), dtype=np.uint8)
+        s, e = shard.frame_range(n_total, world, rank)
+        local = torch.from_numpy(allf[s:e].copy())
+        cs = oracle.ComputeState(*params)
+
+        def callback_batch(fr):
+            return torch.from_numpy(np.stack([oracle.frame_callback(w, h, f, cs) for f in fr.numpy()]))
+
+        def start_texture(buf):
+            buf.copy_(torch.from_numpy(cs.start_texture()))
+
+        def resume(start, halo, t0):
+            cs.resume(w, h, start.numpy(), halo.numpy(), t0)
+
+        out = shard.compat_sharded(local, s, callback_batch=callback_batch, start_texture=start_texture,
+                                   resume=resume, start_buf=torch.zeros((h, w, 4), dtype=torch.uint8),
+                                   halo_buf=torch.zeros((3, h, w, 4), dtype=torch.uint8))
+        # reassemble on rank 0 (padded gather; the product keeps outputs per rank)
+        m = max(b - a for a, b in shard.frame_ranges(n_total, world))
+        pad = torch.zeros((m, h, w, 4), dtype=torch.uint8)
+        pad[: out.shape[0]] = out
+        bufs = [torch.zeros_like(pad) for _ in range(world)] if rank == 0 else None
+        dist.gather(pad, bufs, dst=0)
+        if rank == 0:
+            full = torch.cat([b[: e2 - s2] for b, (s2, e2) in zip(bufs, shard.frame_ranges(n_total, world))])
+            result_q.put(full.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total,params", [(2, 24, (True, 1, 5.0, 0, 0)), (3, 40, (False, 1, 0.7, 255, 2)),
+                                                  (2, 31, (True, 3, 5.0, 1, 0))])
+def test_compat_sharded_equals_single(world, n_total, params):
+    """dips-compat frame_callback over frame ranges (start texture broadcast
+    + 3-frame halo + resume) gives the single ComputeState's outputs."""
+    from oracle import oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_compat_worker, args=(r, world, port, n_total, params, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    w, h = 20, 12
+    frames = np.random.default_rng(77).integers(0, 256, (n_total, h, w, 4), dtype=np.uint8)
+    cs = oracle.ComputeState(*params)
+    want = np.stack([oracle.frame_callback(w, h, f, cs) for f in frames])
+    assert np.array_equal(got, want)

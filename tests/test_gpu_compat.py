@@ -235,3 +235,60 @@ def test_frame_callback_striped_matches_oracle(monkeypatch, colorize, sens, filt
         assert np.array_equal(cs.dispatch(), ref.dispatch())
     finally:
         cs.close()
+
+
+@pytest.mark.parametrize("colorize,sens,filt,chroma", [(False, 5.0, 255, 0), (True, 5.0, 0, 1), (True, 0.7, 1, 3)])
+def test_resume_matches_continuous_run(colorize, sens, filt, chroma):
+    """dips_compat_resume (frame-range sharding): a ComputeState resumed at
+    global frame t0 from the start texture and the raw frames t0-3..t0-1
+    gives the outputs of one ComputeState that saw every frame -- host and
+    device pointers, batch and per-frame calls, several t0."""
+    import torch
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
+    w, h, n = 64, 36, 60
+    frames = _frames(w, h, n, 300 + filt)
+    params = (colorize, 1, sens, DiPsFilter(filt), ChromaFilter(chroma))
+    want = _oracle_callbacks(frames, (colorize, 1, sens, filt, chroma))
+    a = ComputeState(*params)
+    try:
+        assert np.array_equal(a.frame_callback_batch(w, h, frames), want)
+        start = a.start_texture()
+    finally:
+        a.close()
+    for t0 in (7, 8, 33):
+        b = ComputeState(*params)
+        try:
+            b.resume(w, h, start, frames[t0 - 3:t0], t0)
+            got = np.concatenate([b.frame_callback_batch(w, h, frames[t0:t0 + 20]),
+                                  np.stack([frame_callback(w, h, f, b) for f in frames[t0 + 20:]])])
+            assert np.array_equal(got, want[t0:]), (t0, np.argwhere(got != want[t0:])[:4])
+            # device twin
+            dev = torch.from_numpy(frames).cuda()
+            out = torch.empty_like(dev[t0:])
+            b.resume_device(torch.from_numpy(start).cuda(), dev[t0 - 3:t0].contiguous(), t0)
+            b.frame_callback_batch_device(dev[t0:].contiguous(), out)
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy(), want[t0:]), t0
+        finally:
+            b.close()
+
+
+def test_resume_rejects_bad_arguments():
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+    from dips_amd._lib import DipsError
+    w, h = 16, 8
+    f = _frames(w, h, 8, 1)
+    cs = ComputeState(False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
+    try:
+        with pytest.raises(DipsError):
+            cs.resume(w, h, f[0], f[:3], 6)  # t0 < 7: the ring is not in steady state
+        with pytest.raises(ValueError):
+            cs.resume(w, h, f[0], f[:2], 9)  # halo must be 3 frames
+    finally:
+        cs.close()
+    cs3 = ComputeState(False, 3, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
+    try:
+        with pytest.raises(DipsError):
+            cs3.resume(w, h, f[0], f[:3], 9)  # window 3: not on the batch path
+    finally:
+        cs3.close()
