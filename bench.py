@@ -90,11 +90,38 @@ def cpu_baseline(frames_dev, series_dev, mode: int, tau: float, target_s: float)
     # the same sample doubles as a parity check of the timed GPU series
     gpu = series_dev[:n].cpu().numpy().view(np.uint64)
     matches = bool(np.array_equal(gpu, out4))
+    # one core as well (1 thread and all cores), a shorter sample
+    n1 = min(n, 8)
+    t1 = time.perf_counter()
+    out1, _, _ = oracle.series(sample[:n1], mode=mode, tau=tau, nthreads=1, lib=lib)
+    dt1 = time.perf_counter() - t1
+    matches = matches and bool(np.array_equal(out1, out4[:n1]))
     return {"value": round(n_done / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
             "sample": f"first {n} frames of the same synthetic 4K RGB8 batch x {passes} passes, "
                       f"series only (oracle/dips_oracle.c, {build}, {threads} threads over frame "
                       f"ranges), {dt:.2f} s",
+            "single_core": {"value": round(n1 / dt1, 3), "unit": "frames/s", "cores": 1,
+                            "sample": f"first {n1} frames, one pass, {dt1:.2f} s"},
+            "host": _host_cpu(),
             "series_matches_gpu": matches}
+
+
+def _host_cpu() -> dict:
+    """CPU model and logical CPU count of the host the baseline ran on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
 
 
 def main():
