@@ -193,6 +193,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t
     kms, launches = op.kernel_time()
+    each = op.kernel_times()  # one launch per step at N = 1 (two at N > 1 per-frame)
     # series-kernel time per step (one launch per step, two when the halo
     # overlap splits a per-frame batch at N > 1)
     tt = torch.tensor([elapsed, kms / args.steps], dtype=torch.float64, device=dev)
@@ -266,6 +267,8 @@ def main():
                 "traffic": traffic,
                 "kernel": f"series_v2_kernel<3,0,4,{'true' if mode == Mode.PerFrame else 'false'},false>",
                 "kernel_ms": round(kernel_ms, 4),
+                "kernel_ms_median": round(float(np.median(each)), 4) if world == 1 and each else None,
+                "kernel_launches_timed": len(each),
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "partial_bytes_per_launch": int(pbytes) * F,
                 "waves": int(waves),

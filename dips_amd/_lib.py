@@ -152,6 +152,7 @@ def load() -> ctypes.CDLL:
             "dips_synth_frames": ([_vp, u32, u32, u64, u64, u32, _u8p], st),
             "dips_kernel_time": ([_vp, P(ctypes.c_double), P(u64)], st),
             "dips_kernel_time_reset": ([_vp], st),
+            "dips_kernel_time_each": ([_vp, P(ctypes.c_double), u64, P(u64)], st),
             "dips_series_geometry": ([_vp, u32, u32, u32, P(u64), P(u64), P(u64)], st),
             "dips_alt_params_default": ([P(DipsAltParams)], st),
             "dips_alt_create": ([P(DipsAltParams), u32, u32, st, P(_vp)], st),

@@ -14,7 +14,7 @@ from __future__ import annotations
 import ctypes
 import enum
 from dataclasses import dataclass
-from typing import Callable, Iterable, Iterator, Optional, Tuple
+from typing import Callable, Iterable, Iterator, List, Optional, Tuple
 
 import numpy as np
 
@@ -464,6 +464,15 @@ class DiffSeriesOperator:
         self._dev.check(lib.dips_set_stream(self._dev.ptr, ctypes.c_void_p(int(stream))))
         self._dev.check(lib.dips_synth_frames(self._dev.ptr, width, height, int(seed), int(t0), n,
                                               dst.data_ptr()))
+
+    def kernel_times(self) -> List[float]:
+        """Per-launch hipEvent times (ms) of the series kernel since the last reset."""
+        lib, ptr = self._dev._lib, self._dev.ptr
+        n = ctypes.c_uint64()
+        self._dev.check(lib.dips_kernel_time_each(ptr, None, 0, ctypes.byref(n)))
+        buf = (ctypes.c_double * max(1, n.value))()
+        self._dev.check(lib.dips_kernel_time_each(ptr, buf, n.value, ctypes.byref(n)))
+        return list(buf[: n.value])
 
     def kernel_time(self, reset: bool = False) -> Tuple[float, int]:
         ms = ctypes.c_double()

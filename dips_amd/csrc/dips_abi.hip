@@ -63,6 +63,7 @@ struct dips_handle {
     std::vector<hipEvent_t> ev_free;
     double t_ms = 0.0;
     uint64_t t_launches = 0;
+    std::vector<double> t_each;  // per-launch times since the last reset
 
     // dips-compat ComputeState
     uint32_t width = 0, height = 0;
@@ -886,6 +887,7 @@ dips_status dips_kernel_time(dips_handle* h, double* total_ms, uint64_t* launche
         DIPS_HIP(h, hipEventElapsedTime(&ms, pr.first, pr.second));
         h->t_ms += ms;
         h->t_launches += 1;
+        h->t_each.push_back(ms);
         h->ev_free.push_back(pr.first);
         h->ev_free.push_back(pr.second);
     }
@@ -900,6 +902,17 @@ dips_status dips_kernel_time_reset(dips_handle* h) {
     if (st != DIPS_OK) return st;
     h->t_ms = 0.0;
     h->t_launches = 0;
+    h->t_each.clear();
+    return DIPS_OK;
+}
+
+dips_status dips_kernel_time_each(dips_handle* h, double* ms_each, uint64_t cap, uint64_t* launches) {
+    dips_status st = dips_kernel_time(h, nullptr, nullptr);
+    if (st != DIPS_OK) return st;
+    const uint64_t n = h->t_each.size();
+    if (ms_each)
+        for (uint64_t i = 0; i < n && i < cap; ++i) ms_each[i] = h->t_each[i];
+    if (launches) *launches = n;
     return DIPS_OK;
 }
 
