@@ -7,7 +7,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -50,6 +52,8 @@ struct dips_alt_handle {
     DevBuf out1, meta;
     dips_host::StreamPipe pipe;  // host-pointer feed of dips_alt_send_frames
     dips_host::PieceEvents pieces;  // per-piece completion of send_frame's readback
+    dips_host::PieceEvents up_pieces;  // per-stripe upload completion of send_frame
+    HostPinned io_out;                 // send_frame readback staging (striped)
     HostPinned io;
     HostPinned meta_pin[2];  // per-batch flags + chunk table, pinned so the upload stays asynchronous
     hipEvent_t meta_done[2] = {nullptr, nullptr};
@@ -387,6 +391,8 @@ void dips_alt_destroy(dips_alt_handle* h) {
     h->out1.release();
     h->pipe.release();
     h->pieces.release();
+    h->up_pieces.release();
+    h->io_out.release();
     h->meta.release();
     h->io.release();
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -426,7 +432,9 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     // (through the pinned buffer in pieces: host copy and DMA overlapped)
     const uint32_t N = h->p.num_textures;
     uint8_t* slot = h->slots[h->sent % N].as<uint8_t>();
-    ALT_HIP(h, dips_host::upload_via(slot, frame, fb, h->io.bytes(), h->stream));
+    const char* striped_env = std::getenv("DIPS_CALLBACK_STRIPED");  // "0": whole-frame transfers
+    const bool striped = h->p.window_size == 1 && (!striped_env || striped_env[0] != '0');
+    if (!striped) ALT_HIP(h, dips_host::upload_via(slot, frame, fb, h->io.bytes(), h->stream));
     h->sent += 1;
     dips::AltArgs a{};
     for (uint32_t k = 0; k < N; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
@@ -441,9 +449,51 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     a.scalar = h->p.sigmoid_horizontal_scalar;
     a.colorize = h->p.colorize ? 1u : 0u;
     a.snapshot = snapshot ? 1u : 0u;
-    ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
-    // copy_texture_to_buffer + map_async + de-pad (mod.rs:597-643)
-    ALT_HIP(h, dips_host::download_via(out, h->out1.p, fb, h->io.bytes(), h->stream, h->pieces));
+    if (!striped) {
+        ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
+        // copy_texture_to_buffer + map_async + de-pad (mod.rs:597-643)
+        ALT_HIP(h, dips_host::download_via(out, h->out1.p, fb, h->io.bytes(), h->stream, h->pieces));
+        return DIPS_OK;
+    }
+    // W = 1 (per pixel): ~4 MiB row stripes -- stripe s goes up on the
+    // upload stream, is processed as soon as it has landed and comes back on
+    // the compute stream while stripes s+1.. still go up
+    const size_t row = (size_t)h->width * 4u;
+    const uint32_t rows = (uint32_t)std::max<size_t>(1, dips_host::piece_bytes() / row);
+    const uint32_t n_s = (h->height + rows - 1) / rows;
+    ALT_HIP(h, h->io_out.ensure(fb));
+    ALT_HIP(h, h->up_pieces.ensure(n_s));
+    ALT_HIP(h, h->pieces.ensure(n_s));
+    uint8_t* pin_in = h->io.bytes();
+    uint8_t* pin_out = h->io_out.bytes();
+    std::atomic<int> err{(int)hipSuccess};
+    dips_host::CopyPool::global().run(n_s, [&](size_t si) {
+        const size_t o = si * rows * row, len = std::min<size_t>((size_t)rows * row, fb - o);
+        std::memcpy(pin_in + o, frame + o, len);
+        hipError_t e = hipMemcpyAsync(slot + o, pin_in + o, len, hipMemcpyHostToDevice, h->meta_stream);
+        if (e == hipSuccess) e = hipEventRecord(h->up_pieces.ev[si], h->meta_stream);
+        if (e != hipSuccess) err.store((int)e);
+    });
+    ALT_HIP(h, (hipError_t)err.load());
+    for (uint32_t si = 0; si < n_s; ++si) {
+        a.y0 = si * rows;
+        a.y1 = std::min(h->height, a.y0 + rows);
+        const size_t o = (size_t)a.y0 * row, len = (size_t)(a.y1 - a.y0) * row;
+        ALT_HIP(h, hipStreamWaitEvent(h->stream, h->up_pieces.ev[si], 0));
+        ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
+        ALT_HIP(h, hipMemcpyAsync(pin_out + o, h->out1.as<uint8_t>() + o, len, hipMemcpyDeviceToHost, h->stream));
+        ALT_HIP(h, hipEventRecord(h->pieces.ev[si], h->stream));
+    }
+    dips_host::CopyPool::global().run(n_s, [&](size_t si) {
+        const hipError_t e = hipEventSynchronize(h->pieces.ev[si]);
+        if (e != hipSuccess) {
+            err.store((int)e);
+            return;
+        }
+        const size_t o = si * rows * row;
+        std::memcpy(out + o, pin_out + o, std::min<size_t>((size_t)rows * row, fb - o));
+    });
+    ALT_HIP(h, (hipError_t)err.load());
     return DIPS_OK;
 }
 

@@ -40,9 +40,9 @@ __device__ __forceinline__ float alt_texel_intensity(const uint8_t* img, uint64_
 // Intensities of this workgroup's tile plus a halo of `halo` texels; texels
 // outside the frame are 0.0 (pre_compute_shader.wgsl:148-150).
 __device__ void alt_stage_tile(float (*tile)[kLds], const uint8_t* img, uint32_t w, uint32_t h, int halo,
-                               uint32_t chroma) {
+                               uint32_t chroma, uint32_t y0) {
     const int ox = (int)(blockIdx.x * kTile) - halo;
-    const int oy = (int)(blockIdx.y * kTile) - halo;
+    const int oy = (int)(y0 + blockIdx.y * kTile) - halo;
     const int span = kTile + 2 * halo;
     for (int idx = threadIdx.y * kTile + threadIdx.x; idx < span * span; idx += kTile * kTile) {
         const int ty = idx / span, tx = idx - ty * span;
@@ -107,8 +107,8 @@ template <int N>
 __global__ __launch_bounds__(256) void alt_frame_kernel(AltArgs a) {
     __shared__ float tile[kLds][kLds];
     const uint32_t x = blockIdx.x * kTile + threadIdx.x;
-    const uint32_t y = blockIdx.y * kTile + threadIdx.y;
-    const bool inside = x < a.width && y < a.height;
+    const uint32_t y = a.y0 + blockIdx.y * kTile + threadIdx.y;
+    const bool inside = x < a.width && y < (a.y1 ? a.y1 : a.height);
     const uint64_t p = (uint64_t)y * a.width + x;
     float v[N];
 #pragma unroll
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void alt_frame_kernel(AltArgs a) {
             v[k] = inside ? alt_texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
         } else {
             __syncthreads();
-            alt_stage_tile(tile, a.slots[k], a.width, a.height, a.window / 2, a.chroma);
+            alt_stage_tile(tile, a.slots[k], a.width, a.height, a.window / 2, a.chroma, a.y0);
             __syncthreads();
             v[k] = inside ? alt_window_select(tile, a.window) : 0.0f;
         }
@@ -296,7 +296,9 @@ __global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
 
 template <int N>
 hipError_t launch_frame_n(const AltArgs& a, hipStream_t s) {
-    dim3 grid((a.width + kTile - 1) / kTile, (a.height + kTile - 1) / kTile);
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
+    dim3 grid((a.width + kTile - 1) / kTile, (yend - a.y0 + kTile - 1) / kTile);
     hipLaunchKernelGGL(alt_frame_kernel<N>, grid, dim3(kTile, kTile), 0, s, a);
     return hipGetLastError();
 }

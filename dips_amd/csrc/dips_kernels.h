@@ -109,6 +109,7 @@ struct AltArgs {                     // one send_frame dispatch
     float scalar;
     uint32_t colorize;
     uint32_t snapshot;
+    uint32_t y0, y1;                 // rows [y0, y1) only (y1 = 0: all rows)
 };
 
 struct AltBatchArgs {                // a run of frames, N = 2, W = 1
