@@ -194,6 +194,9 @@ def main():
     elapsed = time.perf_counter() - t
     kms, launches = op.kernel_time()
     each = op.kernel_times()  # one launch per step at N = 1 (two at N > 1 per-frame)
+    # measured read-only ceiling on this GPU, outside the timed region: one
+    # plain stream over the same resident bytes (median of 3)
+    read_ms = float(np.median([op.read_ceiling_ms(frames) for _ in range(3)]))
     # series-kernel time per step (one launch per step, two when the halo
     # overlap splits a per-frame batch at N > 1)
     tt = torch.tensor([elapsed, kms / args.steps], dtype=torch.float64, device=dev)
@@ -269,6 +272,13 @@ def main():
                 "kernel_ms": round(kernel_ms, 4),
                 "kernel_ms_median": round(float(np.median(each)), 4) if world == 1 and each else None,
                 "kernel_launches_timed": len(each),
+                "read_ceiling": {
+                    "achieved": round(F * fb / (read_ms / 1e3) / 1e9, 1),
+                    "unit": "GB/s",
+                    "frac": round(achieved / (F * fb / (read_ms / 1e3) / 1e9), 4),
+                    "kernel": "read_ceiling_kernel: non-temporal 16-B loads, 4 in flight per lane, grid-stride, "
+                              "over the same frames (no compute)",
+                },
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "partial_bytes_per_launch": int(pbytes) * F,
                 "waves": int(waves),

@@ -465,6 +465,14 @@ class DiffSeriesOperator:
         self._dev.check(lib.dips_synth_frames(self._dev.ptr, width, height, int(seed), int(t0), n,
                                               dst.data_ptr()))
 
+    def read_ceiling_ms(self, tensor) -> float:
+        """hipEvent time of one read-only stream over a device tensor's bytes."""
+        ms = ctypes.c_double()
+        self._dev.check(self._dev._lib.dips_read_ceiling(self._dev.ptr, tensor.data_ptr(),
+                                                         tensor.numel() * tensor.element_size(),
+                                                         ctypes.byref(ms)))
+        return ms.value
+
     def kernel_times(self) -> List[float]:
         """Per-launch hipEvent times (ms) of the series kernel since the last reset."""
         lib, ptr = self._dev._lib, self._dev.ptr

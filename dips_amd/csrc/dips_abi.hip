@@ -49,6 +49,7 @@ struct dips_handle {
 
     // batch series workspace
     DevBuf partials, stage_frames, stage_ref, stage_series, stage_map;
+    DevBuf probe_out;  // sink of the read-ceiling kernel
     std::map<const void*, int> occupancy;
 
     // streamed feed
@@ -337,6 +338,7 @@ void dips_destroy(dips_handle* h) {
     h->pipe.release();
     h->pieces.release();
     h->up_pieces.release();
+    h->probe_out.release();
     h->io_out.release();
     h->raw.release();
     h->start.release();
@@ -913,6 +915,25 @@ dips_status dips_kernel_time_each(dips_handle* h, double* ms_each, uint64_t cap,
     if (ms_each)
         for (uint64_t i = 0; i < n && i < cap; ++i) ms_each[i] = h->t_each[i];
     if (launches) *launches = n;
+    return DIPS_OK;
+}
+
+dips_status dips_read_ceiling(dips_handle* h, const uint8_t* dev_bytes, uint64_t bytes, double* ms) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!dev_bytes || !ms) return fail(h, DIPS_ERR_INVALID, "read_ceiling: null argument");
+    DIPS_HIP(h, h->probe_out.ensure(256));
+    hipEvent_t e0 = take_event(h), e1 = take_event(h);
+    if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
+    DIPS_HIP(h, hipEventRecord(e0, h->stream));
+    DIPS_HIP(h, dips::launch_read_ceiling(dev_bytes, bytes, h->probe_out.as<uint32_t>(), h->stream));
+    DIPS_HIP(h, hipEventRecord(e1, h->stream));
+    DIPS_HIP(h, hipEventSynchronize(e1));
+    float t = 0.0f;
+    DIPS_HIP(h, hipEventElapsedTime(&t, e0, e1));
+    *ms = t;
+    h->ev_free.push_back(e0);
+    h->ev_free.push_back(e1);
     return DIPS_OK;
 }
 

@@ -161,6 +161,7 @@ hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uin
                                 dips_series_entry* series, hipStream_t s);
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
+hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, hipStream_t s);
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, uint32_t chroma, hipStream_t s);

@@ -334,6 +334,36 @@ __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __re
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].si_fixed), (unsigned long long)sif);
 }
 
+// Read-only stream of `n16` 16-byte words (non-temporal loads, 4 in flight
+// per lane, grid-stride): the measured read ceiling the series kernel is
+// compared with ("% of a measured read-only-stream ceiling").
+// The XOR keeps the loads alive; `out` is written only on a magic value.
+__global__ __launch_bounds__(256) void read_ceiling_kernel(const u32x4* __restrict__ p, uint64_t n16,
+                                                           uint32_t* __restrict__ out) {
+    constexpr int kUnr = 4;
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256u * kUnr;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u * kUnr + threadIdx.x; i < n16; i += stride) {
+        u32x4 v[kUnr];
+#pragma unroll
+        for (int u = 0; u < kUnr; ++u) {
+            const uint64_t j = i + (uint64_t)u * 256u;
+            v[u] = j < n16 ? __builtin_nontemporal_load(p + j) : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < kUnr; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, hipStream_t s) {
+    if (((uintptr_t)p & 15u) != 0) return hipErrorInvalidValue;
+    const uint64_t n16 = bytes / 16u;
+    if (n16 == 0) return hipSuccess;
+    hipLaunchKernelGGL(read_ceiling_kernel, dim3(1024), dim3(256), 0, s, reinterpret_cast<const u32x4*>(p), n16, out);
+    return hipGetLastError();
+}
+
 // Generic path: any frame shape and alignment.  One thread per pixel, the
 // intensity computed in the reference's own form ((cmax+cmin)/2.0,
 // dips_shader.wgsl:73-81) rather than the fast kernel's I2 pairs, so the two

@@ -204,6 +204,12 @@ dips_status dips_series_geometry(dips_handle *h, uint32_t width, uint32_t height
                                  uint32_t n_frames, uint64_t *waves, uint64_t *tiles,
                                  uint64_t *partial_bytes);
 
+/* Measured read ceiling: one read-only stream (non-temporal 16-byte loads,
+ * grid-stride) over `bytes` of DEVICE memory, synchronous; *ms = its
+ * hipEvent duration.  bench.py divides the series kernel's rate by it
+ * ("% of a measured read-only-stream ceiling"). */
+dips_status dips_read_ceiling(dips_handle *h, const uint8_t *dev_bytes, uint64_t bytes, double *ms);
+
 /* Library ABI version (DIPS_ABI_VERSION). */
 int dips_abi_version(void);
 
