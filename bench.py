@@ -235,6 +235,27 @@ def main():
             except Exception:
                 traffic = None
         value = world * F * args.steps / elapsed_max
+        # PCIe-inclusive rate, reported beside (never as) `value` (BASELINE.md:
+        # "the H2D end-to-end rate separately"): the first 96 frames copied to
+        # pageable host memory and fed back through dips_diff_series_streamed
+        pcie = None
+        try:
+            if world > 1:
+                raise RuntimeError("measured at N = 1 only")
+            nh = min(F, 96)
+            host = frames[:nh].cpu().numpy()
+            op.streamed(host[:16], chunk_frames=8)  # warm (pinned / ring allocations)
+            t_h = time.perf_counter()
+            sh = op.streamed(host, chunk_frames=8)
+            dt_h = time.perf_counter() - t_h
+            want = series[:nh].cpu().numpy().view(np.uint64)
+            pcie = {"frames_per_s": round(nh / dt_h, 1), "host_to_device_GBps": round(nh * fb / dt_h / 1e9, 2),
+                    "frames": nh, "path": "pageable host frames -> pooled pinned staging -> H2D on a side "
+                                          "stream, series kernel on the previous chunk (dips_diff_series_streamed)",
+                    "series_matches_resident_run": bool(np.array_equal(sh.as_array(), want))}
+            del host
+        except Exception as e:  # report, never hide
+            pcie = {"skipped": str(e)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
@@ -285,6 +306,7 @@ def main():
                 **({"traffic_source": pmc_note} if pmc_note else {}),
             },
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
         }
         print(json.dumps(out), flush=True)
     op.close()
