@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--mode", choices=["per-frame", "overall"], default="per-frame")
     ap.add_argument("--tau", type=float, default=8.0 / 255.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="skip the pcie_inclusive sample (profiling runs: its chunk launches of the series "
+                         "kernel would mix into the kernel statistics)")
     ap.add_argument("--check", action="store_true",
                     help="rank 0 recomputes the series of all N*F frames in one single-device launch "
                          "and requires the gathered series to equal it (functional check of the N>1 path)")
@@ -242,6 +245,8 @@ def main():
         try:
             if world > 1:
                 raise RuntimeError("measured at N = 1 only")
+            if args.no_pcie:
+                raise RuntimeError("--no-pcie")
             nh = min(F, 96)
             host = frames[:nh].cpu().numpy()
             op.streamed(host[:16], chunk_frames=8)  # warm (pinned / ring allocations)

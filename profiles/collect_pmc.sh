@@ -12,7 +12,7 @@ OUT=gpurun_out/pmc_bench
 mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o run -- \
-    python3 bench.py --frames-per-gpu $F --steps 2 --warmup 1 --mode $MODE --no-cpu-baseline \
+    python3 bench.py --frames-per-gpu $F --steps 2 --warmup 1 --mode $MODE --no-cpu-baseline --no-pcie \
     > $OUT/$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
