@@ -1,0 +1,221 @@
+// dips_raw.cpp -- native host program over the C ABI (include/dips_hip.h),
+// the stand-in for the Rust host side (cargo is absent in this image).
+//
+// It mirrors dips' perform_dips loop (dips/src/frame_extractor.rs:206-276:
+// appsink delivers RGBA8 frames, frame_callback (dips/src/lib.rs:233-246)
+// turns each into the output frame, the muxer writes it) with the GStreamer
+// decode / encode replaced by raw files, and exposes the north-star series:
+//
+//   dips_raw callback IN.rgba W H OUT.rgba [--colorize] [--window N]
+//            [--sensitivity K] [--filter sigmoid|inverse|none]
+//            [--chroma none|red|green|blue] [--batch N]
+//   dips_raw series IN.raw W H rgb8|rgba8|gray8 [--mode overall|per-frame]
+//            [--tau T] [--chunk N]        -> CSV frame,sad,sj,count,si
+//
+// Input files are memory-mapped and handed over as host pointers: the
+// library stages them through pinned memory and overlaps the PCIe transfers
+// with the kernels.  Exit status 0 on success, 1 on a usage error, 2 on a
+// library error (message from dips_last_error on stderr).
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/dips_hip.h"
+
+namespace {
+
+struct Mapped {
+    const uint8_t* p = nullptr;
+    size_t n = 0;
+    bool open(const char* path) {
+        const int fd = ::open(path, O_RDONLY);
+        if (fd < 0) return false;
+        struct stat st {};
+        if (fstat(fd, &st) != 0 || st.st_size <= 0) {
+            ::close(fd);
+            return false;
+        }
+        n = (size_t)st.st_size;
+        void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+        ::close(fd);
+        if (m == MAP_FAILED) return false;
+        p = static_cast<const uint8_t*>(m);
+        return true;
+    }
+    ~Mapped() {
+        if (p) munmap(const_cast<uint8_t*>(p), n);
+    }
+};
+
+int usage() {
+    std::fprintf(stderr,
+                 "usage: dips_raw callback IN.rgba W H OUT.rgba [--colorize] [--window N] [--sensitivity K]\n"
+                 "                [--filter sigmoid|inverse|none] [--chroma none|red|green|blue] [--batch N]\n"
+                 "       dips_raw series IN.raw W H rgb8|rgba8|gray8 [--mode overall|per-frame] [--tau T]\n"
+                 "                [--chunk N]\n");
+    return 1;
+}
+
+int lib_error(dips_handle* h, const char* what, int st) {
+    std::fprintf(stderr, "dips_raw: %s failed (%d): %s\n", what, st, dips_last_error(h));
+    return 2;
+}
+
+bool parse_u32(const char* s, uint32_t* v) {
+    char* end = nullptr;
+    const unsigned long x = std::strtoul(s, &end, 10);
+    if (!s[0] || *end || x == 0 || x > 0xFFFFFFFFul) return false;
+    *v = (uint32_t)x;
+    return true;
+}
+
+int run_callback(int argc, char** argv) {
+    if (argc < 6) return usage();
+    uint32_t w = 0, h = 0, batch = 1;
+    if (!parse_u32(argv[3], &w) || !parse_u32(argv[4], &h)) return usage();
+    dips_params p;
+    dips_params_default(&p);  // DiPsProperties defaults (dips/src/lib.rs:71-90)
+    for (int i = 6; i < argc; ++i) {
+        const std::string a = argv[i];
+        const bool has = i + 1 < argc;
+        if (a == "--colorize") {
+            p.colorize = 1;
+        } else if (a == "--window" && has) {
+            p.spatial_window_size = std::atoi(argv[++i]);
+        } else if (a == "--sensitivity" && has) {
+            p.sensitivity = std::strtof(argv[++i], nullptr);
+        } else if (a == "--filter" && has) {
+            const std::string f = argv[++i];
+            p.filter_type = f == "sigmoid" ? DIPS_FILTER_SIGMOID
+                            : f == "inverse" ? DIPS_FILTER_INVERSE_SIGMOID
+                                             : DIPS_FILTER_UNFILTERED;
+        } else if (a == "--chroma" && has) {
+            const std::string c = argv[++i];
+            p.chroma_filter = c == "red" ? DIPS_CHROMA_RED
+                              : c == "green" ? DIPS_CHROMA_GREEN
+                              : c == "blue" ? DIPS_CHROMA_BLUE
+                                            : DIPS_CHROMA_NONE;
+        } else if (a == "--batch" && has) {
+            if (!parse_u32(argv[++i], &batch)) return usage();
+        } else {
+            return usage();
+        }
+    }
+    Mapped in;
+    if (!in.open(argv[2])) {
+        std::fprintf(stderr, "dips_raw: cannot map %s\n", argv[2]);
+        return 1;
+    }
+    const size_t fb = (size_t)w * h * 4u;
+    if (in.n % fb != 0) {
+        std::fprintf(stderr, "dips_raw: %s is not a whole number of %ux%u RGBA8 frames\n", argv[2], w, h);
+        return 1;
+    }
+    const uint64_t n = in.n / fb;
+    FILE* out = std::fopen(argv[5], "wb");
+    if (!out) {
+        std::fprintf(stderr, "dips_raw: cannot create %s\n", argv[5]);
+        return 1;
+    }
+    dips_handle* hd = nullptr;
+    int st = dips_create(&p, 0, &hd);
+    if (st != DIPS_OK) {
+        std::fclose(out);
+        return lib_error(nullptr, "dips_create", st);
+    }
+    std::vector<uint8_t> buf(fb * batch);
+    int rc = 0;
+    for (uint64_t t = 0; t < n && rc == 0;) {
+        const uint32_t m = (uint32_t)std::min<uint64_t>(batch, n - t);
+        const uint8_t* src = in.p + t * fb;
+        if (batch == 1) {
+            // frame_callback: frames 0..2 come back unchanged (lib.rs:241-245)
+            st = dips_frame_callback(hd, w, h, src, fb, buf.data(), buf.size());
+            if (st < 0) rc = lib_error(hd, "dips_frame_callback", st);
+        } else {
+            st = dips_frame_callback_batch(hd, w, h, src, m, buf.data());
+            if (st != DIPS_OK) rc = lib_error(hd, "dips_frame_callback_batch", st);
+        }
+        if (rc == 0 && std::fwrite(buf.data(), fb, m, out) != m) {
+            std::fprintf(stderr, "dips_raw: short write\n");
+            rc = 1;
+        }
+        t += m;
+    }
+    dips_destroy(hd);
+    if (std::fclose(out) != 0 && rc == 0) rc = 1;
+    return rc;
+}
+
+int run_series(int argc, char** argv) {
+    if (argc < 6) return usage();
+    uint32_t w = 0, h = 0, chunk = 0;
+    if (!parse_u32(argv[3], &w) || !parse_u32(argv[4], &h)) return usage();
+    dips_params p;
+    dips_params_default(&p);
+    const std::string fmt = argv[5];
+    p.format = fmt == "rgb8" ? DIPS_FMT_RGB8 : fmt == "rgba8" ? DIPS_FMT_RGBA8 : fmt == "gray8" ? DIPS_FMT_GRAY8 : 0u;
+    if (!p.format) return usage();
+    for (int i = 6; i < argc; ++i) {
+        const std::string a = argv[i];
+        const bool has = i + 1 < argc;
+        if (a == "--mode" && has) {
+            const std::string m = argv[++i];
+            if (m != "overall" && m != "per-frame") return usage();
+            p.mode = m == "overall" ? DIPS_MODE_OVERALL : DIPS_MODE_PER_FRAME;
+        } else if (a == "--tau" && has) {
+            p.tau = std::strtof(argv[++i], nullptr);
+        } else if (a == "--chunk" && has) {
+            if (!parse_u32(argv[++i], &chunk)) return usage();
+        } else {
+            return usage();
+        }
+    }
+    Mapped in;
+    if (!in.open(argv[2])) {
+        std::fprintf(stderr, "dips_raw: cannot map %s\n", argv[2]);
+        return 1;
+    }
+    const size_t fb = (size_t)w * h * p.format;
+    if (in.n % fb != 0 || in.n / fb > 0xFFFFFFFFull) {
+        std::fprintf(stderr, "dips_raw: %s is not a whole number of %ux%u %s frames\n", argv[2], w, h, fmt.c_str());
+        return 1;
+    }
+    const uint32_t n = (uint32_t)(in.n / fb);
+    dips_handle* hd = nullptr;
+    int st = dips_create(&p, 0, &hd);
+    if (st != DIPS_OK) return lib_error(nullptr, "dips_create", st);
+    std::vector<dips_series_entry> series(n);
+    st = dips_diff_series_streamed(hd, w, h, in.p, n, nullptr, series.data(), chunk);
+    if (st != DIPS_OK) {
+        const int rc = lib_error(hd, "dips_diff_series_streamed", st);
+        dips_destroy(hd);
+        return rc;
+    }
+    std::printf("frame,sad,sj,count,si\n");
+    for (uint32_t t = 0; t < n; ++t)
+        std::printf("%u,%llu,%llu,%llu,%.17g\n", t, (unsigned long long)series[t].sad,
+                    (unsigned long long)series[t].sj, (unsigned long long)series[t].count,
+                    dips_series_si(&series[t]));
+    dips_destroy(hd);
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) return usage();
+    const std::string cmd = argv[1];
+    if (cmd == "callback") return run_callback(argc, argv);
+    if (cmd == "series") return run_series(argc, argv);
+    return usage();
+}

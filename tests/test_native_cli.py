@@ -1,0 +1,76 @@
+"""The native host program over the C ABI (dips_amd/bin/dips_raw, built by
+__graft_entry__.build()): the perform_dips loop on raw RGBA8 files and the
+difference series CSV, against the oracle (GPU tests) and its usage / error
+behaviour (CPU tests)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "dips_amd", "bin", "dips_raw")
+
+
+def _run(args, **kw):
+    return subprocess.run([BIN] + [str(a) for a in args], capture_output=True, text=True, timeout=120, **kw)
+
+
+def test_binary_built_and_usage():
+    assert os.access(BIN, os.X_OK), "build() makes dips_amd/bin/dips_raw"
+    r = _run([])
+    assert r.returncode == 1 and "usage" in r.stderr
+    r = _run(["series", "x", "0", "4", "rgb8"])
+    assert r.returncode == 1  # zero width is a usage error
+
+
+def test_missing_input_is_an_error(tmp_path):
+    r = _run(["callback", tmp_path / "none.rgba", 8, 8, tmp_path / "o.rgba"])
+    assert r.returncode == 1 and "cannot map" in r.stderr
+
+
+def test_ragged_file_is_an_error(tmp_path):
+    f = tmp_path / "ragged.rgba"
+    f.write_bytes(b"\0" * (8 * 8 * 4 + 3))
+    r = _run(["callback", f, 8, 8, tmp_path / "o.rgba"])
+    assert r.returncode == 1 and "whole number" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 7])
+@pytest.mark.parametrize("colorize,filt,chroma", [(False, "none", "none"), (True, "sigmoid", "green")])
+def test_callback_file_matches_oracle(tmp_path, batch, colorize, filt, chroma):
+    w, h, n = 64, 40, 23
+    frames = np.random.default_rng(batch).integers(0, 256, (n, h, w, 4), dtype=np.uint8)
+    src, dst = tmp_path / "in.rgba", tmp_path / "out.rgba"
+    frames.tofile(src)
+    args = ["callback", src, w, h, dst, "--filter", filt, "--chroma", chroma, "--batch", batch]
+    if colorize:
+        args.append("--colorize")
+    r = _run(args)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(dst, dtype=np.uint8).reshape(n, h, w, 4)
+    codes = {"none": 255, "sigmoid": 0}
+    chromas = {"none": 0, "green": 2}
+    cs = oracle.ComputeState(colorize, 1, 5.0, codes[filt], chromas[chroma])
+    want = np.stack([oracle.frame_callback(w, h, f, cs) for f in frames])
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt,c", [("rgb8", 3), ("gray8", 1)])
+@pytest.mark.parametrize("mode", ["overall", "per-frame"])
+def test_series_csv_matches_oracle(tmp_path, fmt, c, mode):
+    w, h, n = 96, 40, 17
+    frames = oracle.synth(c, w, h, 3, 0, n)
+    src = tmp_path / "in.raw"
+    frames.tofile(src)
+    r = _run(["series", src, w, h, fmt, "--mode", mode, "--tau", 8 / 255, "--chunk", 5])
+    assert r.returncode == 0, r.stderr
+    rows = [line.split(",") for line in r.stdout.strip().splitlines()[1:]]
+    got = np.array([[int(x) for x in row[1:4]] for row in rows], dtype=np.uint64)
+    out4, si, _ = oracle.series(frames, mode=0 if mode == "overall" else 1, tau=8 / 255)
+    assert np.array_equal(got, out4[:, :3])
+    np.testing.assert_allclose([float(row[4]) for row in rows], si, rtol=1e-12, atol=1e-12)
