@@ -462,6 +462,7 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     const uint32_t rows = (uint32_t)std::max<size_t>(1, dips_host::piece_bytes() / row);
     const uint32_t n_s = (h->height + rows - 1) / rows;
     ALT_HIP(h, h->io_out.ensure(fb));
+    ALT_HIP(h, hipStreamSynchronize(h->meta_stream));  // no upload of an earlier call still reads `io`
     ALT_HIP(h, h->up_pieces.ensure(n_s));
     ALT_HIP(h, h->pieces.ensure(n_s));
     uint8_t* pin_in = h->io.bytes();

@@ -583,8 +583,11 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
     DIPS_HIP(h, h->up_pieces.ensure(n_s));
     DIPS_HIP(h, h->pieces.ensure(n_s));
     // the previous call's transfers out of io / into io_out are complete
-    // once the compute stream (which waited for every upload) has drained
+    // once both streams have drained (the compute stream waited for every
+    // upload; the upload stream is synchronised too in case an earlier call
+    // failed between its uploads and its kernels)
     DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
     // update_temporal_texture (bind_groups.rs:407-427)
     uint8_t* slot = h->slots[h->ring_idx].as<uint8_t>();
     h->uniform_idx = h->ring_idx;
