@@ -257,6 +257,24 @@ class DiPsRunner:
         self.compute.close()
 
 
+def run_loop_flags(n_frames: int, refresh_markers: Iterable[int] = ()) -> np.ndarray:
+    """The snapshot flag run_dips_on_file gives each of frames 0..n-1
+    (dips_alt/src/lib.rs:636-670, the same loop as dips_alt_run): a snapshot
+    when `index` reaches FRAME_COUNT; index counts up to FRAME_COUNT + 1 and
+    restarts at 0 after the frame whose 1-based position is a refresh marker."""
+    markers = set(int(m) for m in refresh_markers)
+    flags = np.zeros(n_frames, dtype=bool)
+    index = overall = 0
+    for t in range(n_frames):
+        flags[t] = index == FRAME_COUNT
+        if index <= FRAME_COUNT:
+            index += 1
+        overall += 1
+        if overall in markers:
+            index = 0
+    return flags
+
+
 def run_dips_on_frames(frames, properties: Optional[DiPsProperties] = None,
                        refresh_markers: Iterable[int] = (), device: int = 0) -> np.ndarray:
     """All of a clip's frames ([N, rows, cols, 4] RGBA8) through the
@@ -350,5 +368,5 @@ def parse_args(argv: Sequence[str]) -> CliArgs:
     return a
 
 
-__all__ = ["FRAME_COUNT", "Filter", "ChromaFilter", "Encoding", "DiPsProperties", "DiPsCompute",
+__all__ = ["FRAME_COUNT", "run_loop_flags", "Filter", "ChromaFilter", "Encoding", "DiPsProperties", "DiPsCompute",
            "DiPsRunner", "run_dips_on_frames", "CliArgs", "CliError", "parse_args"]

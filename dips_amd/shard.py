@@ -184,6 +184,68 @@ def compat_sharded(local_frames: torch.Tensor, t0: int, *,
     return callback_batch(local_frames)
 
 
+# ---------------------------------------------------------------------------
+# dips_alt run loop over frame ranges.  Output frame t reads the N texture
+# slots (frames t-N+1..t) and the snapshot texture, which the last snapshot
+# frame s < t set from the slots it saw (frames s-N+1..s); the snapshot
+# flags follow from the refresh markers alone (alt.run_loop_flags).  Rank k
+# therefore needs the raw frames s-N+1..s and t0-N..t0-1 from the ranks that
+# own them, replays them through a fresh DiPsCompute (snapshot on s,
+# outputs discarded) and continues with its own frames and flags -- no new
+# operator state beyond what send_frames already keeps.
+# ---------------------------------------------------------------------------
+def alt_replay_frames(t0: int, flags, num_textures: int) -> Tuple[List[int], List[bool]]:
+    """Global frames (>= 0) rank starting at t0 replays, with their flags."""
+    if t0 == 0:
+        return [], []
+    prior = [t for t in range(t0) if flags[t]]
+    frames, fl = [], []
+    if prior:
+        s = prior[-1]
+        for g in range(max(0, s - num_textures + 1), s + 1):
+            frames.append(g)
+            fl.append(g == s)
+    for g in range(max(0, t0 - num_textures), t0):
+        frames.append(g)
+        fl.append(False)
+    return frames, fl
+
+
+def alt_sharded(local_frames: torch.Tensor, t0: int, n_total: int, flags, num_textures: int, *,
+                send_frames: Callable[[torch.Tensor, List[bool]], torch.Tensor], group=None) -> torch.Tensor:
+    """dips_alt run loop over this rank's frames (global t0..), identical to
+    one DiPsCompute that saw every frame.  `flags`: run_loop_flags of all
+    n_total frames; send_frames(frames, flags) drives this rank's fresh
+    DiPsCompute and returns the outputs.  Needed frames travel point to
+    point from their owners (one op per frame, posted in increasing frame
+    order on both sides)."""
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    ranges = frame_ranges(n_total, world)
+    owner = lambda g: next(r for r, (a, b) in enumerate(ranges) if a <= g < b)  # noqa: E731
+    ops, recv = [], {}
+    for j in range(1, world):
+        need, _ = alt_replay_frames(ranges[j][0], flags, num_textures)
+        for g in sorted(set(need)):
+            o = owner(g)
+            if o == j:
+                continue
+            if o == rank:
+                ops.append(dist.P2POp(dist.isend, local_frames[g - t0].contiguous(), j, group))
+            elif j == rank:
+                buf = torch.empty_like(local_frames[0])
+                recv[g] = buf
+                ops.append(dist.P2POp(dist.irecv, buf, o, group))
+    works = dist.batch_isend_irecv(ops) if ops else []
+    for w in works:
+        w.wait()
+    need, fl = alt_replay_frames(t0, flags, num_textures)
+    if need:
+        replay = torch.stack([recv[g] for g in need])
+        send_frames(replay, fl)  # state only: slots and snapshot as at global frame t0
+    return send_frames(local_frames, [bool(f) for f in flags[t0:t0 + local_frames.shape[0]]])
+
+
 def sharded_series(local_frames: torch.Tensor, *, per_frame: bool, n_total: int,
                    compute: Callable[[torch.Tensor, Optional[torch.Tensor], torch.Tensor], None],
                    reference: Optional[torch.Tensor] = None, group=None,

@@ -151,3 +151,72 @@ def test_compat_sharded_equals_single(world, n_total, params):
     cs = oracle.ComputeState(*params)
     want = np.stack([oracle.frame_callback(w, h, f, cs) for f in frames])
     assert np.array_equal(got, want)
+
+
+def test_alt_run_loop_flags_match_oracle_loop():
+    """alt.run_loop_flags restates run_dips_on_file's snapshot schedule: one
+    oracle DiPsCompute fed frame by frame with those flags gives the oracle
+    run loop's outputs."""
+    from oracle import oracle
+    from dips_amd.alt import run_loop_flags
+    w, h, n = 12, 8, 30
+    frames = np.random.default_rng(5).integers(0, 256, (n, h, w, 4), dtype=np.uint8)
+    for markers in ([], [3], [5, 6, 19], [1, 2, 3, 28]):
+        flags = run_loop_flags(n, markers)
+        a = oracle.AltCompute(2, w, h)
+        got = np.stack([a.send_frame(frames[t], bool(flags[t])) for t in range(n)])
+        want = oracle.AltCompute(2, w, h).run(frames, markers)
+        assert np.array_equal(got, want), markers
+
+
+def _alt_worker(rank, world, port, n_total, n_tex, markers, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle
+        from dips_amd.alt import run_loop_flags
+        w, h = 14, 10
+        allf = np.random.default_rng(31).integers(0, 256, (n_total, h, w, 4), dtype=np.uint8)
+        s, e = shard.frame_range(n_total, world, rank)
+        local = torch.from_numpy(allf[s:e].copy())
+        flags = run_loop_flags(n_total, markers)
+        comp = oracle.AltCompute(n_tex, w, h, True, 1, 5.0, 0, 0)
+
+        def send_frames(fr, fl):
+            return torch.from_numpy(np.stack([comp.send_frame(f, bool(x)) for f, x in zip(fr.numpy(), fl)]))
+
+        out = shard.alt_sharded(local, s, n_total, flags, n_tex, send_frames=send_frames)
+        m = max(b - a for a, b in shard.frame_ranges(n_total, world))
+        pad = torch.zeros((m, h, w, 4), dtype=torch.uint8)
+        pad[: out.shape[0]] = out
+        bufs = [torch.zeros_like(pad) for _ in range(world)] if rank == 0 else None
+        dist.gather(pad, bufs, dst=0)
+        if rank == 0:
+            full = torch.cat([b[: e2 - s2] for b, (s2, e2) in zip(bufs, shard.frame_ranges(n_total, world))])
+            result_q.put(full.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total,n_tex,markers", [(2, 20, 2, [5, 6]), (3, 31, 3, [9, 10, 22]),
+                                                        (3, 12, 2, [2, 3, 4, 5, 6, 7, 8, 9, 10, 11])])
+def test_alt_sharded_equals_single(world, n_total, n_tex, markers):
+    """dips_alt run loop over frame ranges (the last snapshot's source frames
+    and an N-frame halo replayed into a fresh DiPsCompute) gives the single
+    loop's outputs, snapshots falling on and across shard edges."""
+    from oracle import oracle
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_alt_worker, args=(r, world, port, n_total, n_tex, markers, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    w, h = 14, 10
+    frames = np.random.default_rng(31).integers(0, 256, (n_total, h, w, 4), dtype=np.uint8)
+    want = oracle.AltCompute(n_tex, w, h, True, 1, 5.0, 0, 0).run(frames, markers)
+    assert np.array_equal(got, want)

@@ -217,3 +217,41 @@ def test_send_frame_striped_matches_oracle(monkeypatch, n_tex, filt, colorize, p
             assert np.array_equal(got, want), (t, np.argwhere(got != want)[:4])
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("n_tex,markers", [(2, [5, 6, 30]), (3, [4, 17, 18])])
+def test_replay_resume_matches_one_loop(n_tex, markers):
+    """Frame-range sharding of the dips_alt loop (shard.alt_sharded): a fresh
+    DiPsCompute that replays the last snapshot's source frames and the
+    N-frame halo, then takes frames t0.. with the loop's flags, gives the
+    outputs of one loop over every frame -- host and device pointers."""
+    import torch
+    from dips_amd import shard
+    from dips_amd.alt import DiPsCompute, DiPsRunner, run_loop_flags
+    w, h, n = 64, 32, 48
+    frames = _frames(w, h, n, 70 + n_tex)
+    props = _props(True, 1, 5.0, 0, 0)
+    r = DiPsRunner(h, w, props, markers, num_textures=n_tex)
+    try:
+        want = r(frames)
+    finally:
+        r.close()
+    flags = run_loop_flags(n, markers)
+    for t0 in (1, 7, 19, 33):
+        need, fl = shard.alt_replay_frames(t0, flags, n_tex)
+        c = DiPsCompute(n_tex, h, w, props)
+        try:
+            if need:
+                c.send_frames(frames[need], fl)
+            got = c.send_frames(frames[t0:], list(flags[t0:]))
+            assert np.array_equal(got, want[t0:]), (t0, np.argwhere(got != want[t0:])[:4])
+            dev = torch.from_numpy(frames).cuda()
+            if need:
+                rep = dev[need].contiguous()
+                c.send_frames_device(rep, torch.empty_like(rep), fl)
+            out = torch.empty_like(dev[t0:])
+            c.send_frames_device(dev[t0:].contiguous(), out, list(flags[t0:]))
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy(), want[t0:]), t0
+        finally:
+            c.close()
