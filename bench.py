@@ -138,6 +138,11 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     torch.cuda.set_device(local)  # one rank per GPU (RCCL rejects two ranks on one device)
+    if world > 1:
+        # leave one wave slot per SIMD to RCCL's send/recv kernels (the halo
+        # exchange runs beside the persistent series kernel); 4 and 5 waves
+        # per SIMD run the kernel at the same speed
+        os.environ.setdefault("DIPS_SERIES_WAVES_PER_SIMD", "4")
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)

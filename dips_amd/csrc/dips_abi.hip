@@ -167,7 +167,17 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
     g.items = g.n_tiles * n_frames;
     const void* k = dips::series_fast_kernel_ptr(C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map);
     if (!k) return g;
-    const uint64_t resident = (uint64_t)occupancy_blocks(h, k) * (uint64_t)h->cu_count * 4u;
+    // waves per SIMD: the kernel's occupancy, optionally capped by
+    // DIPS_SERIES_WAVES_PER_SIMD (bench.py sets 4 at N > 1 so that RCCL's
+    // halo kernels find a free slot beside the persistent grid instead of
+    // delaying part of it; 3-5 waves per SIMD run at the same speed,
+    // profiles/r01_wave_count_probe.txt)
+    uint64_t per_simd = (uint64_t)occupancy_blocks(h, k);
+    if (const char* cap = std::getenv("DIPS_SERIES_WAVES_PER_SIMD")) {
+        const unsigned long c = std::strtoul(cap, nullptr, 10);
+        if (c >= 1 && c < per_simd) per_simd = c;
+    }
+    const uint64_t resident = per_simd * (uint64_t)h->cu_count * 4u;
     g.n_waves = g.items < resident ? g.items : resident;
     g.blocks = (g.n_waves + 3) / 4;
     g.ok = g.n_tiles < (1ull << 32) && g.blocks < (1ull << 31);

@@ -239,3 +239,30 @@ def test_long_batch_segments_match_oracle(c, mode):
         out4, si, dmap = oracle.series(frames, mode=mode, chroma=chroma, tau=tau, want_map=True, nthreads=8)
         _check(got, out4, si, gmap, dmap)
         _check(got_nomap, out4, si)
+
+
+def test_wave_cap_same_series(monkeypatch):
+    """DIPS_SERIES_WAVES_PER_SIMD (set by bench.py at N > 1) only changes how
+    the (tile, frame) items are split over waves: same series, fewer waves."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    w, h, n = 640, 360, 300
+    dev = torch.empty((n, h, w, 3), dtype=torch.uint8, device="cuda")
+    out = []
+    for cap in (None, "3", "1"):
+        if cap is None:
+            monkeypatch.delenv("DIPS_SERIES_WAVES_PER_SIMD", raising=False)
+        else:
+            monkeypatch.setenv("DIPS_SERIES_WAVES_PER_SIMD", cap)
+        op = DiffSeriesOperator(PixelFormat.RGB8, Mode.PerFrame, 8 / 255, 0)
+        try:
+            op.synth_device(dev, w, h, 0xD1B5, 0)
+            ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+            op.run_device(dev, ser)
+            torch.cuda.synchronize()
+            waves, _, _ = op.geometry(w, h, n)
+            out.append((waves, ser.cpu().numpy()))
+        finally:
+            op.close()
+    assert out[0][0] > out[1][0] > out[2][0]
+    assert all(np.array_equal(out[0][1], o[1]) for o in out[1:])
