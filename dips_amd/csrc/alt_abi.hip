@@ -7,7 +7,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -458,43 +457,15 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     // W = 1 (per pixel): ~4 MiB row stripes -- stripe s goes up on the
     // upload stream, is processed as soon as it has landed and comes back on
     // the compute stream while stripes s+1.. still go up
-    const size_t row = (size_t)h->width * 4u;
-    const uint32_t rows = (uint32_t)std::max<size_t>(1, dips_host::piece_bytes() / row);
-    const uint32_t n_s = (h->height + rows - 1) / rows;
     ALT_HIP(h, h->io_out.ensure(fb));
     ALT_HIP(h, hipStreamSynchronize(h->meta_stream));  // no upload of an earlier call still reads `io`
-    ALT_HIP(h, h->up_pieces.ensure(n_s));
-    ALT_HIP(h, h->pieces.ensure(n_s));
-    uint8_t* pin_in = h->io.bytes();
-    uint8_t* pin_out = h->io_out.bytes();
-    std::atomic<int> err{(int)hipSuccess};
-    dips_host::CopyPool::global().run(n_s, [&](size_t si) {
-        const size_t o = si * rows * row, len = std::min<size_t>((size_t)rows * row, fb - o);
-        std::memcpy(pin_in + o, frame + o, len);
-        hipError_t e = hipMemcpyAsync(slot + o, pin_in + o, len, hipMemcpyHostToDevice, h->meta_stream);
-        if (e == hipSuccess) e = hipEventRecord(h->up_pieces.ev[si], h->meta_stream);
-        if (e != hipSuccess) err.store((int)e);
-    });
-    ALT_HIP(h, (hipError_t)err.load());
-    for (uint32_t si = 0; si < n_s; ++si) {
-        a.y0 = si * rows;
-        a.y1 = std::min(h->height, a.y0 + rows);
-        const size_t o = (size_t)a.y0 * row, len = (size_t)(a.y1 - a.y0) * row;
-        ALT_HIP(h, hipStreamWaitEvent(h->stream, h->up_pieces.ev[si], 0));
-        ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
-        ALT_HIP(h, hipMemcpyAsync(pin_out + o, h->out1.as<uint8_t>() + o, len, hipMemcpyDeviceToHost, h->stream));
-        ALT_HIP(h, hipEventRecord(h->pieces.ev[si], h->stream));
-    }
-    dips_host::CopyPool::global().run(n_s, [&](size_t si) {
-        const hipError_t e = hipEventSynchronize(h->pieces.ev[si]);
-        if (e != hipSuccess) {
-            err.store((int)e);
-            return;
-        }
-        const size_t o = si * rows * row;
-        std::memcpy(out + o, pin_out + o, std::min<size_t>((size_t)rows * row, fb - o));
-    });
-    ALT_HIP(h, (hipError_t)err.load());
+    ALT_HIP(h, dips_host::run_striped_frame(frame, out, h->height, (size_t)h->width * 4u, h->io.bytes(),
+                                            h->io_out.bytes(), slot, h->out1.as<uint8_t>(), h->meta_stream,
+                                            h->stream, h->up_pieces, h->pieces, [&](uint32_t y0, uint32_t y1) {
+                                                a.y0 = y0;
+                                                a.y1 = y1;
+                                                return dips::launch_alt_frame(a, h->stream);
+                                            }));
     return DIPS_OK;
 }
 

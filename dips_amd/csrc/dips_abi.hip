@@ -9,7 +9,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -587,11 +586,7 @@ dips_status frame_callback_device(dips_handle* h, uint32_t width, uint32_t heigh
 int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
     const uint32_t W = h->width, H = h->height;
     const size_t row = (size_t)W * 4u, fb = row * H;
-    const uint32_t rows = (uint32_t)std::max<size_t>(1, dips_host::piece_bytes() / row);
-    const uint32_t n_s = (H + rows - 1) / rows;
     DIPS_HIP(h, h->io_out.ensure(fb));
-    DIPS_HIP(h, h->up_pieces.ensure(n_s));
-    DIPS_HIP(h, h->pieces.ensure(n_s));
     // the previous call's transfers out of io / into io_out are complete
     // once both streams have drained (the compute stream waited for every
     // upload; the upload stream is synchronised too in case an earlier call
@@ -603,16 +598,6 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
     h->uniform_idx = h->ring_idx;
     h->ring_idx = (h->ring_idx + 1u) % 4u;
     h->added += 1;
-    uint8_t* pin_in = h->io.bytes();
-    std::atomic<int> err{(int)hipSuccess};
-    dips_host::CopyPool::global().run(n_s, [&](size_t si) {
-        const size_t o = si * rows * row, len = std::min<size_t>((size_t)rows * row, fb - o);
-        std::memcpy(pin_in + o, frame + o, len);
-        hipError_t e = hipMemcpyAsync(slot + o, pin_in + o, len, hipMemcpyHostToDevice, h->copy_stream);
-        if (e == hipSuccess) e = hipEventRecord(h->up_pieces.ev[si], h->copy_stream);
-        if (e != hipSuccess) err.store((int)e);
-    });
-    DIPS_HIP(h, (hipError_t)err.load());
     dips::CompatArgs a{};
     for (int k = 0; k < 4; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
     a.start = h->start.as<uint8_t>();
@@ -626,26 +611,13 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
     a.filter = h->p.filter_type;
     a.sensitivity = h->p.sensitivity;
     a.colorize = h->p.colorize ? 1u : 0u;
-    uint8_t* pin_out = h->io_out.bytes();
-    for (uint32_t si = 0; si < n_s; ++si) {
-        a.y0 = si * rows;
-        a.y1 = std::min(H, a.y0 + rows);
-        const size_t o = (size_t)a.y0 * row, len = (size_t)(a.y1 - a.y0) * row;
-        DIPS_HIP(h, hipStreamWaitEvent(h->stream, h->up_pieces.ev[si], 0));
-        DIPS_HIP(h, dips::launch_compat_main(a, h->stream));
-        DIPS_HIP(h, hipMemcpyAsync(pin_out + o, h->out.as<uint8_t>() + o, len, hipMemcpyDeviceToHost, h->stream));
-        DIPS_HIP(h, hipEventRecord(h->pieces.ev[si], h->stream));
-    }
-    dips_host::CopyPool::global().run(n_s, [&](size_t si) {
-        const hipError_t e = hipEventSynchronize(h->pieces.ev[si]);
-        if (e != hipSuccess) {
-            err.store((int)e);
-            return;
-        }
-        const size_t o = si * rows * row;
-        std::memcpy(out + o, pin_out + o, std::min<size_t>((size_t)rows * row, fb - o));
-    });
-    DIPS_HIP(h, (hipError_t)err.load());
+    DIPS_HIP(h, dips_host::run_striped_frame(frame, out, H, row, h->io.bytes(), h->io_out.bytes(), slot,
+                                             h->out.as<uint8_t>(), h->copy_stream, h->stream, h->up_pieces,
+                                             h->pieces, [&](uint32_t y0, uint32_t y1) {
+                                                 a.y0 = y0;
+                                                 a.y1 = y1;
+                                                 return dips::launch_compat_main(a, h->stream);
+                                             }));
     return 1;
 }
 

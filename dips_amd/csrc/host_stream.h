@@ -103,6 +103,53 @@ inline hipError_t download_via(uint8_t* host, const void* dev, size_t bytes, uin
     return (hipError_t)err.load();
 }
 
+// One frame through a per-pixel kernel in row stripes, both PCIe directions
+// at once: stripe s is staged by the copy pool and DMA'd into `dev_in` on
+// `up`; `launch(y0, y1)` enqueues the kernel of rows [y0, y1) on `compute`
+// once that stripe has landed; the stripe of `dev_out` then comes back on
+// `compute` and the pool copies it out as soon as its event fires.  The
+// caller makes sure both streams are idle and `pin_in` / `pin_out` (frame
+// size each) are free.
+template <typename Launch>
+hipError_t run_striped_frame(const uint8_t* frame, uint8_t* out, uint32_t height, size_t row, uint8_t* pin_in,
+                             uint8_t* pin_out, uint8_t* dev_in, const uint8_t* dev_out, hipStream_t up,
+                             hipStream_t compute, PieceEvents& up_ev, PieceEvents& down_ev, Launch&& launch) {
+    const size_t fb = row * height;
+    const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
+    const uint32_t n_s = (height + rows - 1) / rows;
+    hipError_t e = up_ev.ensure(n_s);
+    if (e == hipSuccess) e = down_ev.ensure(n_s);
+    if (e != hipSuccess) return e;
+    std::atomic<int> err{(int)hipSuccess};
+    CopyPool::global().run(n_s, [&](size_t si) {
+        const size_t o = si * rows * row, len = std::min<size_t>((size_t)rows * row, fb - o);
+        std::memcpy(pin_in + o, frame + o, len);
+        hipError_t r = hipMemcpyAsync(dev_in + o, pin_in + o, len, hipMemcpyHostToDevice, up);
+        if (r == hipSuccess) r = hipEventRecord(up_ev.ev[si], up);
+        if (r != hipSuccess) err.store((int)r);
+    });
+    if ((e = (hipError_t)err.load()) != hipSuccess) return e;
+    for (uint32_t si = 0; si < n_s; ++si) {
+        const uint32_t y0 = si * rows, y1 = std::min(height, y0 + rows);
+        const size_t o = (size_t)y0 * row, len = (size_t)(y1 - y0) * row;
+        if ((e = hipStreamWaitEvent(compute, up_ev.ev[si], 0)) != hipSuccess) return e;
+        if ((e = launch(y0, y1)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(pin_out + o, dev_out + o, len, hipMemcpyDeviceToHost, compute)) != hipSuccess)
+            return e;
+        if ((e = hipEventRecord(down_ev.ev[si], compute)) != hipSuccess) return e;
+    }
+    CopyPool::global().run(n_s, [&](size_t si) {
+        const hipError_t r = hipEventSynchronize(down_ev.ev[si]);
+        if (r != hipSuccess) {
+            err.store((int)r);
+            return;
+        }
+        const size_t o = si * rows * row;
+        std::memcpy(out + o, pin_out + o, std::min<size_t>((size_t)rows * row, fb - o));
+    });
+    return (hipError_t)err.load();
+}
+
 // Frames per pipelined chunk: ~256 MiB (two chunks in flight per direction
 // keep both PCIe directions and the kernel busy); DIPS_FEED_CHUNK_BYTES
 // overrides the byte budget (the tests use it to force many ragged chunks
