@@ -292,3 +292,55 @@ def test_resume_rejects_bad_arguments():
             cs3.resume(w, h, f[0], f[:3], 9)  # window 3: not on the batch path
     finally:
         cs3.close()
+
+
+def test_handles_on_concurrent_threads(monkeypatch):
+    """The ABI's threading contract: a handle is not internally synchronised,
+    but distinct handles may be driven from different threads at the same
+    time (ctypes drops the GIL during the calls; the staging copies share
+    one process-wide pool).  Four threads, each with its own ComputeState /
+    DiPsCompute, per-frame and batch calls, outputs equal to the oracle."""
+    import threading
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
+    from dips_amd.alt import DiPsCompute
+    w, h, n = 256, 192, 14
+    monkeypatch.setenv("DIPS_PIECE_BYTES", str(64 * 1024))  # several stripes: the copy pool runs
+    clips = [_frames(w, h, n, 500 + k) for k in range(4)]
+    results, errors = {}, []
+
+    def compat_worker(k):
+        try:
+            cs = ComputeState(True, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+            try:
+                got = [frame_callback(w, h, f, cs) for f in clips[k][:9]]
+                got += list(cs.frame_callback_batch(w, h, clips[k][9:]))
+            finally:
+                cs.close()
+            results[k] = np.stack(got)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    def alt_worker(k):
+        try:
+            c = DiPsCompute(2, h, w)
+            try:
+                got = [c.send_frame(f, True if t == 2 else None) for t, f in enumerate(clips[k][:6])]
+                got += list(c.send_frames(clips[k][6:]))
+            finally:
+                c.close()
+            results[k] = np.stack(got)
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    threads = [threading.Thread(target=compat_worker if k % 2 == 0 else alt_worker, args=(k,)) for k in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    for k in (0, 2):
+        assert np.array_equal(results[k], _oracle_callbacks(clips[k], (True, 1, 5.0, 0, 0))), k
+    for k in (1, 3):
+        ref = oracle.AltCompute(2, w, h)
+        want = np.stack([ref.send_frame(f, t == 2) for t, f in enumerate(clips[k])])
+        assert np.array_equal(results[k], want), k
