@@ -7,7 +7,8 @@
 //   alt_frame_kernel<N>   one send_frame dispatch (pre_compute_main :188-263)
 //                         for any N = num_textures in 1..16 and any spatial
 //                         window; W > 1 stages the intensity neighbourhood of
-//                         the 16x16 tile in LDS.
+//                         the 16x16 tile in LDS and sorts each window in
+//                         registers (window_net.h).
 //   alt_batch_kernel      a whole run of HBM-resident frames for N = 2, W = 1,
 //                         the configuration dips_alt runs (FRAME_COUNT = 2,
 //                         lib.rs:36; window_size 1, mod.rs:176-186).  A wave
@@ -23,6 +24,7 @@
 // so for n = 2 it is min(v0, v1) and for n = 1 it is 0.
 #include "epilogue_fast.h"
 #include "intensity_v2.h"
+#include "window_net.h"
 
 namespace dips {
 
@@ -58,26 +60,20 @@ __device__ void alt_stage_tile(float (*tile)[kLds], const uint8_t* img, uint32_t
 // W^2 - (2h)^2 zeros; the result is element W^2/2 + 1.  All values are >= 0,
 // so that element is 0 while it falls among the zeros, otherwise the
 // (k - zeros)-th smallest window value.
-__device__ float alt_window_select(float (*tile)[kLds], int window) {
+__host__ __device__ constexpr int alt_window_rank(int window) {
     const int hw = window / 2;
-    const int side = 2 * hw;
-    const int n = side * side;
+    const int n = (2 * hw) * (2 * hw);
     const int ws2 = window * window;
     const int zeros = ws2 - n;
     const int k = ws2 / 2 + 1;
-    if (k < zeros) return 0.0f;
-    const int kk = k - zeros;
-    const int tx = threadIdx.x, ty = threadIdx.y;
-    for (int c = 0; c < n; ++c) {
-        const float vc = tile[ty + c / side][tx + c % side];
-        int rank = 0;
-        for (int j = 0; j < n; ++j) {
-            const float vj = tile[ty + j / side][tx + j % side];
-            rank += (vj < vc || (vj == vc && j < c)) ? 1 : 0;
-        }
-        if (rank == kk) return vc;
-    }
-    return 0.0f;  // unreachable
+    return k < zeros ? -1 : k - zeros;
+}
+
+template <int SIDE>
+__device__ __forceinline__ float alt_window_select(float (*tile)[kLds], int window) {
+    const int kk = alt_window_rank(window);
+    if (kk < 0) return 0.0f;
+    return wnet::window_kth<SIDE, kLds>(tile, threadIdx.y, threadIdx.x, kk);
 }
 
 // Element [n/2] of the sorted zero-padded temporal array (see file comment).
@@ -103,25 +99,31 @@ __device__ __forceinline__ float alt_temporal(const float (&v)[N]) {
 
 __device__ __forceinline__ uint32_t gray_rgba(uint32_t s) { return s | (s << 8) | (s << 16) | (255u << 24); }
 
-template <int N>
+// SIDE = 2 * (window / 2); 0 for W = 1.
+template <int N, int SIDE>
 __global__ __launch_bounds__(256) void alt_frame_kernel(AltArgs a) {
     __shared__ float tile[kLds][kLds];
     const uint32_t x = blockIdx.x * kTile + threadIdx.x;
     const uint32_t y = a.y0 + blockIdx.y * kTile + threadIdx.y;
     const bool inside = x < a.width && y < (a.y1 ? a.y1 : a.height);
     const uint64_t p = (uint64_t)y * a.width + x;
-    float v[N];
+    float v[N] = {};
+    // median_array[k] = spatial_median_filter(coords, dims, k)
+    // (the generated array, dynamic_texture_array.rs:67-69)
+    if constexpr (SIDE == 0) {
 #pragma unroll
-    for (int k = 0; k < N; ++k) {
-        // median_array[k] = spatial_median_filter(coords, dims, k)
-        // (the generated array, dynamic_texture_array.rs:67-69)
-        if (a.window == 1) {
-            v[k] = inside ? alt_texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
-        } else {
+        for (int k = 0; k < N; ++k) v[k] = inside ? alt_texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
+    } else {
+        // one copy of the window network, run once per slot; the result is
+        // routed into v[] by an unrolled select (no dynamic register index)
+#pragma unroll 1
+        for (int k = 0; k < N; ++k) {
             __syncthreads();
-            alt_stage_tile(tile, a.slots[k], a.width, a.height, a.window / 2, a.chroma, a.y0);
+            alt_stage_tile(tile, a.slots[k], a.width, a.height, SIDE / 2, a.chroma, a.y0);
             __syncthreads();
-            v[k] = inside ? alt_window_select(tile, a.window) : 0.0f;
+            const float r = inside ? alt_window_select<SIDE>(tile, a.window) : 0.0f;
+#pragma unroll
+            for (int j = 0; j < N; ++j) v[j] = j == k ? r : v[j];
         }
     }
     if (!inside) return;
@@ -299,7 +301,13 @@ hipError_t launch_frame_n(const AltArgs& a, hipStream_t s) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
     dim3 grid((a.width + kTile - 1) / kTile, (yend - a.y0 + kTile - 1) / kTile);
-    hipLaunchKernelGGL(alt_frame_kernel<N>, grid, dim3(kTile, kTile), 0, s, a);
+    switch (a.window / 2) {
+#define DIPS_SIDE(H) \
+    case H: hipLaunchKernelGGL((alt_frame_kernel<N, 2 * H>), grid, dim3(kTile, kTile), 0, s, a); break;
+        DIPS_SIDE(0) DIPS_SIDE(1) DIPS_SIDE(2) DIPS_SIDE(3) DIPS_SIDE(4) DIPS_SIDE(5)
+#undef DIPS_SIDE
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -11,11 +11,14 @@
 // Both run one thread per pixel on 16x16 workgroups.  For a spatial window
 // W > 1 the workgroup first stages the intensity of its (16 + 2h - 1)^2
 // neighbourhood in LDS (out-of-frame texels are 0.0, dips_shader.wgsl:135-136)
-// and each thread selects the window's order statistic from LDS.  The
+// and each thread selects the window's order statistic from LDS through a
+// register sorting network (window_net.h).  Kernels are instantiated for
+// W = 1 and W > 1 so the W = 1 launches keep their small register budget.  The
 // reference filters the newest slot in place while neighbours read it (a
 // data race); here the filter reads a separate copy (`raw`).
 #include "dips_math.h"
 #include "dips_kernels.h"
+#include "window_net.h"
 
 namespace dips {
 
@@ -48,57 +51,61 @@ __device__ void stage_tile(float (*tile)[kLds], const uint8_t* img, uint32_t w, 
 // bubble sort (j+1 clamped to 120 by naga's Restrict policy) sorts indices
 // 0..min(W^2,120); the result is element min(W^2/2 + 1, 120).  All values are
 // >= 0, so that element is 0 while it falls among the zeros, otherwise the
-// (k - zeros)-th smallest window value.
-__device__ float window_select(float (*tile)[kLds], int window) {
+// (k - zeros)-th smallest window value.  window_rank is that rank among the
+// (2h)^2 window values, or -1 when the result falls among the zeros (W = 3:
+// k = 5 < 6 zeros, so W = 3 filters every texel to 0).
+__host__ __device__ constexpr int window_rank(int window) {
     const int hw = window / 2;
-    const int side = 2 * hw;
-    const int n = side * side;
+    const int n = (2 * hw) * (2 * hw);
     const int ws2 = window * window;
     const int region = (ws2 < 120 ? ws2 : 120) + 1;
     const int zeros = region - n;
-    int k = ws2 / 2 + 1;
-    if (k > 120) k = 120;
-    if (k < zeros) return 0.0f;
-    const int kk = k - zeros;
-    // tile[ty + j + hw][tx + i + hw] for i, j in [-hw, hw) -> rows/cols [ty, ty + side)
-    const int tx = threadIdx.x, ty = threadIdx.y;
-    for (int c = 0; c < n; ++c) {
-        const float vc = tile[ty + c / side][tx + c % side];
-        int rank = 0;
-        for (int j = 0; j < n; ++j) {
-            const float vj = tile[ty + j / side][tx + j % side];
-            rank += (vj < vc || (vj == vc && j < c)) ? 1 : 0;
-        }
-        if (rank == kk) return vc;
-    }
-    return 0.0f;  // unreachable
+    const int k = ws2 / 2 + 1 > 120 ? 120 : ws2 / 2 + 1;
+    return k < zeros ? -1 : k - zeros;
 }
 
+// tile[ty + j + hw][tx + i + hw] for i, j in [-hw, hw) -> rows/cols [ty, ty + SIDE)
+template <int SIDE>
+__device__ __forceinline__ float window_select(float (*tile)[kLds], int kk) {
+    return wnet::window_kth<SIDE, kLds>(tile, threadIdx.y, threadIdx.x, kk);
+}
+
+// SIDE = 2 * (window / 2): 0 for W = 1 (no neighbourhood), else the side of
+// the sorted window, so each launch carries only its own network's registers.
+template <int SIDE>
 __global__ __launch_bounds__(256) void compat_precompute_kernel(CompatArgs a) {
     __shared__ float tile[kLds][kLds];
     const uint32_t x = blockIdx.x * kTile + threadIdx.x;
     const uint32_t y = blockIdx.y * kTile + threadIdx.y;
     const bool inside = x < a.width && y < a.height;
     const uint64_t p = (uint64_t)y * a.width + x;
-    float m[4];
+    float m[4] = {};
+    if constexpr (SIDE == 0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (a.window == 1) {
-            m[k] = inside ? texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
-        } else {
+        for (int k = 0; k < 4; ++k) m[k] = inside ? texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
+    } else if (window_rank(a.window) < 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[k] = 0.0f;
+    } else {
+        // one copy of the window network, run once per slot (see alt_frame_kernel)
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
             __syncthreads();
-            stage_tile(tile, a.slots[k], a.width, a.height, a.window / 2, a.chroma);
+            stage_tile(tile, a.slots[k], a.width, a.height, SIDE / 2, a.chroma);
             __syncthreads();
-            m[k] = inside ? window_select(tile, a.window) : 0.0f;
+            const float r = inside ? window_select<SIDE>(tile, window_rank(a.window)) : 0.0f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m[j] = j == k ? r : m[j];
         }
-        // get_intensity(vec4(f, f, f, 1)) = f (pre_compute_shader.wgsl:105-108)
     }
+    // get_intensity(vec4(f, f, f, 1)) = f (pre_compute_shader.wgsl:105-108)
     if (!inside) return;
     const uint32_t s = unorm_store(upper_median4(m[0], m[1], m[2], m[3]));
     // start texture is gray RGBA8 (pre_compute_shader.wgsl:128-131)
     *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(a.start) + 4 * p) = s | (s << 8) | (s << 16) | (255u << 24);
 }
 
+template <int SIDE>
 __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
     __shared__ float tile[kLds][kLds];
     const uint32_t x = blockIdx.x * kTile + threadIdx.x;
@@ -107,19 +114,22 @@ __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
     const bool inside = x < a.width && y < yend;
     const uint64_t p = (uint64_t)y * a.width + x;
     float fi;
-    if (a.window == 1) {
+    if constexpr (SIDE == 0) {
         if (!inside) return;
         fi = texel_intensity(a.raw, p, a.chroma);
+    } else if (window_rank(a.window) < 0) {
+        if (!inside) return;
+        fi = 0.0f;
     } else {
-        stage_tile(tile, a.raw, a.width, a.height, a.window / 2, a.chroma, a.y0);
+        stage_tile(tile, a.raw, a.width, a.height, SIDE / 2, a.chroma, a.y0);
         __syncthreads();
         if (!inside) return;
-        fi = window_select(tile, a.window);
+        fi = window_select<SIDE>(tile, window_rank(a.window));
     }
     // in-place store of the filtered newest slot, quantised (dips_shader.wgsl:187)
     const uint32_t qi = unorm_store(fi);
     *reinterpret_cast<uint32_t*>(a.slots[a.newest] + 4 * p) = qi | (qi << 8) | (qi << 16) | (255u << 24);
-    float m[4];
+    float m[4] = {};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         // the newest slot re-reads its own quantised gray texel (:192)
@@ -149,7 +159,13 @@ hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, u
 
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s) {
     dim3 grid((a.width + kTile - 1) / kTile, (a.height + kTile - 1) / kTile);
-    hipLaunchKernelGGL(compat_precompute_kernel, grid, dim3(kTile, kTile), 0, s, a);
+    switch (a.window / 2) {
+#define DIPS_SIDE(H) \
+    case H: hipLaunchKernelGGL(compat_precompute_kernel<2 * H>, grid, dim3(kTile, kTile), 0, s, a); break;
+        DIPS_SIDE(0) DIPS_SIDE(1) DIPS_SIDE(2) DIPS_SIDE(3) DIPS_SIDE(4) DIPS_SIDE(5)
+#undef DIPS_SIDE
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -157,7 +173,13 @@ hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
     dim3 grid((a.width + kTile - 1) / kTile, (yend - a.y0 + kTile - 1) / kTile);
-    hipLaunchKernelGGL(compat_main_kernel, grid, dim3(kTile, kTile), 0, s, a);
+    switch (a.window / 2) {
+#define DIPS_SIDE(H) \
+    case H: hipLaunchKernelGGL(compat_main_kernel<2 * H>, grid, dim3(kTile, kTile), 0, s, a); break;
+        DIPS_SIDE(0) DIPS_SIDE(1) DIPS_SIDE(2) DIPS_SIDE(3) DIPS_SIDE(4) DIPS_SIDE(5)
+#undef DIPS_SIDE
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -50,6 +50,30 @@ def test_send_frame_matches_oracle(n_tex, window, filt, colorize, chroma):
         gpu.close()
 
 
+@pytest.mark.parametrize("ties", [False, True])
+@pytest.mark.parametrize("window", list(range(2, 12)))
+def test_send_frame_every_window_matches_oracle(window, ties):
+    """dips_alt spatial filter (W^2 sort, pre_compute_shader.wgsl:141-184) for
+    every window 2..11 on a ragged 53x29 frame; `ties` draws the bytes from
+    five values so most windows hold equal intensities."""
+    from dips_amd.alt import DiPsCompute
+    w, h = 53, 29
+    rng = np.random.default_rng(200 + window)
+    if ties:
+        frames = np.array([0, 1, 2, 128, 255], dtype=np.uint8)[rng.integers(0, 5, (5, h, w, 4))]
+    else:
+        frames = rng.integers(0, 256, (5, h, w, 4), dtype=np.uint8)
+    gpu = DiPsCompute(3, h, w, _props(True, window, 3.0, 255, 0))
+    ref = oracle.AltCompute(3, w, h, True, window, 3.0, 255, 0)
+    try:
+        for t in range(5):
+            a = gpu.send_frame(frames[t], () if t == 1 else None)
+            b = ref.send_frame(frames[t], t == 1)
+            assert np.array_equal(a, b), (t, np.argwhere(a != b)[:4])
+    finally:
+        gpu.close()
+
+
 BATCH_SHAPES = [(64, 48), (40, 17), (37, 21), (3, 1)]  # npx % 4 == 0 -> batch kernel; else per-frame
 
 

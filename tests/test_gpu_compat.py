@@ -47,6 +47,38 @@ def test_compute_state_matches_oracle(colorize, window, sens, filt, chroma):
         gpu.close()
 
 
+def _tie_frames(w, h, n, seed):
+    """Frames drawn from five byte values: many equal intensities per window."""
+    rng = np.random.default_rng(seed)
+    return np.array([0, 1, 2, 128, 255], dtype=np.uint8)[rng.integers(0, 5, (n, h, w, 4))]
+
+
+@pytest.mark.parametrize("ties", [False, True])
+@pytest.mark.parametrize("chroma", [0, 2])
+@pytest.mark.parametrize("window", list(range(2, 12)))
+def test_every_window_matches_oracle(window, chroma, ties):
+    """Spatial median (dips_shader.wgsl:120-170) for every window 2..11: each
+    side 2h = 2..10 and each rank the quirky index maps to (window_net.h
+    sorting networks), on a ragged 53x29 frame (partial 16x16 tiles)."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+    w, h = 53, 29
+    frames = (_tie_frames if ties else _frames)(w, h, 6, 100 + window)
+    gpu = ComputeState(True, window, 5.0, DiPsFilter.Unfiltered, ChromaFilter(chroma))
+    ref = oracle.ComputeState(True, window, 5.0, 255, chroma)
+    try:
+        for k in range(6):
+            gpu.add_texture(w, h, frames[k])
+            ref.add_texture(w, h, frames[k])
+            a, b = gpu.dispatch(), ref.dispatch()
+            if k < 3:
+                continue
+            assert np.array_equal(a, b), (k, np.argwhere(a != b)[:5])
+            if k == 3:
+                assert np.array_equal(gpu.start_texture(), ref.start_texture())
+    finally:
+        gpu.close()
+
+
 def test_frame_callback_passthrough_then_visual():
     """lib.rs:241-245: frames 0..2 come back unchanged; from frame 3 on the
     callback returns the visualisation."""

@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""window_rate.py -- dips ComputeState with the spatial median (SURVEY.md s8f
+next-3: W in 1..11) over HBM-resident 4K RGBA8 frames
+(frame_callback_batch_device; W > 1 runs frame by frame), frames/s by wall
+clock after a warm-up.  One JSON line per window size."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from dips_amd import ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, PixelFormat
+    W, H = 3840, 2160
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+    dev = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+    op = DiffSeriesOperator(PixelFormat.RGBA8)
+    op.synth_device(dev, W, H, 0xD1B5, 0)
+    op.close()
+    out = torch.empty_like(dev)
+    for win in range(1, 12):
+        cs = ComputeState(False, win, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
+        cs.frame_callback_batch_device(dev[:8], out[:8])  # warm-up + start texture
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        cs.frame_callback_batch_device(dev[8:], out[8:])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        cs.close()
+        m = n - 8
+        print(json.dumps({"window": win, "frames": m, "frames_per_s": round(m / dt, 1),
+                          "ms_per_frame": round(dt / m * 1e3, 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
