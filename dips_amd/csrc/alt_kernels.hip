@@ -7,8 +7,9 @@
 //   alt_frame_kernel<N>   one send_frame dispatch (pre_compute_main :188-263)
 //                         for any N = num_textures in 1..16 and any spatial
 //                         window; W > 1 stages the intensity neighbourhood of
-//                         the 16x16 tile in LDS and sorts each window in
-//                         registers (window_net.h).
+//                         the 16x16 tile in LDS and sorts the windows of two
+//                         vertically adjacent pixels per thread in registers
+//                         (window_net.h).
 //   alt_batch_kernel      a whole run of HBM-resident frames for N = 2, W = 1,
 //                         the configuration dips_alt runs (FRAME_COUNT = 2,
 //                         lib.rs:36; window_size 1, mod.rs:176-186).  A wave
@@ -41,12 +42,13 @@ __device__ __forceinline__ float alt_texel_intensity(const uint8_t* img, uint64_
 
 // Intensities of this workgroup's tile plus a halo of `halo` texels; texels
 // outside the frame are 0.0 (pre_compute_shader.wgsl:148-150).
+template <int NT = kTile * kTile>
 __device__ void alt_stage_tile(float (*tile)[kLds], const uint8_t* img, uint32_t w, uint32_t h, int halo,
                                uint32_t chroma, uint32_t y0) {
     const int ox = (int)(blockIdx.x * kTile) - halo;
     const int oy = (int)(y0 + blockIdx.y * kTile) - halo;
     const int span = kTile + 2 * halo;
-    for (int idx = threadIdx.y * kTile + threadIdx.x; idx < span * span; idx += kTile * kTile) {
+    for (int idx = threadIdx.y * kTile + threadIdx.x; idx < span * span; idx += NT) {
         const int ty = idx / span, tx = idx - ty * span;
         const int gx = ox + tx, gy = oy + ty;
         float v = 0.0f;
@@ -69,11 +71,17 @@ __host__ __device__ constexpr int alt_window_rank(int window) {
     return k < zeros ? -1 : k - zeros;
 }
 
+// The filtered intensities of the two vertically adjacent pixels at tile
+// rows ty, ty + 1 (window_net.h window_kth_pair).
 template <int SIDE>
-__device__ __forceinline__ float alt_window_select(float (*tile)[kLds], int window) {
-    const int kk = alt_window_rank(window);
-    if (kk < 0) return 0.0f;
-    return wnet::window_kth<SIDE, kLds>(tile, threadIdx.y, threadIdx.x, kk);
+__device__ __forceinline__ void alt_window_select2(float (*tile)[kLds], int window, int ty, float& f0, float& f1) {
+    constexpr int k0 = alt_window_rank(SIDE), k1 = alt_window_rank(SIDE + 1);
+    f0 = f1 = 0.0f;
+    if (window == SIDE) {
+        if constexpr (k0 >= 0) wnet::window_kth_pair<SIDE, k0, kLds>(tile, ty, threadIdx.x, f0, f1);
+    } else {
+        if constexpr (k1 >= 0) wnet::window_kth_pair<SIDE, k1, kLds>(tile, ty, threadIdx.x, f0, f1);
+    }
 }
 
 // Element [n/2] of the sorted zero-padded temporal array (see file comment).
@@ -99,34 +107,10 @@ __device__ __forceinline__ float alt_temporal(const float (&v)[N]) {
 
 __device__ __forceinline__ uint32_t gray_rgba(uint32_t s) { return s | (s << 8) | (s << 16) | (255u << 24); }
 
-// SIDE = 2 * (window / 2); 0 for W = 1.
-template <int N, int SIDE>
-__global__ __launch_bounds__(256) void alt_frame_kernel(AltArgs a) {
-    __shared__ float tile[kLds][kLds];
-    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
-    const uint32_t y = a.y0 + blockIdx.y * kTile + threadIdx.y;
-    const bool inside = x < a.width && y < (a.y1 ? a.y1 : a.height);
-    const uint64_t p = (uint64_t)y * a.width + x;
-    float v[N] = {};
-    // median_array[k] = spatial_median_filter(coords, dims, k)
-    // (the generated array, dynamic_texture_array.rs:67-69)
-    if constexpr (SIDE == 0) {
-#pragma unroll
-        for (int k = 0; k < N; ++k) v[k] = inside ? alt_texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
-    } else {
-        // one copy of the window network, run once per slot; the result is
-        // routed into v[] by an unrolled select (no dynamic register index)
-#pragma unroll 1
-        for (int k = 0; k < N; ++k) {
-            __syncthreads();
-            alt_stage_tile(tile, a.slots[k], a.width, a.height, SIDE / 2, a.chroma, a.y0);
-            __syncthreads();
-            const float r = inside ? alt_window_select<SIDE>(tile, a.window) : 0.0f;
-#pragma unroll
-            for (int j = 0; j < N; ++j) v[j] = j == k ? r : v[j];
-        }
-    }
-    if (!inside) return;
+// send_frame's per-pixel tail once the N slot intensities are known
+// (:228-261).
+template <int N>
+__device__ __forceinline__ void alt_finish(const AltArgs& a, uint64_t p, const float (&v)[N]) {
     const float med = alt_temporal<N>(v);
     uint32_t o;
     if (a.snapshot) {
@@ -141,6 +125,50 @@ __global__ __launch_bounds__(256) void alt_frame_kernel(AltArgs a) {
         o = visual_epilogue(unorm_load(a.snap[p]) - med, a.filter, a.scalar, a.colorize != 0u);
     }
     *reinterpret_cast<uint32_t*>(a.out + 4 * p) = o;
+}
+
+// SIDE = 2 * (window / 2): 0 for W = 1 (one pixel per thread, 16x16
+// threads), else two vertically adjacent pixels per thread (16x8 threads).
+template <int SIDE>
+constexpr int kAltRows = SIDE == 0 ? 1 : 2;
+
+template <int N, int SIDE>
+__global__ __launch_bounds__(256) void alt_frame_kernel(AltArgs a) {
+    constexpr int R = kAltRows<SIDE>;
+    __shared__ float tile[kLds][kLds];
+    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
+    const uint32_t yb = a.y0 + blockIdx.y * kTile + threadIdx.y * R;
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    float v[R][N] = {};
+    // median_array[k] = spatial_median_filter(coords, dims, k)
+    // (the generated array, dynamic_texture_array.rs:67-69)
+    if constexpr (SIDE == 0) {
+        if (x >= a.width || yb >= yend) return;
+        const uint64_t p = (uint64_t)yb * a.width + x;
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[0][k] = alt_texel_intensity(a.slots[k], p, a.chroma);
+    } else {
+        // one copy of the window network, run once per slot; the results are
+        // routed into v[][] by an unrolled select (no dynamic register index)
+#pragma unroll 1
+        for (int k = 0; k < N; ++k) {
+            __syncthreads();
+            alt_stage_tile<kTile * kTile / R>(tile, a.slots[k], a.width, a.height, SIDE / 2, a.chroma, a.y0);
+            __syncthreads();
+            float f0, f1;
+            alt_window_select2<SIDE>(tile, a.window, threadIdx.y * R, f0, f1);
+#pragma unroll
+            for (int j = 0; j < N; ++j) {
+                v[0][j] = j == k ? f0 : v[0][j];
+                v[1][j] = j == k ? f1 : v[1][j];
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t y = yb + r;
+        if (x < a.width && y < yend) alt_finish<N>(a, (uint64_t)y * a.width + x, v[r]);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -303,7 +331,7 @@ hipError_t launch_frame_n(const AltArgs& a, hipStream_t s) {
     dim3 grid((a.width + kTile - 1) / kTile, (yend - a.y0 + kTile - 1) / kTile);
     switch (a.window / 2) {
 #define DIPS_SIDE(H) \
-    case H: hipLaunchKernelGGL((alt_frame_kernel<N, 2 * H>), grid, dim3(kTile, kTile), 0, s, a); break;
+    case H: hipLaunchKernelGGL((alt_frame_kernel<N, 2 * H>), grid, dim3(kTile, kTile / kAltRows<2 * H>), 0, s, a); break;
         DIPS_SIDE(0) DIPS_SIDE(1) DIPS_SIDE(2) DIPS_SIDE(3) DIPS_SIDE(4) DIPS_SIDE(5)
 #undef DIPS_SIDE
         default: return hipErrorInvalidValue;

@@ -8,13 +8,13 @@
 //                      upper median of the four slots, diff against S,
 //                      filter / sensitivity / colour epilogue, RGBA8 out.
 //
-// Both run one thread per pixel on 16x16 workgroups.  For a spatial window
-// W > 1 the workgroup first stages the intensity of its (16 + 2h - 1)^2
+// Both cover 16x16 pixel tiles.  W = 1: one thread per pixel.  For a spatial
+// window W > 1 the workgroup first stages the intensity of its (16 + 2h)^2
 // neighbourhood in LDS (out-of-frame texels are 0.0, dips_shader.wgsl:135-136)
-// and each thread selects the window's order statistic from LDS through a
-// register sorting network (window_net.h).  Kernels are instantiated for
-// W = 1 and W > 1 so the W = 1 launches keep their small register budget.  The
-// reference filters the newest slot in place while neighbours read it (a
+// and each of its 16x8 threads selects the order statistic of two vertically
+// adjacent windows through register sorting networks (window_net.h).  Kernels
+// are instantiated per window side, so the W = 1 launches keep their small
+// register budget.  The reference filters the newest slot in place while neighbours read it (a
 // data race); here the filter reads a separate copy (`raw`).
 #include "dips_math.h"
 #include "dips_kernels.h"
@@ -31,13 +31,14 @@ __device__ __forceinline__ float texel_intensity(const uint8_t* img, uint64_t p,
     return intensity_rgb(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, chroma);
 }
 
-// Stage the intensity neighbourhood of this workgroup's tile.
+// Stage the intensity neighbourhood of this workgroup's tile (NT threads).
+template <int NT = kTile * kTile>
 __device__ void stage_tile(float (*tile)[kLds], const uint8_t* img, uint32_t w, uint32_t h, int halo,
                            uint32_t chroma, uint32_t y0 = 0) {
     const int ox = (int)(blockIdx.x * kTile) - halo;
     const int oy = (int)(y0 + blockIdx.y * kTile) - halo;
     const int span = kTile + 2 * halo;
-    for (int idx = threadIdx.y * kTile + threadIdx.x; idx < span * span; idx += kTile * kTile) {
+    for (int idx = threadIdx.y * kTile + threadIdx.x; idx < span * span; idx += NT) {
         const int ty = idx / span, tx = idx - ty * span;
         const int gx = ox + tx, gy = oy + ty;
         float v = 0.0f;
@@ -64,72 +65,75 @@ __host__ __device__ constexpr int window_rank(int window) {
     return k < zeros ? -1 : k - zeros;
 }
 
-// tile[ty + j + hw][tx + i + hw] for i, j in [-hw, hw) -> rows/cols [ty, ty + SIDE)
+// tile[ty + j + hw][tx + i + hw] for i, j in [-hw, hw) -> rows/cols [ty, ty + SIDE).
+// A thread filters the two pixels at tile rows ty, ty + 1 (window_kth_pair).
+// Windows SIDE and SIDE + 1 share the side; each gets its own rank constant.
 template <int SIDE>
-__device__ __forceinline__ float window_select(float (*tile)[kLds], int kk) {
-    return wnet::window_kth<SIDE, kLds>(tile, threadIdx.y, threadIdx.x, kk);
+__device__ __forceinline__ void window_select2(float (*tile)[kLds], int window, int ty, float& f0, float& f1) {
+    constexpr int k0 = window_rank(SIDE), k1 = window_rank(SIDE + 1);
+    f0 = f1 = 0.0f;
+    if (window == SIDE) {
+        if constexpr (k0 >= 0) wnet::window_kth_pair<SIDE, k0, kLds>(tile, ty, threadIdx.x, f0, f1);
+    } else {
+        if constexpr (k1 >= 0) wnet::window_kth_pair<SIDE, k1, kLds>(tile, ty, threadIdx.x, f0, f1);
+    }
 }
 
-// SIDE = 2 * (window / 2): 0 for W = 1 (no neighbourhood), else the side of
-// the sorted window, so each launch carries only its own network's registers.
+// SIDE = 2 * (window / 2): 0 for W = 1 (no neighbourhood, one pixel per
+// thread, 16x16 threads), else the side of the sorted window (two vertically
+// adjacent pixels per thread, 16x8 threads), so each launch carries only its
+// own network's registers.
+template <int SIDE>
+constexpr int kRows = SIDE == 0 ? 1 : 2;
+
 template <int SIDE>
 __global__ __launch_bounds__(256) void compat_precompute_kernel(CompatArgs a) {
+    constexpr int R = kRows<SIDE>;
     __shared__ float tile[kLds][kLds];
     const uint32_t x = blockIdx.x * kTile + threadIdx.x;
-    const uint32_t y = blockIdx.y * kTile + threadIdx.y;
-    const bool inside = x < a.width && y < a.height;
-    const uint64_t p = (uint64_t)y * a.width + x;
-    float m[4] = {};
+    const uint32_t yb = blockIdx.y * kTile + threadIdx.y * R;
+    float m[R][4] = {};
     if constexpr (SIDE == 0) {
+        const bool inside = x < a.width && yb < a.height;
+        const uint64_t p = (uint64_t)yb * a.width + x;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) m[k] = inside ? texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
-    } else if (window_rank(a.window) < 0) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) m[k] = 0.0f;
-    } else {
-        // one copy of the window network, run once per slot (see alt_frame_kernel)
+        for (int k = 0; k < 4; ++k) m[0][k] = inside ? texel_intensity(a.slots[k], p, a.chroma) : 0.0f;
+    } else if (window_rank(a.window) >= 0) {
+        // one copy of the window network, run once per slot; results routed
+        // into m[][] by an unrolled select (no dynamic register index)
 #pragma unroll 1
         for (int k = 0; k < 4; ++k) {
             __syncthreads();
-            stage_tile(tile, a.slots[k], a.width, a.height, SIDE / 2, a.chroma);
+            stage_tile<kTile * kTile / R>(tile, a.slots[k], a.width, a.height, SIDE / 2, a.chroma);
             __syncthreads();
-            const float r = inside ? window_select<SIDE>(tile, window_rank(a.window)) : 0.0f;
+            float f0, f1;
+            window_select2<SIDE>(tile, a.window, threadIdx.y * R, f0, f1);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) m[j] = j == k ? r : m[j];
+            for (int j = 0; j < 4; ++j) {
+                m[0][j] = j == k ? f0 : m[0][j];
+                m[1][j] = j == k ? f1 : m[1][j];
+            }
         }
     }
     // get_intensity(vec4(f, f, f, 1)) = f (pre_compute_shader.wgsl:105-108)
-    if (!inside) return;
-    const uint32_t s = unorm_store(upper_median4(m[0], m[1], m[2], m[3]));
-    // start texture is gray RGBA8 (pre_compute_shader.wgsl:128-131)
-    *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(a.start) + 4 * p) = s | (s << 8) | (s << 16) | (255u << 24);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t y = yb + r;
+        if (x >= a.width || y >= a.height) continue;
+        const uint64_t p = (uint64_t)y * a.width + x;
+        const uint32_t s = unorm_store(upper_median4(m[r][0], m[r][1], m[r][2], m[r][3]));
+        // start texture is gray RGBA8 (pre_compute_shader.wgsl:128-131)
+        *reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(a.start) + 4 * p) = s | (s << 8) | (s << 16) | (255u << 24);
+    }
 }
 
-template <int SIDE>
-__global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
-    __shared__ float tile[kLds][kLds];
-    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
-    const uint32_t y = a.y0 + blockIdx.y * kTile + threadIdx.y;
-    const uint32_t yend = a.y1 ? a.y1 : a.height;
-    const bool inside = x < a.width && y < yend;
-    const uint64_t p = (uint64_t)y * a.width + x;
-    float fi;
-    if constexpr (SIDE == 0) {
-        if (!inside) return;
-        fi = texel_intensity(a.raw, p, a.chroma);
-    } else if (window_rank(a.window) < 0) {
-        if (!inside) return;
-        fi = 0.0f;
-    } else {
-        stage_tile(tile, a.raw, a.width, a.height, SIDE / 2, a.chroma, a.y0);
-        __syncthreads();
-        if (!inside) return;
-        fi = window_select<SIDE>(tile, window_rank(a.window));
-    }
+// compute_main's per-pixel tail once the newest slot's filtered intensity fi
+// is known (dips_shader.wgsl:187-239).
+__device__ __forceinline__ void compat_finish(const CompatArgs& a, uint64_t p, float fi) {
     // in-place store of the filtered newest slot, quantised (dips_shader.wgsl:187)
     const uint32_t qi = unorm_store(fi);
     *reinterpret_cast<uint32_t*>(a.slots[a.newest] + 4 * p) = qi | (qi << 8) | (qi << 16) | (255u << 24);
-    float m[4] = {};
+    float m[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         // the newest slot re-reads its own quantised gray texel (:192)
@@ -138,6 +142,29 @@ __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
     const float original = unorm_load(a.start[4 * p]);  // textureLoad(start_texture).r (:213)
     const float diff = original - upper_median4(m[0], m[1], m[2], m[3]);
     *reinterpret_cast<uint32_t*>(a.out + 4 * p) = visual_epilogue(diff, a.filter, a.sensitivity, a.colorize != 0u);
+}
+
+template <int SIDE>
+__global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
+    constexpr int R = kRows<SIDE>;
+    __shared__ float tile[kLds][kLds];
+    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
+    const uint32_t yb = a.y0 + blockIdx.y * kTile + threadIdx.y * R;
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    float fi[R] = {};
+    if constexpr (SIDE == 0) {
+        if (x >= a.width || yb >= yend) return;
+        fi[0] = texel_intensity(a.raw, (uint64_t)yb * a.width + x, a.chroma);
+    } else if (window_rank(a.window) >= 0) {
+        stage_tile<kTile * kTile / R>(tile, a.raw, a.width, a.height, SIDE / 2, a.chroma, a.y0);
+        __syncthreads();
+        window_select2<SIDE>(tile, a.window, threadIdx.y * R, fi[0], fi[1]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t y = yb + r;
+        if (x < a.width && y < yend) compat_finish(a, (uint64_t)y * a.width + x, fi[r]);
+    }
 }
 
 // A ring slot as frame_callback leaves it for a W = 1 frame: the gray texel
@@ -161,7 +188,7 @@ hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s) {
     dim3 grid((a.width + kTile - 1) / kTile, (a.height + kTile - 1) / kTile);
     switch (a.window / 2) {
 #define DIPS_SIDE(H) \
-    case H: hipLaunchKernelGGL(compat_precompute_kernel<2 * H>, grid, dim3(kTile, kTile), 0, s, a); break;
+    case H: hipLaunchKernelGGL(compat_precompute_kernel<2 * H>, grid, dim3(kTile, kTile / kRows<2 * H>), 0, s, a); break;
         DIPS_SIDE(0) DIPS_SIDE(1) DIPS_SIDE(2) DIPS_SIDE(3) DIPS_SIDE(4) DIPS_SIDE(5)
 #undef DIPS_SIDE
         default: return hipErrorInvalidValue;
@@ -175,7 +202,7 @@ hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s) {
     dim3 grid((a.width + kTile - 1) / kTile, (yend - a.y0 + kTile - 1) / kTile);
     switch (a.window / 2) {
 #define DIPS_SIDE(H) \
-    case H: hipLaunchKernelGGL(compat_main_kernel<2 * H>, grid, dim3(kTile, kTile), 0, s, a); break;
+    case H: hipLaunchKernelGGL(compat_main_kernel<2 * H>, grid, dim3(kTile, kTile / kRows<2 * H>), 0, s, a); break;
         DIPS_SIDE(0) DIPS_SIDE(1) DIPS_SIDE(2) DIPS_SIDE(3) DIPS_SIDE(4) DIPS_SIDE(5)
 #undef DIPS_SIDE
         default: return hipErrorInvalidValue;

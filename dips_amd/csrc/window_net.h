@@ -16,7 +16,8 @@
 //     both ends below n (pads at the top positions would be +inf, and an
 //     ascending comparator whose upper end holds +inf is a no-op, so the
 //     dropped comparators never change anything);
-//   * element kk is picked with an unrolled select.
+//   * the rank kk is a template argument (one instantiation per window), so
+//     the compiler drops every comparator that does not feed element kk.
 //
 // Intensities are +0.0 or positive finite floats, so their bit patterns
 // order exactly like their values: a comparator is one v_min_u32 + one
@@ -79,10 +80,13 @@ __device__ __forceinline__ void run_network(uint32_t* v, std::index_sequence<I..
     (cmpx<NetHolder<N>::net.lo[I], NetHolder<N>::net.hi[I]>(v), ...);
 }
 
-// kk-th smallest (0-based) of tile[ty + r][tx + c], r, c in [0, SIDE).
-template <int SIDE, int LDS>
-__device__ __forceinline__ float window_kth(const float (*tile)[LDS], int ty, int tx, int kk) {
+// KK-th smallest (0-based) of tile[ty + r][tx + c], r, c in [0, SIDE).  KK is
+// a compile-time constant, so after unrolling only the comparators that feed
+// element KK survive (~19 % fewer at side 10) and no select is needed.
+template <int SIDE, int KK, int LDS>
+__device__ __forceinline__ float window_kth(const float (*tile)[LDS], int ty, int tx) {
     constexpr int n = SIDE * SIDE;
+    static_assert(KK >= 0 && KK < n, "rank outside the window");
     static_assert(NetHolder<n>::net.count <= kMaxComparators, "network too large");
     uint32_t v[n];
 #pragma unroll
@@ -90,10 +94,58 @@ __device__ __forceinline__ float window_kth(const float (*tile)[LDS], int ty, in
 #pragma unroll
         for (int c = 0; c < SIDE; ++c) v[r * SIDE + c] = __float_as_uint(tile[ty + r][tx + c]);
     run_network<n>(v, std::make_index_sequence<NetHolder<n>::net.count>{});
-    uint32_t out = 0;
+    return __uint_as_float(v[KK]);
+}
+
+// The same order statistic for the two vertically adjacent windows at tile
+// rows [ty, ty + SIDE) and [ty + 1, ty + SIDE + 1).  They share the
+// SIDE - 1 middle rows (m = SIDE (SIDE - 1) values, sorted once); each adds
+// one private row (SIDE values, sorted).  The KK-th smallest of a sorted S
+// and a sorted row R is min over i of max(S[KK - i], R[i - 1]) (i values taken
+// from R), so only S[KK - SIDE .. KK] is needed and the compiler keeps only
+// the comparators feeding those.  Side 10: ~455 comparators per pixel
+// instead of ~890.
+template <int M, int R, int KK>
+__device__ __forceinline__ uint32_t kth_of_two(const uint32_t* s, const uint32_t* r) {
+    constexpr int lo = KK + 1 - M > 0 ? KK + 1 - M : 0;
+    constexpr int hi = R < KK + 1 ? R : KK + 1;
+    uint32_t best = 0xFFFFFFFFu;
 #pragma unroll
-    for (int i = 0; i < n; ++i) out = i == kk ? v[i] : out;
-    return __uint_as_float(out);
+    for (int i = lo; i <= hi; ++i) {
+        const int si = KK - i < 0 ? 0 : KK - i;
+        const int ri = i - 1 < 0 ? 0 : i - 1;
+        uint32_t term;
+        if (i == 0)
+            term = s[si];                            // nothing from R
+        else if (KK - i < 0)
+            term = r[ri];                            // all KK + 1 from R
+        else
+            term = s[si] > r[ri] ? s[si] : r[ri];
+        best = term < best ? term : best;
+    }
+    return best;
+}
+
+template <int SIDE, int KK, int LDS>
+__device__ __forceinline__ void window_kth_pair(const float (*tile)[LDS], int ty, int tx, float& out0,
+                                                float& out1) {
+    constexpr int m = SIDE * (SIDE - 1);
+    static_assert(KK >= 0 && KK < SIDE * SIDE, "rank outside the window");
+    uint32_t s[m], r0[SIDE], r1[SIDE];
+#pragma unroll
+    for (int c = 0; c < SIDE; ++c) {
+        r0[c] = __float_as_uint(tile[ty][tx + c]);
+        r1[c] = __float_as_uint(tile[ty + SIDE][tx + c]);
+    }
+#pragma unroll
+    for (int r = 0; r < SIDE - 1; ++r)
+#pragma unroll
+        for (int c = 0; c < SIDE; ++c) s[r * SIDE + c] = __float_as_uint(tile[ty + 1 + r][tx + c]);
+    run_network<m>(s, std::make_index_sequence<NetHolder<m>::net.count>{});
+    run_network<SIDE>(r0, std::make_index_sequence<NetHolder<SIDE>::net.count>{});
+    run_network<SIDE>(r1, std::make_index_sequence<NetHolder<SIDE>::net.count>{});
+    out0 = __uint_as_float(kth_of_two<m, SIDE, KK>(s, r0));
+    out1 = __uint_as_float(kth_of_two<m, SIDE, KK>(s, r1));
 }
 
 }  // namespace wnet
