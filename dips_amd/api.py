@@ -247,7 +247,7 @@ class ComputeState:
     # -- frame-range sharding (3-frame halo + start texture) --
     def resume(self, width: int, height: int, start, halo, t0: int) -> None:
         """Continue as if frame_callback had seen global frames 0..t0-1
-        (t0 >= 7, window 1): `start` is the start texture of the handle that
+        (t0 >= 7, any window): `start` is the start texture of the handle that
         saw frames 0..3, `halo` the raw RGBA8 frames t0-3..t0-1 ([3, H, W, 4])."""
         s, hl = _as_u8(start), _as_u8(halo)
         if s.size != width * height * 4 or hl.size != 3 * width * height * 4:

@@ -184,6 +184,51 @@ hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, u
     return hipGetLastError();
 }
 
+// The ring texel of compute_main for a whole batch of frames (W > 1, steady
+// state): gray q(filtered intensity), the same value compat_main stores into
+// the newest slot (dips_shader.wgsl:187).  blockIdx.z = frame.
+template <int SIDE>
+__global__ __launch_bounds__(256) void compat_filter_frames_kernel(const uint8_t* __restrict__ frames,
+                                                                   uint8_t* __restrict__ dst, uint32_t w, uint32_t h,
+                                                                   int32_t window, uint32_t chroma) {
+    constexpr int R = kRows<SIDE>;
+    __shared__ float tile[kLds][kLds];
+    const uint64_t fo = (uint64_t)blockIdx.z * w * h * 4u;
+    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
+    const uint32_t yb = blockIdx.y * kTile + threadIdx.y * R;
+    float fi[R] = {};
+    if (window_rank(window) >= 0) {
+        stage_tile<kTile * kTile / R>(tile, frames + fo, w, h, SIDE / 2, chroma);
+        __syncthreads();
+        window_select2<SIDE>(tile, window, threadIdx.y * R, fi[0], fi[1]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t y = yb + r;
+        if (x >= w || y >= h) continue;
+        const uint32_t q = unorm_store(fi[r]);
+        *reinterpret_cast<uint32_t*>(dst + fo + 4 * ((uint64_t)y * w + x)) = q | (q << 8) | (q << 16) | (255u << 24);
+    }
+}
+
+hipError_t launch_compat_filter_frames(const uint8_t* frames, uint8_t* dst, uint32_t width, uint32_t height,
+                                       uint32_t n, int32_t window, uint32_t chroma, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (window < 2 || window > 2 * kMaxHalo + 1 || n > 65535u) return hipErrorInvalidValue;
+    dim3 grid((width + kTile - 1) / kTile, (height + kTile - 1) / kTile, n);
+    switch (window / 2) {
+#define DIPS_SIDE(H)                                                                                                \
+    case H:                                                                                                         \
+        hipLaunchKernelGGL(compat_filter_frames_kernel<2 * H>, grid, dim3(kTile, kTile / 2), 0, s, frames, dst, width, \
+                           height, window, chroma);                                                                 \
+        break;
+        DIPS_SIDE(1) DIPS_SIDE(2) DIPS_SIDE(3) DIPS_SIDE(4) DIPS_SIDE(5)
+#undef DIPS_SIDE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s) {
     dim3 grid((a.width + kTile - 1) / kTile, (a.height + kTile - 1) / kTile);
     switch (a.window / 2) {

@@ -75,6 +75,7 @@ struct dips_handle {
     HostPinned io;
     uint64_t added = 0;       // frames added so far (global frame index of the next one)
     DevBuf slots_alt[4];      // second ring for the multi-chunk batch kernel (swapped in after it)
+    DevBuf filtered;          // W > 1 batch: ring texels of a chunk of frames (compat_filter_frames)
     dips_host::StreamPipe pipe;  // host-pointer feed of dips_frame_callback_batch
     dips_host::PieceEvents pieces;  // per-piece completion of the per-frame readback
     dips_host::PieceEvents up_pieces;  // per-stripe upload completion (striped frame_callback)
@@ -350,6 +351,7 @@ void dips_destroy(dips_handle* h) {
     h->probe_out.release();
     h->io_out.release();
     h->raw.release();
+    h->filtered.release();
     h->start.release();
     h->out.release();
     h->io.release();
@@ -473,14 +475,18 @@ int dispatch_impl(dips_handle* h, uint8_t* out, size_t cap, bool device_dst) {
     return 1;
 }
 
+dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_t m, const uint8_t* filter_src);
+
 // frame_callback over frames[0..n) (device pointers), asynchronous: the
 // first frames of the stream one by one (start texture, unquantised ring),
-// then the steady state (global frame >= 7, W = 1) in one batch kernel.
+// then the steady state (global frame >= 7) in one batch kernel; for W > 1
+// the frames are first replaced by their filtered ring texels, a chunk at a
+// time (compat_filter_frames), and the batch kernel runs on those.
 dips_status frame_callback_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames, uint32_t n,
                                   uint8_t* out) {
     const size_t fb = (size_t)width * height * 4u;
     uint32_t t = 0;
-    for (; t < n && (h->added < 7 || h->p.spatial_window_size != 1); ++t) {
+    for (; t < n && h->added < 7; ++t) {
         dips_status st = add_texture_impl(h, width, height, frames + (size_t)t * fb, fb, true);
         if (st != DIPS_OK) return st;
         const int r = dispatch_impl(h, out + (size_t)t * fb, fb, true);
@@ -506,6 +512,28 @@ dips_status frame_callback_device(dips_handle* h, uint32_t width, uint32_t heigh
         }
         return DIPS_OK;
     }
+    const int32_t window = h->p.spatial_window_size;
+    if (window == 1) return batch_steady(h, bf, bo, m, nullptr);
+    // filtered ring texels of up to g frames at a time (~1 GiB of scratch)
+    uint64_t g = std::max<uint64_t>(16u, (1ull << 30) / fb);
+    if (const char* e = std::getenv("DIPS_WINDOW_BATCH_FRAMES")) g = std::max(1ul, std::strtoul(e, nullptr, 10));
+    g = std::min<uint64_t>(std::min<uint64_t>(g, m), 65535u);
+    DIPS_HIP(h, h->filtered.ensure(g * fb));
+    for (uint32_t s0 = 0; s0 < m; s0 += (uint32_t)g) {
+        const uint32_t gn = (uint32_t)std::min<uint64_t>(g, m - s0);
+        dips_status st = batch_steady(h, h->filtered.as<uint8_t>(), bo + (size_t)s0 * fb, gn, bf + (size_t)s0 * fb);
+        if (st != DIPS_OK) return st;
+    }
+    return DIPS_OK;
+}
+
+// The batch kernel over m steady-state frames at bf (device, 16-B aligned),
+// outputs to bo; the ring slots are read before and rewritten after.  With
+// filter_src, the m frames there are first filtered into bf (W > 1).
+dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_t m, const uint8_t* filter_src) {
+    const uint32_t width = h->width, height = h->height;
+    const size_t fb = (size_t)width * height * 4u;
+    const uint64_t npx = (uint64_t)width * height;
     const bool fast = dips::alt_fast_epilogue_ok(h->p.filter_type, h->p.sensitivity);
     const void* k = dips::compat_batch_kernel_ptr((int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0,
                                                   fast);
@@ -560,6 +588,9 @@ dips_status frame_callback_device(dips_handle* h, uint32_t width, uint32_t heigh
         if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
         DIPS_HIP(h, hipEventRecord(e0, h->stream));
     }
+    if (filter_src)
+        DIPS_HIP(h, dips::launch_compat_filter_frames(filter_src, const_cast<uint8_t*>(bf), width, height, m,
+                                                      h->p.spatial_window_size, h->p.chroma_filter, h->stream));
     DIPS_HIP(h, dips::launch_compat_batch(a, (int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0, fast,
                                           (uint32_t)((n_tiles * n_chunks + 3u) / 4u), h->stream));
     if (timing) {
@@ -663,8 +694,6 @@ dips_status dips_compat_resume(dips_handle* h, uint32_t width, uint32_t height, 
     if (!start_rgba || !halo || width == 0 || height == 0)
         return fail(h, DIPS_ERR_INVALID, "compat_resume: null or empty argument");
     if (t0 < 7) return fail(h, DIPS_ERR_INVALID, "compat_resume: t0 must be >= 7 (steady state of the ring)");
-    if (h->p.spatial_window_size != 1)
-        return fail(h, DIPS_ERR_INVALID, "compat_resume: only spatial_window_size 1 (the batch path) resumes");
     const size_t fb = (size_t)width * height * 4u;
     const bool dev = (h->p.flags & DIPS_FLAG_DEVICE_PTRS) != 0;
     for (auto& sl : h->slots) DIPS_HIP(h, sl.ensure(fb));
@@ -675,7 +704,7 @@ dips_status dips_compat_resume(dips_handle* h, uint32_t width, uint32_t height, 
     DIPS_HIP(h, hipStreamSynchronize(h->stream));
     const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     DIPS_HIP(h, hipMemcpyAsync(h->start.p, start_rgba, fb, kind, h->stream));
-    // slot (t0-1-j) mod 4 <- gray texel of frame t0-1-j (halo[2-j]); the
+    // slot (t0-1-j) mod 4 <- ring texel of frame t0-1-j (halo[2-j]); the
     // raw frame goes through h->raw when it comes from the host
     for (int j = 0; j < 3; ++j) {
         const uint8_t* src = halo + (size_t)(2 - j) * fb;
@@ -683,8 +712,12 @@ dips_status dips_compat_resume(dips_handle* h, uint32_t width, uint32_t height, 
             DIPS_HIP(h, hipMemcpyAsync(h->raw.p, src, fb, hipMemcpyHostToDevice, h->stream));
             src = h->raw.as<uint8_t>();
         }
-        DIPS_HIP(h, dips::launch_compat_gray(src, h->slots[(t0 - 1 - (uint64_t)j) % 4u].as<uint8_t>(),
-                                             (uint64_t)width * height, h->p.chroma_filter, h->stream));
+        uint8_t* slot = h->slots[(t0 - 1 - (uint64_t)j) % 4u].as<uint8_t>();
+        if (h->p.spatial_window_size == 1)
+            DIPS_HIP(h, dips::launch_compat_gray(src, slot, (uint64_t)width * height, h->p.chroma_filter, h->stream));
+        else  // the filtered texel compute_main stored (dips_shader.wgsl:120-170, 187)
+            DIPS_HIP(h, dips::launch_compat_filter_frames(src, slot, width, height, 1, h->p.spatial_window_size,
+                                                          h->p.chroma_filter, h->stream));
     }
     DIPS_HIP(h, hipMemsetAsync(h->slots[t0 % 4u].p, 0, fb, h->stream));
     if (!dev) DIPS_HIP(h, hipStreamSynchronize(h->stream));  // host buffers are borrowed for the call only

@@ -165,5 +165,11 @@ hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, 
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, uint32_t chroma, hipStream_t s);
+// W > 1 steady state: the ring texel compute_main stores for each of n frames
+// (gray q(spatial_median_filter(frame)), dips_shader.wgsl:120-170, 187), so
+// that the batch kernel can run on the filtered frames.  frames, dst: n x
+// width x height RGBA8.
+hipError_t launch_compat_filter_frames(const uint8_t* frames, uint8_t* dst, uint32_t width, uint32_t height,
+                                       uint32_t n, int32_t window, uint32_t chroma, hipStream_t s);
 
 }  // namespace dips

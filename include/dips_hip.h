@@ -151,8 +151,9 @@ int dips_start_texture(dips_handle *h, uint8_t *out_rgba, size_t cap);
  * ring and start texture of dips/src/gpu/mod.rs:170-216, bind_groups.rs:
  * 407-427), rebuilt from the start texture S (dips_start_texture of the
  * handle that saw frames 0..3) and the raw RGBA8 frames t0-3, t0-2, t0-1
- * (`halo`, 3 contiguous frames in that order).  Requires t0 >= 7 and
- * spatial_window_size 1.  Device pointers with DIPS_FLAG_DEVICE_PTRS
+ * (`halo`, 3 contiguous frames in that order; for spatial_window_size > 1
+ * they are filtered into the ring as compute_main would have).  Requires
+ * t0 >= 7.  Device pointers with DIPS_FLAG_DEVICE_PTRS
  * (asynchronous), host pointers otherwise. */
 dips_status dips_compat_resume(dips_handle *h, uint32_t width, uint32_t height,
                                const uint8_t *start_rgba, const uint8_t *halo, uint64_t t0);

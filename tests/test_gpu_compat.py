@@ -174,6 +174,35 @@ def test_frame_callback_batch_matches_oracle(colorize, window, sens, filt, chrom
         assert np.array_equal(got, want), ((w, h), pieces, np.argwhere(got != want)[:4])
 
 
+@pytest.mark.parametrize("scratch_frames", [None, 5])
+@pytest.mark.parametrize("chroma", [0, 2])
+@pytest.mark.parametrize("window", list(range(2, 12)))
+def test_frame_callback_batch_window_matches_oracle(window, chroma, scratch_frames, monkeypatch):
+    """W > 1 in steady state: compat_filter_frames writes the filtered ring
+    texels of a chunk of frames, then the batch kernel runs on them.  Every
+    window 2..11, split calls (the ring carries over), a scratch of 5 frames
+    (several filter + batch rounds per call, each round's first frames read
+    the ring the previous round left) and a 20-frame hold (ties)."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+    if scratch_frames is not None:
+        monkeypatch.setenv("DIPS_WINDOW_BATCH_FRAMES", str(scratch_frames))
+    params = (True, window, 5.0, 0, chroma)
+    for (w, h), pieces in [((40, 21), [30]), ((64, 48), [9, 4, 17])]:
+        frames = (_tie_frames if window % 2 else _frames)(w, h, 30, 300 + window)
+        frames[20] = frames[19]
+        want = _oracle_callbacks(frames, params)
+        cs = ComputeState(True, window, 5.0, DiPsFilter.Sigmoid, ChromaFilter(chroma))
+        try:
+            outs, s = [], 0
+            for k in pieces:
+                outs.append(cs.frame_callback_batch(w, h, frames[s:s + k]))
+                s += k
+        finally:
+            cs.close()
+        got = np.concatenate(outs)
+        assert np.array_equal(got, want), ((w, h), pieces, np.argwhere(got != want)[:4])
+
+
 def test_frame_callback_batch_multi_chunk_and_mixed_calls():
     """A small frame (4 tiles) over 150 frames runs as ~10 frame chunks (the
     second ring set and the chunk-start rebuild from HBM); per-frame calls
@@ -305,6 +334,33 @@ def test_resume_matches_continuous_run(colorize, sens, filt, chroma):
             b.close()
 
 
+@pytest.mark.parametrize("window", [2, 3, 5, 8, 11])
+def test_resume_window_matches_continuous_run(window):
+    """dips_compat_resume with a spatial window: the halo frames are filtered
+    into the ring (compat_filter_frames), then batch and per-frame calls
+    continue exactly like one ComputeState that saw every frame."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
+    w, h, n = 48, 36, 40
+    frames = _frames(w, h, n, 700 + window)
+    params = (True, window, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+    want = _oracle_callbacks(frames, (True, window, 5.0, 0, 0))
+    a = ComputeState(*params)
+    try:
+        assert np.array_equal(a.frame_callback_batch(w, h, frames), want)
+        start = a.start_texture()
+    finally:
+        a.close()
+    for t0 in (7, 22):
+        b = ComputeState(*params)
+        try:
+            b.resume(w, h, start, frames[t0 - 3:t0], t0)
+            got = np.concatenate([b.frame_callback_batch(w, h, frames[t0:t0 + 12]),
+                                  np.stack([frame_callback(w, h, f, b) for f in frames[t0 + 12:]])])
+            assert np.array_equal(got, want[t0:]), (t0, np.argwhere(got != want[t0:])[:4])
+        finally:
+            b.close()
+
+
 def test_resume_rejects_bad_arguments():
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter
     from dips_amd._lib import DipsError
@@ -318,12 +374,6 @@ def test_resume_rejects_bad_arguments():
             cs.resume(w, h, f[0], f[:2], 9)  # halo must be 3 frames
     finally:
         cs.close()
-    cs3 = ComputeState(False, 3, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
-    try:
-        with pytest.raises(DipsError):
-            cs3.resume(w, h, f[0], f[:3], 9)  # window 3: not on the batch path
-    finally:
-        cs3.close()
 
 
 def test_handles_on_concurrent_threads(monkeypatch):
