@@ -185,45 +185,65 @@ hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, u
 }
 
 // The ring texel of compute_main for a whole batch of frames (W > 1, steady
-// state): gray q(filtered intensity), the same value compat_main stores into
-// the newest slot (dips_shader.wgsl:187).  blockIdx.z = frame.
-template <int SIDE>
-__global__ __launch_bounds__(256) void compat_filter_frames_kernel(const uint8_t* __restrict__ frames,
+// state): gray q(filtered intensity), the value compat_main stores into the
+// newest slot (dips_shader.wgsl:187).  q is non-decreasing, so q of the k-th
+// smallest intensity is the k-th smallest q: the tile holds q(I) and the
+// networks run on bytes, two windows per instruction (u16x2 halves,
+// window_kth_quad).  A workgroup covers 32x16 pixels; each thread filters
+// columns tx and tx + 16 of rows 2ty and 2ty + 1.  blockIdx.z = frame.
+constexpr int kFilterW = 32;
+
+template <int WIN>
+__global__ __launch_bounds__(128) void compat_filter_frames_kernel(const uint8_t* __restrict__ frames,
                                                                    uint8_t* __restrict__ dst, uint32_t w, uint32_t h,
-                                                                   int32_t window, uint32_t chroma) {
-    constexpr int R = kRows<SIDE>;
-    __shared__ float tile[kLds][kLds];
+                                                                   uint32_t chroma) {
+    constexpr int SIDE = 2 * (WIN / 2), KK = window_rank(WIN);
+    constexpr int LW = kFilterW + SIDE, LH = kTile + SIDE;
+    __shared__ uint32_t tile[LH][LW];
     const uint64_t fo = (uint64_t)blockIdx.z * w * h * 4u;
-    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
-    const uint32_t yb = blockIdx.y * kTile + threadIdx.y * R;
-    float fi[R] = {};
-    if (window_rank(window) >= 0) {
-        stage_tile<kTile * kTile / R>(tile, frames + fo, w, h, SIDE / 2, chroma);
+    const uint32_t tx = threadIdx.x, ty = threadIdx.y;
+    uint32_t o0 = 0, o1 = 0;  // q of rows 2ty, 2ty + 1; column tx low, tx + 16 high
+    if constexpr (KK >= 0) {
+        const int ox = (int)(blockIdx.x * kFilterW) - SIDE / 2;
+        const int oy = (int)(blockIdx.y * kTile) - SIDE / 2;
+        for (int idx = ty * kTile + tx; idx < LH * LW; idx += kTile * kTile / 2) {
+            const int r = idx / LW, c = idx - r * LW;
+            const int gx = ox + c, gy = oy + r;
+            uint32_t q = 0;  // out-of-frame texels are 0.0 (dips_shader.wgsl:135-136)
+            if (gx >= 0 && gy >= 0 && gx < (int)w && gy < (int)h)
+                q = unorm_store(texel_intensity(frames + fo, (uint64_t)gy * w + gx, chroma));
+            tile[r][c] = q;
+        }
         __syncthreads();
-        window_select2<SIDE>(tile, window, threadIdx.y * R, fi[0], fi[1]);
+        wnet::window_kth_quad<SIDE, KK, LW>(tile, 2 * ty, tx, kTile, o0, o1);
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t y = yb + r;
-        if (x >= w || y >= h) continue;
-        const uint32_t q = unorm_store(fi[r]);
-        *reinterpret_cast<uint32_t*>(dst + fo + 4 * ((uint64_t)y * w + x)) = q | (q << 8) | (q << 16) | (255u << 24);
+    for (int r = 0; r < 2; ++r) {
+        const uint32_t y = blockIdx.y * kTile + 2 * ty + r;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t x = blockIdx.x * kFilterW + tx + c * kTile;
+            if (x >= w || y >= h) continue;
+            const uint32_t q = ((r ? o1 : o0) >> (16 * c)) & 0xFFu;
+            *reinterpret_cast<uint32_t*>(dst + fo + 4 * ((uint64_t)y * w + x)) = q | (q << 8) | (q << 16) | (255u << 24);
+        }
     }
 }
 
 hipError_t launch_compat_filter_frames(const uint8_t* frames, uint8_t* dst, uint32_t width, uint32_t height,
                                        uint32_t n, int32_t window, uint32_t chroma, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    if (window < 2 || window > 2 * kMaxHalo + 1 || n > 65535u) return hipErrorInvalidValue;
-    dim3 grid((width + kTile - 1) / kTile, (height + kTile - 1) / kTile, n);
-    switch (window / 2) {
-#define DIPS_SIDE(H)                                                                                                \
-    case H:                                                                                                         \
-        hipLaunchKernelGGL(compat_filter_frames_kernel<2 * H>, grid, dim3(kTile, kTile / 2), 0, s, frames, dst, width, \
-                           height, window, chroma);                                                                 \
+    if (n > 65535u) return hipErrorInvalidValue;
+    dim3 grid((width + kFilterW - 1) / kFilterW, (height + kTile - 1) / kTile, n);
+    switch (window) {
+#define DIPS_WIN(W)                                                                                                \
+    case W:                                                                                                        \
+        hipLaunchKernelGGL(compat_filter_frames_kernel<W>, grid, dim3(kTile, kTile / 2), 0, s, frames, dst, width, \
+                           height, chroma);                                                                        \
         break;
-        DIPS_SIDE(1) DIPS_SIDE(2) DIPS_SIDE(3) DIPS_SIDE(4) DIPS_SIDE(5)
-#undef DIPS_SIDE
+        DIPS_WIN(2) DIPS_WIN(3) DIPS_WIN(4) DIPS_WIN(5) DIPS_WIN(6) DIPS_WIN(7) DIPS_WIN(8) DIPS_WIN(9) DIPS_WIN(10)
+        DIPS_WIN(11)
+#undef DIPS_WIN
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

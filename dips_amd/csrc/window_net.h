@@ -68,15 +68,26 @@ struct NetHolder {
     static constexpr Network<N> net{};
 };
 
-template <int A, int B>
-__device__ __forceinline__ void cmpx(uint32_t* v) {
-    const uint32_t a = v[A], b = v[B];
-    v[A] = a < b ? a : b;
-    v[B] = a < b ? b : a;
+// Element types of the networks: u32 (f32 bit patterns, one window per
+// value) and u16x2 (two quantised windows per value, v_pk_min/max_u16).
+typedef unsigned short pk16 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t vmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t vmax(uint32_t a, uint32_t b) { return a < b ? b : a; }
+__device__ __forceinline__ pk16 vmin(pk16 a, pk16 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ pk16 vmax(pk16 a, pk16 b) { return __builtin_elementwise_max(a, b); }
+template <typename T> __device__ __forceinline__ T all_ones();
+template <> __device__ __forceinline__ uint32_t all_ones<uint32_t>() { return 0xFFFFFFFFu; }
+template <> __device__ __forceinline__ pk16 all_ones<pk16>() { return pk16{0xFFFF, 0xFFFF}; }
+
+template <int A, int B, typename T>
+__device__ __forceinline__ void cmpx(T* v) {
+    const T a = v[A], b = v[B];
+    v[A] = vmin(a, b);
+    v[B] = vmax(a, b);
 }
 
-template <int N, size_t... I>
-__device__ __forceinline__ void run_network(uint32_t* v, std::index_sequence<I...>) {
+template <int N, typename T, size_t... I>
+__device__ __forceinline__ void run_network(T* v, std::index_sequence<I...>) {
     (cmpx<NetHolder<N>::net.lo[I], NetHolder<N>::net.hi[I]>(v), ...);
 }
 
@@ -105,23 +116,23 @@ __device__ __forceinline__ float window_kth(const float (*tile)[LDS], int ty, in
 // from R), so only S[KK - SIDE .. KK] is needed and the compiler keeps only
 // the comparators feeding those.  Side 10: ~455 comparators per pixel
 // instead of ~890.
-template <int M, int R, int KK>
-__device__ __forceinline__ uint32_t kth_of_two(const uint32_t* s, const uint32_t* r) {
+template <int M, int R, int KK, typename T>
+__device__ __forceinline__ T kth_of_two(const T* s, const T* r) {
     constexpr int lo = KK + 1 - M > 0 ? KK + 1 - M : 0;
     constexpr int hi = R < KK + 1 ? R : KK + 1;
-    uint32_t best = 0xFFFFFFFFu;
+    T best = all_ones<T>();
 #pragma unroll
     for (int i = lo; i <= hi; ++i) {
         const int si = KK - i < 0 ? 0 : KK - i;
         const int ri = i - 1 < 0 ? 0 : i - 1;
-        uint32_t term;
+        T term;
         if (i == 0)
             term = s[si];                            // nothing from R
         else if (KK - i < 0)
             term = r[ri];                            // all KK + 1 from R
         else
-            term = s[si] > r[ri] ? s[si] : r[ri];
-        best = term < best ? term : best;
+            term = vmax(s[si], r[ri]);
+        best = vmin(term, best);
     }
     return best;
 }
@@ -146,6 +157,36 @@ __device__ __forceinline__ void window_kth_pair(const float (*tile)[LDS], int ty
     run_network<SIDE>(r1, std::make_index_sequence<NetHolder<SIDE>::net.count>{});
     out0 = __uint_as_float(kth_of_two<m, SIDE, KK>(s, r0));
     out1 = __uint_as_float(kth_of_two<m, SIDE, KK>(s, r1));
+}
+
+// Four windows at once on quantised values: tile holds u8 values (one per
+// u32), the windows at tile rows [ty, ty + SIDE) and [ty + 1, ty + SIDE + 1)
+// for columns tx and tx + D share one pass of the same networks, column tx
+// in the low and column tx + D in the high u16 half.  out0 / out1: the two
+// rows' results, packed the same way.
+template <int SIDE, int KK, int LDSW>
+__device__ __forceinline__ void window_kth_quad(const uint32_t (*tile)[LDSW], int ty, int tx, int D, uint32_t& out0,
+                                                uint32_t& out1) {
+    constexpr int m = SIDE * (SIDE - 1);
+    static_assert(KK >= 0 && KK < SIDE * SIDE, "rank outside the window");
+    auto pk = [&](int r, int c) {
+        return __builtin_bit_cast(pk16, tile[r][tx + c] | (tile[r][tx + D + c] << 16));
+    };
+    pk16 s[m], r0[SIDE], r1[SIDE];
+#pragma unroll
+    for (int c = 0; c < SIDE; ++c) {
+        r0[c] = pk(ty, c);
+        r1[c] = pk(ty + SIDE, c);
+    }
+#pragma unroll
+    for (int r = 0; r < SIDE - 1; ++r)
+#pragma unroll
+        for (int c = 0; c < SIDE; ++c) s[r * SIDE + c] = pk(ty + 1 + r, c);
+    run_network<m>(s, std::make_index_sequence<NetHolder<m>::net.count>{});
+    run_network<SIDE>(r0, std::make_index_sequence<NetHolder<SIDE>::net.count>{});
+    run_network<SIDE>(r1, std::make_index_sequence<NetHolder<SIDE>::net.count>{});
+    out0 = __builtin_bit_cast(uint32_t, kth_of_two<m, SIDE, KK>(s, r0));
+    out1 = __builtin_bit_cast(uint32_t, kth_of_two<m, SIDE, KK>(s, r1));
 }
 
 }  // namespace wnet

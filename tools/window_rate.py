@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """window_rate.py -- dips ComputeState with the spatial median (SURVEY.md s8f
 next-3: W in 1..11) over HBM-resident 4K RGBA8 frames
-(frame_callback_batch_device; W > 1 runs frame by frame), frames/s by wall
+(frame_callback_batch_device; W > 1 through compat_filter_frames + the
+batch kernel), frames/s by wall
 clock after a warm-up.  One JSON line per window size."""
 from __future__ import annotations
 
