@@ -61,6 +61,8 @@ struct dips_alt_handle {
     bool meta_pending[2] = {false, false};
     int meta_turn = 0;
     int occupancy = 0;
+    int occupancy_pre = 0;  // the prefiltered (W > 1) batch kernel
+    DevBuf filtered;        // W > 1 batch: filtered f32 intensities of a chunk of frames (+ the one before)
 
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
     std::vector<hipEvent_t> ev_free;
@@ -150,19 +152,32 @@ const uint8_t* slot_at(const dips_alt_handle* h, const uint8_t* frames, uint64_t
     return h->slots[k].as<uint8_t>();
 }
 
+// W > 1, N = 2: the same batch kernel on prefiltered intensities
+// (launch_alt_filter_frames), so each frame is filtered once instead of once
+// per slot and frame.
+bool window_eligible(const dips_alt_handle* h, const uint8_t* frames, const uint8_t* out) {
+    return h->p.num_textures == 2 && h->p.window_size > 1 && !(h->p.flags & DIPS_FLAG_FORCE_GENERIC) &&
+           h->n_px() % 4u == 0 && ((uintptr_t)frames & 3u) == 0 && ((uintptr_t)out & 15u) == 0;
+}
+
+// prev0 / prefiltered: frames and prev0 hold f32 intensities (chroma -1
+// kernel); otherwise prev0 = the slot of the frame before frames[0].
 dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags, uint8_t* out,
-                     hipStream_t s) {
+                     hipStream_t s, const uint8_t* prev0 = nullptr) {
+    const bool pre = prev0 != nullptr;
+    const int chroma = pre ? -1 : (int)h->p.chroma_filter;
     const bool fast = dips::alt_fast_epilogue_ok(h->p.filter_type, h->p.sigmoid_horizontal_scalar);
-    const void* k = dips::alt_batch_kernel_ptr((int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0, fast);
+    const void* k = dips::alt_batch_kernel_ptr(chroma, (int)h->p.filter_type, h->p.colorize != 0, fast);
     if (!k) return fail(h, DIPS_ERR_INVALID, "no batch kernel for these parameters");
-    if (h->occupancy == 0) {
+    int& occ = pre ? h->occupancy_pre : h->occupancy;
+    if (occ == 0) {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess || nb < 1) nb = 1;
-        h->occupancy = nb;
+        occ = nb;
     }
     const uint64_t n_vec = h->n_px() / 4u;
     const uint64_t n_tiles = (n_vec + 64u * dips::kUnrollAlt - 1) / (64u * dips::kUnrollAlt);
-    const uint64_t resident = (uint64_t)h->occupancy * 4u * (uint64_t)h->cu_count;
+    const uint64_t resident = (uint64_t)occ * 4u * (uint64_t)h->cu_count;
     // chunks of >= 16 frames; enough (tile, chunk) items to fill the chip
     uint64_t n_chunks = (resident + n_tiles - 1) / n_tiles;
     n_chunks = std::min<uint64_t>(n_chunks, (n + 15u) / 16u);
@@ -209,7 +224,7 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
 
     dips::AltBatchArgs a{};
     a.frames = frames;
-    a.prev0 = h->slots[(h->sent + 1u) % 2u].as<uint8_t>();
+    a.prev0 = pre ? prev0 : h->slots[(h->sent + 1u) % 2u].as<uint8_t>();
     a.snap_in = h->snap[h->cur].as<uint8_t>();
     a.snap_out = h->snap[1 - h->cur].as<uint8_t>();
     a.out = out;
@@ -234,14 +249,42 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
         if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
         ALT_HIP(h, hipEventRecord(e0, s));
     }
-    ALT_HIP(h, dips::launch_alt_batch(a, (int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0,
-                                      fast, blocks, s));
+    ALT_HIP(h, dips::launch_alt_batch(a, chroma, (int)h->p.filter_type, h->p.colorize != 0, fast, blocks, s));
     if (timing) {
         ALT_HIP(h, hipEventRecord(e1, s));
         h->ev_pending.emplace_back(e0, e1);
     }
     ALT_HIP(h, hipEventRecord(h->meta_free, s));  // the next table upload waits for this kernel
     if (last >= 0) h->cur = 1 - h->cur;
+    return DIPS_OK;
+}
+
+// W > 1, N = 2: filter a chunk of frames (plus the one before it) into
+// f32 intensities, then the batch kernel over them; ~1 GiB of scratch.
+dips_status run_prefiltered(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags,
+                            uint8_t* out, hipStream_t s) {
+    const size_t fb = h->frame_bytes();
+    uint64_t g = std::max<uint64_t>(16u, (1ull << 30) / fb);
+    if (const char* e = std::getenv("DIPS_WINDOW_BATCH_FRAMES")) g = std::max(1ul, std::strtoul(e, nullptr, 10));
+    g = std::min<uint64_t>(std::min<uint64_t>(g, n), 65534u);
+    ALT_HIP(h, h->filtered.ensure((g + 1) * fb));
+    float* G = h->filtered.as<float>();
+    const uint8_t* G8 = h->filtered.as<uint8_t>();
+    const int32_t win = h->p.window_size;
+    const uint32_t ch = h->p.chroma_filter;
+    for (uint32_t s0 = 0; s0 < n; s0 += (uint32_t)g) {
+        const uint32_t gn = (uint32_t)std::min<uint64_t>(g, n - s0);
+        if (s0 == 0) {  // the frame before the batch: slot (sent + 1) mod 2 (zeros before the first frame)
+            ALT_HIP(h, dips::launch_alt_filter_frames(h->slots[(h->sent + 1u) % 2u].as<uint8_t>(), G, h->width,
+                                                      h->height, 1, win, ch, s));
+            ALT_HIP(h, dips::launch_alt_filter_frames(frames, G + h->n_px(), h->width, h->height, gn, win, ch, s));
+        } else {
+            ALT_HIP(h, dips::launch_alt_filter_frames(frames + (size_t)(s0 - 1) * fb, G, h->width, h->height, gn + 1,
+                                                      win, ch, s));
+        }
+        dips_status st = run_fast(h, G8 + fb, gn, flags ? flags + s0 : nullptr, out + (size_t)s0 * fb, s, G8);
+        if (st != DIPS_OK) return st;
+    }
     return DIPS_OK;
 }
 
@@ -271,8 +314,9 @@ dips_status run_generic(dips_alt_handle* h, const uint8_t* frames, uint32_t n, c
 dips_status send_frames_device(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags,
                                uint8_t* out, hipStream_t s) {
     if (n == 0) return DIPS_OK;
-    dips_status st = fast_eligible(h, frames, out) ? run_fast(h, frames, n, flags, out, s)
-                                                   : run_generic(h, frames, n, flags, out, s);
+    dips_status st = fast_eligible(h, frames, out)     ? run_fast(h, frames, n, flags, out, s)
+                     : window_eligible(h, frames, out) ? run_prefiltered(h, frames, n, flags, out, s)
+                                                       : run_generic(h, frames, n, flags, out, s);
     if (st != DIPS_OK) return st;
     // the texture slots now hold the batch's last N frames (write_texture, mod.rs:510-521)
     const uint64_t N = h->p.num_textures;
@@ -387,6 +431,7 @@ void dips_alt_destroy(dips_alt_handle* h) {
     for (auto& mp : h->meta_pin) mp.release();
     for (auto& s : h->slots) s.release();
     for (auto& s : h->snap) s.release();
+    h->filtered.release();
     h->out1.release();
     h->pipe.release();
     h->pieces.release();

@@ -180,6 +180,20 @@ struct AltTile {
     uint32_t voff[U];  // byte offset of the lane's vec u inside a frame
 };
 
+// I2s of a vec's four pixels: from RGBA8 bytes (CH = chroma filter 0..3), or
+// CH = kAltPrefiltered: the vec already holds the four spatially filtered
+// intensities as f32 I2s (alt_filter_frames_kernel, W > 1).
+constexpr int kAltPrefiltered = -1;
+template <int CH>
+__device__ __forceinline__ void alt_derive(const uint32_t (&d)[4], St2& s) {
+    if constexpr (CH == kAltPrefiltered) {
+        s.i[0] = f32x2{__uint_as_float(d[0]), __uint_as_float(d[1])};
+        s.i[1] = f32x2{__uint_as_float(d[2]), __uint_as_float(d[3])};
+    } else {
+        derive_v2<4, CH>(d, s);
+    }
+}
+
 template <int CH, int U>
 __device__ __forceinline__ void alt_intensity(const uint8_t* frame, uint32_t fb, const AltTile<U>& tl,
                                               f32x2 (&dst)[U][2]) {
@@ -189,7 +203,7 @@ __device__ __forceinline__ void alt_intensity(const uint8_t* frame, uint32_t fb,
         uint32_t d[4];
         load_vec<4>(r, tl.voff[u], d);
         St2 s;
-        derive_v2<4, CH>(d, s);
+        alt_derive<CH>(d, s);
         dst[u][0] = s.i[0];
         dst[u][1] = s.i[1];
     }
@@ -271,7 +285,7 @@ __global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             St2 n;
-            derive_v2<4, CH>(d[u], n);
+            alt_derive<CH>(d[u], n);
             float med[4];
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
@@ -339,6 +353,33 @@ hipError_t launch_frame_n(const AltArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// The spatially filtered intensity of every pixel of n frames (dips_alt
+// spatial_median_filter, W > 1, pre_compute_shader.wgsl:134-186) as f32 I2s
+// = I * 2^23 (exact), laid out like the RGBA8 frame (4 B/px), for the
+// prefiltered batch kernel.  The temporal min and the epilogue act on these
+// f32 values, so unlike the dips ring (compat_filter_frames_kernel) they are
+// not quantised.  blockIdx.z = frame.
+template <int WIN>
+__global__ __launch_bounds__(128) void alt_filter_frames_kernel(const uint8_t* __restrict__ frames,
+                                                                float* __restrict__ dst, uint32_t w, uint32_t h,
+                                                                uint32_t chroma) {
+    constexpr int SIDE = 2 * (WIN / 2), KK = alt_window_rank(WIN);
+    __shared__ float tile[kLds][kLds];
+    const uint64_t po = (uint64_t)blockIdx.z * w * h;
+    float f0 = 0.0f, f1 = 0.0f;
+    if constexpr (KK >= 0) {
+        alt_stage_tile<kTile * kTile / 2>(tile, frames + 4 * po, w, h, SIDE / 2, chroma, 0);
+        __syncthreads();
+        wnet::window_kth_pair<SIDE, KK, kLds>(tile, 2 * threadIdx.y, threadIdx.x, f0, f1);
+    }
+    const uint32_t x = blockIdx.x * kTile + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const uint32_t y = blockIdx.y * kTile + 2 * threadIdx.y + r;
+        if (x < w && y < h) dst[po + (uint64_t)y * w + x] = (r ? f1 : f0) * 8388608.0f;
+    }
+}
+
 template <int CH, int FILT, bool FAST>
 const void* batch_ptr_fc(bool colorize) {
     return colorize ? reinterpret_cast<const void*>(&alt_batch_kernel<CH, FILT, 1, FAST, kUnrollAlt>)
@@ -374,6 +415,7 @@ const void* alt_batch_kernel_ptr(int chroma, int filter, bool colorize, bool fas
         case 1: return batch_ptr_c<1>(filter, colorize, fast);
         case 2: return batch_ptr_c<2>(filter, colorize, fast);
         case 3: return batch_ptr_c<3>(filter, colorize, fast);
+        case kAltPrefiltered: return batch_ptr_c<kAltPrefiltered>(filter, colorize, fast);
         default: return nullptr;
     }
 }
@@ -385,6 +427,25 @@ hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool 
     AltBatchArgs args = a;
     void* params[] = {&args};
     return hipLaunchKernel(k, dim3(blocks), dim3(256), params, 0, s);
+}
+
+hipError_t launch_alt_filter_frames(const uint8_t* frames, float* dst, uint32_t width, uint32_t height, uint32_t n,
+                                   int32_t window, uint32_t chroma, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (n > 65535u) return hipErrorInvalidValue;
+    dim3 grid((width + kTile - 1) / kTile, (height + kTile - 1) / kTile, n);
+    switch (window) {
+#define DIPS_WIN(W)                                                                                             \
+    case W:                                                                                                     \
+        hipLaunchKernelGGL(alt_filter_frames_kernel<W>, grid, dim3(kTile, kTile / 2), 0, s, frames, dst, width, \
+                           height, chroma);                                                                     \
+        break;
+        DIPS_WIN(2) DIPS_WIN(3) DIPS_WIN(4) DIPS_WIN(5) DIPS_WIN(6) DIPS_WIN(7) DIPS_WIN(8) DIPS_WIN(9) DIPS_WIN(10)
+        DIPS_WIN(11)
+#undef DIPS_WIN
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 // Ring-slot refresh after a batch (write_texture, dips_alt mod.rs:510-521):

@@ -137,7 +137,12 @@ struct CopyFramesArgs {
 };
 hipError_t launch_copy_frames(const CopyFramesArgs& a, uint32_t count, hipStream_t s);
 // fast: the branch-free epilogue (alt_fast_epilogue_ok)
+// chroma -1: frames are prefiltered f32 I2s intensities (launch_alt_filter_frames)
 const void* alt_batch_kernel_ptr(int chroma, int filter, bool colorize, bool fast);
+// W > 1: the filtered intensity (I * 2^23, f32) of each pixel of n RGBA8
+// frames, one f32 per pixel (the layout the batch kernel reads with chroma -1)
+hipError_t launch_alt_filter_frames(const uint8_t* frames, float* dst, uint32_t width, uint32_t height, uint32_t n,
+                                   int32_t window, uint32_t chroma, hipStream_t s);
 hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool colorize, bool fast, uint32_t blocks,
                             hipStream_t s);
 // the fast epilogue's preconditions (epilogue_fast.h): sigmoid with a scalar

@@ -81,9 +81,28 @@ def main():
         name = f"compute_state_{idx:02d}.npz"
         np.savez_compressed(os.path.join(HERE, name), frames=frames, outputs=np.stack(outs))
         manifest["compute_state"].append({"file": name, "params": list(params)})
+    # dips_alt run loop (run_dips_on_file, dips_alt/src/lib.rs:588-683):
+    # (num_textures, colorize, window, scalar, filter, chroma), refresh markers
+    manifest["alt"] = []
+    arng = np.random.default_rng(20261016)
+    alt_cases = [(2, True, 1, 5.0, 0, 0), (2, False, 1, 3.0, 1, 2), (2, True, 4, 5.0, 1, 0),
+                 (3, True, 1, 5.0, 0, 1), (2, False, 7, 0.7, 0, 3), (1, True, 2, 5.0, 0, 0)]
+    for idx, (n_tex, col, win, k, filt, chroma) in enumerate(alt_cases):
+        w, h = 24, 14
+        frames = arng.integers(0, 256, (10, h, w, 4), dtype=np.uint8)
+        frames[6] = frames[5]
+        markers = [5] if idx % 2 == 0 else []
+        a = nr.AltCompute(n_tex, w, h, col, win, k, filt, chroma).run(frames, markers)
+        b = oracle.AltCompute(n_tex, w, h, col, win, k, filt, chroma).run(frames, markers)
+        assert np.array_equal(a, b)
+        name = f"alt_{idx:02d}.npz"
+        np.savez_compressed(os.path.join(HERE, name), frames=frames, outputs=a)
+        manifest["alt"].append({"file": name, "num_textures": n_tex, "colorize": col, "window": win,
+                                "scalar": k, "filter": filt, "chroma": chroma, "markers": markers})
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
-    print(f"wrote {len(manifest['series'])} series + {len(manifest['compute_state'])} ComputeState fixtures")
+    print(f"wrote {len(manifest['series'])} series + {len(manifest['compute_state'])} ComputeState + "
+          f"{len(manifest['alt'])} dips_alt fixtures")
 
 
 if __name__ == "__main__":

@@ -116,6 +116,56 @@ def test_run_pieces_equal_one_call(n_tex, window):
         assert np.array_equal(got, want), (pieces, np.argwhere(got != want)[:4])
 
 
+@pytest.mark.parametrize("scratch_frames", [None, 5])
+@pytest.mark.parametrize("window", list(range(2, 12)))
+def test_run_window_batch_matches_oracle(window, scratch_frames, monkeypatch):
+    """N = 2, W > 1 through the prefiltered batch path (alt_filter_frames_kernel
+    + the batch kernel on f32 intensities): every window 2..11, refresh
+    markers (a snapshot at a chunk's first frame included), split calls and a
+    5-frame scratch (several filter + batch rounds per call)."""
+    from dips_amd.alt import ChromaFilter, DiPsRunner
+    if scratch_frames is not None:
+        monkeypatch.setenv("DIPS_WINDOW_BATCH_FRAMES", str(scratch_frames))
+    for (w, h), pieces, chroma in [((40, 17), [30], 0), ((64, 48), [9, 4, 17], 2)]:
+        frames = _frames(w, h, 30, 40 + window)
+        frames[20] = frames[19]
+        markers = [4, 11, 12, 26]
+        want = oracle.AltCompute(2, w, h, True, window, 5.0, 0, chroma).run(frames, markers)
+        r = DiPsRunner(h, w, _props(True, window, 5.0, 0, chroma), markers)
+        try:
+            outs, s = [], 0
+            for k in pieces:
+                outs.append(r(frames[s:s + k]))
+                s += k
+        finally:
+            r.close()
+        got = np.concatenate(outs)
+        assert np.array_equal(got, want), ((w, h), pieces, np.argwhere(got != want)[:4])
+
+
+@pytest.mark.parametrize("window", [2, 5, 11])
+def test_window_batch_equals_per_frame_kernel(window):
+    """W > 1: the prefiltered batch path and the per-frame kernel agree over a
+    clip cut into several frame chunks (chunk starts rebuild the previous
+    intensities and snapshots from the filtered buffer)."""
+    from dips_amd.alt import DiPsCompute
+    w, h = 64, 32
+    frames = _frames(w, h, 150, 19 + window)
+    flags = np.zeros(150, bool)
+    flags[[0, 2, 40, 41, 97, 149]] = True
+    outs = []
+    for generic in (False, True):
+        c = DiPsCompute(2, h, w, _props(False, window, 3.0, 1, 0), force_generic=generic)
+        try:
+            outs.append(c.send_frames(frames[:70], flags[:70]))
+            outs.append(c.send_frames(frames[70:], flags[70:]))
+            outs.append(c.snapshot_texture())
+        finally:
+            c.close()
+    for a, b in zip(outs[:3], outs[3:]):
+        assert np.array_equal(a, b)
+
+
 def test_batch_kernel_equals_per_frame_kernel():
     """The N = 2 batch kernel and the generic per-frame kernel agree on a
     clip long enough to be cut into several frame chunks (the chunk start

@@ -222,6 +222,12 @@ def test_golden_manifest_and_fixtures():
                 assert o is None
             else:
                 assert np.array_equal(o, outs[k - 3]), (case["file"], k)
+    for case in manifest["alt"]:
+        z = _load_golden(case["file"])
+        fr = z["frames"]
+        got = oracle.AltCompute(case["num_textures"], fr.shape[2], fr.shape[1], case["colorize"], case["window"],
+                                case["scalar"], case["filter"], case["chroma"]).run(fr, case["markers"])
+        assert np.array_equal(got, z["outputs"]), case["file"]
 
 
 def test_v2_intensity_identity():
