@@ -4,18 +4,24 @@
 //                      the start texture S = q(upper median of the four
 //                      spatially filtered first frames), run once.
 //   compat_main:       compute_main (dips_shader.wgsl:172-240) for one frame:
-//                      filter the newest ring slot (quantised on store, A4),
-//                      upper median of the four slots, diff against S,
+//                      store the newest slot's filtered texel (quantised,
+//                      A4), upper median of the four slots, diff against S,
 //                      filter / sensitivity / colour epilogue, RGBA8 out.
+//   compat_filter_frames: the spatial filter (W > 1) of one or many frames
+//                      into gray ring texels, ahead of compat_main or the
+//                      batch kernel.
 //
-// Both cover 16x16 pixel tiles.  W = 1: one thread per pixel.  For a spatial
-// window W > 1 the workgroup first stages the intensity of its (16 + 2h)^2
-// neighbourhood in LDS (out-of-frame texels are 0.0, dips_shader.wgsl:135-136)
-// and each of its 16x8 threads selects the order statistic of two vertically
-// adjacent windows through register sorting networks (window_net.h).  Kernels
-// are instantiated per window side, so the W = 1 launches keep their small
-// register budget.  The reference filters the newest slot in place while neighbours read it (a
-// data race); here the filter reads a separate copy (`raw`).
+// compat_precompute and compat_main cover 16x16 pixel tiles.  W = 1: one
+// thread per pixel.  For a spatial window W > 1 compat_precompute stages the
+// intensity of its (16 + 2h)^2 neighbourhood in LDS (out-of-frame texels are
+// 0.0, dips_shader.wgsl:135-136) and each of its 16x8 threads selects the
+// order statistic of two vertically adjacent windows through register
+// sorting networks (window_net.h); compat_filter_frames does the same on
+// quantised bytes, four windows per network pass (32x16 tiles).  Kernels are
+// instantiated per window, so the W = 1 launches keep their small register
+// budget.  The reference filters the newest slot in place while neighbours
+// read it (a data race); here the filter reads the slot and
+// writes a separate buffer (`raw`), which compat_main then stores.
 #include "dips_math.h"
 #include "dips_kernels.h"
 #include "window_net.h"
@@ -144,27 +150,18 @@ __device__ __forceinline__ void compat_finish(const CompatArgs& a, uint64_t p, f
     *reinterpret_cast<uint32_t*>(a.out + 4 * p) = visual_epilogue(diff, a.filter, a.sensitivity, a.colorize != 0u);
 }
 
-template <int SIDE>
+// compute_main for one frame once `raw` holds the newest slot's filter
+// input: the frame itself (W = 1, vec4(I, I, I, 1), dips_shader.wgsl:123-126)
+// or, for W > 1, its filtered ring texel from compat_filter_frames_kernel
+// (gray q, whose intensity is u(q) under every chroma filter, so the store
+// below writes q back).  One thread per pixel.
 __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
-    constexpr int R = kRows<SIDE>;
-    __shared__ float tile[kLds][kLds];
     const uint32_t x = blockIdx.x * kTile + threadIdx.x;
-    const uint32_t yb = a.y0 + blockIdx.y * kTile + threadIdx.y * R;
+    const uint32_t y = a.y0 + blockIdx.y * kTile + threadIdx.y;
     const uint32_t yend = a.y1 ? a.y1 : a.height;
-    float fi[R] = {};
-    if constexpr (SIDE == 0) {
-        if (x >= a.width || yb >= yend) return;
-        fi[0] = texel_intensity(a.raw, (uint64_t)yb * a.width + x, a.chroma);
-    } else if (window_rank(a.window) >= 0) {
-        stage_tile<kTile * kTile / R>(tile, a.raw, a.width, a.height, SIDE / 2, a.chroma, a.y0);
-        __syncthreads();
-        window_select2<SIDE>(tile, a.window, threadIdx.y * R, fi[0], fi[1]);
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t y = yb + r;
-        if (x < a.width && y < yend) compat_finish(a, (uint64_t)y * a.width + x, fi[r]);
-    }
+    if (x >= a.width || y >= yend) return;
+    const uint64_t p = (uint64_t)y * a.width + x;
+    compat_finish(a, p, texel_intensity(a.raw, p, a.chroma));
 }
 
 // A ring slot as frame_callback leaves it for a W = 1 frame: the gray texel
@@ -265,13 +262,7 @@ hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
     dim3 grid((a.width + kTile - 1) / kTile, (yend - a.y0 + kTile - 1) / kTile);
-    switch (a.window / 2) {
-#define DIPS_SIDE(H) \
-    case H: hipLaunchKernelGGL(compat_main_kernel<2 * H>, grid, dim3(kTile, kTile / kRows<2 * H>), 0, s, a); break;
-        DIPS_SIDE(0) DIPS_SIDE(1) DIPS_SIDE(2) DIPS_SIDE(3) DIPS_SIDE(4) DIPS_SIDE(5)
-#undef DIPS_SIDE
-        default: return hipErrorInvalidValue;
-    }
+    hipLaunchKernelGGL(compat_main_kernel, grid, dim3(kTile, kTile), 0, s, a);
     return hipGetLastError();
 }
 

@@ -464,7 +464,10 @@ int dispatch_impl(dips_handle* h, uint8_t* out, size_t cap, bool device_dst) {
     if (a.window == 1) {
         a.raw = a.slots[a.newest];  // per-pixel in-place filter is race free
     } else {
-        DIPS_HIP(h, hipMemcpyAsync(h->raw.p, a.slots[a.newest], fb, hipMemcpyDeviceToDevice, h->stream));
+        // spatial_median_filter of the newest slot as it was before the
+        // dispatch (dips_shader.wgsl:120-170), stored as the gray ring texel
+        DIPS_HIP(h, dips::launch_compat_filter_frames(a.slots[a.newest], h->raw.as<uint8_t>(), h->width, h->height, 1,
+                                                      a.window, a.chroma, h->stream));
         a.raw = h->raw.as<uint8_t>();
     }
     DIPS_HIP(h, dips::launch_compat_main(a, h->stream));
