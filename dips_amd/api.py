@@ -429,6 +429,8 @@ class DiffSeriesOperator:
         rp = None
         if ref is not None:
             ref = _as_u8(ref)
+            if ref.size != frames[0].size:
+                raise ValueError("ref must have the shape of one frame")
             rp = ref.ctypes.data
         self._host.check(self._host._lib.dips_diff_series_streamed(
             self._host.ptr, w, h, frames.ctypes.data, n, rp, out.ctypes.data, int(chunk_frames)))
@@ -444,6 +446,14 @@ class DiffSeriesOperator:
         for t in (frames, series_out, ref, map_out):
             if t is not None and (not t.is_cuda or not t.is_contiguous()):
                 raise ValueError("device path needs contiguous HIP tensors")
+        import torch
+        for t in (frames, ref, map_out):
+            if t is not None and t.dtype != torch.uint8:
+                raise ValueError("frames, ref and map_out must be uint8 tensors")
+        if ref is not None and ref.numel() != h * w * int(self.fmt):
+            raise ValueError("ref must have the size of one frame")
+        if map_out is not None and tuple(map_out.shape) != tuple(frames.shape):
+            raise ValueError("map_out must have the shape of frames")
         lib = self._dev._lib
         if stream is None:
             import torch

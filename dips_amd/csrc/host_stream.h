@@ -212,6 +212,11 @@ hipError_t run_stream_pipe(StreamPipe& p, hipStream_t compute, uint64_t n, size_
     *fn_status = 0;
     hipError_t e = p.init();
     if (e != hipSuccess) return e;
+    // a previous call that ended early (HIP error, negative fn status) may
+    // have left DMAs in flight that read pin_in / write pin_out: drain both
+    // copy streams before the staging buffers are reused
+    if ((e = hipStreamSynchronize(p.up)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(p.down)) != hipSuccess) return e;
     if (chunk == 0 || chunk > n) chunk = n;
     for (int i = 0; i < 2; ++i) {
         if ((e = p.pin_in[i].ensure(ib * chunk)) != hipSuccess) return e;
@@ -244,6 +249,9 @@ hipError_t run_stream_pipe(StreamPipe& p, hipStream_t compute, uint64_t n, size_
             const int st = fn(p.dev_in[b].template as<uint8_t>(), p.dev_out[b].template as<uint8_t>(), m);
             if (st < 0) {
                 *fn_status = st;
+                // leave no DMA running on the staging buffers
+                (void)hipStreamSynchronize(p.up);
+                (void)hipStreamSynchronize(p.down);
                 return hipSuccess;
             }
             if ((e = hipEventRecord(p.computed[b], compute)) != hipSuccess) return e;

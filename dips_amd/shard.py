@@ -150,6 +150,26 @@ def start_compat_halo(local_frames: torch.Tensor, halo: torch.Tensor, group=None
     return dist.batch_isend_irecv(ops) if ops else []
 
 
+def _check_compat_shards(local_frames: torch.Tensor, t0: int, rank: int, world: int, group=None) -> None:
+    """Validate every rank's (t0, n) on every rank before any frame moves, so
+    that a bad layout raises the same error everywhere instead of leaving the
+    other ranks blocked in a send, receive or broadcast."""
+    mine = torch.tensor([t0, local_frames.shape[0]], dtype=torch.int64, device=local_frames.device)
+    if world > 1:
+        parts = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine, group=group)
+        shards = [(int(p[0]), int(p[1])) for p in parts]
+    else:
+        shards = [(int(mine[0]), int(mine[1]))]
+    if shards[0][0] != 0:
+        raise ValueError("rank 0 owns the first frames")
+    for r, (s, n) in enumerate(shards):
+        if r > 0 and s < 7:
+            raise ValueError(f"ranks after the first must start at global frame >= 7 (rank {r} starts at {s})")
+        if r + 1 < world and n < COMPAT_HALO:
+            raise ValueError("every shard of the dips-compat path needs >= 3 frames")
+
+
 def compat_sharded(local_frames: torch.Tensor, t0: int, *,
                    callback_batch: Callable[[torch.Tensor], torch.Tensor],
                    start_texture: Callable[[torch.Tensor], None],
@@ -163,10 +183,9 @@ def compat_sharded(local_frames: torch.Tensor, t0: int, *,
     resume(S, halo, t0) sets the state.  Returns this rank's outputs."""
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
+    _check_compat_shards(local_frames, t0, rank, world, group)
     works = start_compat_halo(local_frames, halo_buf, group)
     if rank == 0:
-        if t0 != 0:
-            raise ValueError("rank 0 owns the first frames")
         head = callback_batch(local_frames[:4])  # frames 0..3: passthrough, then S
         start_texture(start_buf)
     if world > 1:
@@ -176,8 +195,6 @@ def compat_sharded(local_frames: torch.Tensor, t0: int, *,
         for w in works:
             w.wait()
         return torch.cat([head, tail])
-    if t0 < 7:
-        raise ValueError("ranks after the first must start at global frame >= 7")
     for w in works:
         w.wait()
     resume(start_buf, halo_buf, t0)
@@ -241,7 +258,20 @@ def alt_sharded(local_frames: torch.Tensor, t0: int, n_total: int, flags, num_te
         w.wait()
     need, fl = alt_replay_frames(t0, flags, num_textures)
     if need:
-        replay = torch.stack([recv[g] for g in need])
+        frames = [recv[g] for g in need]
+        halo_len = t0 - max(0, t0 - num_textures)
+        if halo_len < num_textures and len(need) > halo_len:
+            # t0 < N: the single loop still has N - t0 zero (never written)
+            # slots at frame t0, evicted before frame 0's slot; the snapshot
+            # replay filled them, so push that many all-zero frames (a zero
+            # texel is what wgpu's zero-initialised slot reads as) before the
+            # halo, in the single loop's eviction order
+            zero = torch.zeros_like(local_frames[0])
+            k = len(need) - halo_len
+            pad = num_textures - halo_len
+            frames = frames[:k] + [zero] * pad + frames[k:]
+            fl = fl[:k] + [False] * pad + fl[k:]
+        replay = torch.stack(frames)
         send_frames(replay, fl)  # state only: slots and snapshot as at global frame t0
     return send_frames(local_frames, [bool(f) for f in flags[t0:t0 + local_frames.shape[0]]])
 

@@ -200,7 +200,10 @@ def _alt_worker(rank, world, port, n_total, n_tex, markers, result_q):
 
 
 @pytest.mark.parametrize("world,n_total,n_tex,markers", [(2, 20, 2, [5, 6]), (3, 31, 3, [9, 10, 22]),
-                                                        (3, 12, 2, [2, 3, 4, 5, 6, 7, 8, 9, 10, 11])])
+                                                        (3, 12, 2, [2, 3, 4, 5, 6, 7, 8, 9, 10, 11]),
+                                                        # N > t0 + 1: zero slots still live at the shard
+                                                        # start, a snapshot before it
+                                                        (2, 10, 16, []), (3, 14, 6, [1]), (2, 9, 5, [])])
 def test_alt_sharded_equals_single(world, n_total, n_tex, markers):
     """dips_alt run loop over frame ranges (the last snapshot's source frames
     and an N-frame halo replayed into a fresh DiPsCompute) gives the single
@@ -220,3 +223,42 @@ def test_alt_sharded_equals_single(world, n_total, n_tex, markers):
     frames = np.random.default_rng(31).integers(0, 256, (n_total, h, w, 4), dtype=np.uint8)
     want = oracle.AltCompute(n_tex, w, h, True, 1, 5.0, 0, 0).run(frames, markers)
     assert np.array_equal(got, want)
+
+
+def _compat_bad_worker(rank, world, port, n_total, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w, h = 8, 4
+        s, e = shard.frame_range(n_total, world, rank)
+        local = torch.zeros((e - s, h, w, 4), dtype=torch.uint8)
+        try:
+            shard.compat_sharded(local, s, callback_batch=lambda fr: fr, start_texture=lambda b: None,
+                                 resume=lambda *a: None, start_buf=torch.zeros((h, w, 4), dtype=torch.uint8),
+                                 halo_buf=torch.zeros((3, h, w, 4), dtype=torch.uint8))
+            result_q.put((rank, "no error"))
+        except ValueError as ex:
+            result_q.put((rank, str(ex)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 8), (3, 20)])
+def test_compat_sharded_bad_layout_fails_on_every_rank(world, n_total):
+    """A shard layout the dips-compat resume cannot take (a rank starting
+    before global frame 7) raises the same ValueError on every rank instead
+    of leaving the others blocked in the halo exchange."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_compat_bad_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r for r, _ in got] == list(range(world))
+    msgs = {m for _, m in got}
+    assert len(msgs) == 1 and "frame >= 7" in msgs.pop()
