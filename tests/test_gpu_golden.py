@@ -26,14 +26,21 @@ def test_series_fixture(case):
     from dips_amd import ChromaFilter, DiffSeriesOperator, Mode, PixelFormat
     z = _load(case["file"])
     fmt = {1: PixelFormat.Gray8, 3: PixelFormat.RGB8, 4: PixelFormat.RGBA8}[case["channels"]]
-    op = DiffSeriesOperator(fmt, Mode(case["mode"]), case["tau"], ChromaFilter(case["chroma"]))
-    try:
-        got, dmap = op(z["frames"], ref=z.get("ref"), want_map=True)
-    finally:
-        op.close()
-    assert np.array_equal(got.as_array(), z["out4"]), case["file"]
-    assert np.array_equal(dmap, z["dmap"]), case["file"]
-    np.testing.assert_allclose(got.si, z["si"], rtol=0, atol=1e-6)
+    # the shape picks the fast kernel (64x48) or the generic one (37x23);
+    # force_generic runs the generic kernel on the fast shapes as well, and
+    # the map / no-map launches are separate kernel instantiations
+    for generic in (False, True):
+        op = DiffSeriesOperator(fmt, Mode(case["mode"]), case["tau"], ChromaFilter(case["chroma"]),
+                                force_generic=generic)
+        try:
+            got, dmap = op(z["frames"], ref=z.get("ref"), want_map=True)
+            got_nomap, _ = op(z["frames"], ref=z.get("ref"))
+        finally:
+            op.close()
+        for g in (got, got_nomap):
+            assert np.array_equal(g.as_array(), z["out4"]), (case["file"], generic)
+            np.testing.assert_allclose(g.si, z["si"], rtol=0, atol=1e-6)
+        assert np.array_equal(dmap, z["dmap"]), (case["file"], generic)
 
 
 @pytest.mark.gpu

@@ -57,6 +57,30 @@ def test_series_matches_oracle(c, mode, shape):
         _check(got_nomap, out4, si)
 
 
+@pytest.mark.parametrize("c", [3, 4])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("chroma", [1, 3])
+@pytest.mark.parametrize("tau", [0.0, 8 / 255])
+def test_series_chroma_red_blue(c, mode, chroma, tau):
+    """series_v2_kernel<C, CH=1|3, ...> (chroma Red / Blue, dips_shader.wgsl:
+    64-72) with and without a threshold, with and without the byte map, on
+    the fast shapes, the ragged generic shapes and the generic kernel forced
+    on a fast shape -- every instantiation against the oracle."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    for (w, h), generic in [((64, 48), False), ((128, 8), False), ((37, 23), False), ((64, 48), True)]:
+        for kind in ("synth", "random"):
+            frames = _frames(c, w, h, 9, 70 + chroma, kind)
+            op = DiffSeriesOperator(PixelFormat(c), Mode(mode), tau, chroma, force_generic=generic)
+            try:
+                got, gmap = op(frames, want_map=True)
+                got_nomap, _ = op(frames)
+            finally:
+                op.close()
+            out4, si, dmap = oracle.series(frames, mode=mode, chroma=chroma, tau=tau, want_map=True)
+            _check(got, out4, si, gmap, dmap)
+            _check(got_nomap, out4, si)
+
+
 @pytest.mark.parametrize("c", [1, 3, 4])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_series_explicit_ref(c, mode):
@@ -229,7 +253,8 @@ def test_long_batch_segments_match_oracle(c, mode):
     w, h = 80, 36  # 2880 px: 2.8 RGB tiles of 1024 px, 1.4 gray tiles of 2048 px
     n = 20011 if c == 1 else 8009
     frames = _frames(c, w, h, n, 40 + c + mode, "random")
-    for chroma, tau in [(0, 8 / 255), (1, 0.0)] if c != 1 else [(0, 8 / 255), (0, 0.0)]:
+    for chroma, tau in ([(0, 8 / 255), (1, 0.0), (3, 8 / 255), (1, 8 / 255)] if c != 1
+                        else [(0, 8 / 255), (0, 0.0)]):
         op = DiffSeriesOperator(PixelFormat(c), Mode(mode), tau, chroma)
         try:
             got, gmap = op(frames, want_map=True)
@@ -266,3 +291,27 @@ def test_wave_cap_same_series(monkeypatch):
             op.close()
     assert out[0][0] > out[1][0] > out[2][0]
     assert all(np.array_equal(out[0][1], o[1]) for o in out[1:])
+
+
+def test_config0_gray8_full_clip_matches_oracle():
+    """BASELINE.json configs[0] at its full size: 640x480 gray8, the
+    300-frame synthetic clip, 'overall' mode (tau 0 and 8/255), through the
+    HIP path (host and device pointers) against the oracle, every entry and
+    the whole byte map bit-exact."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    w, h, n = 640, 480, 300
+    frames = oracle.synth(1, w, h, 0xD1B5, 0, n)
+    dev = torch.from_numpy(frames).cuda()
+    for tau in (0.0, 8 / 255):
+        out4, si, dmap = oracle.series(frames, mode=0, tau=tau, want_map=True, nthreads=8)
+        op = DiffSeriesOperator(PixelFormat.Gray8, Mode.Overall, tau)
+        try:
+            got, gmap = op(frames, want_map=True)
+            ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+            op.run_device(dev, ser)
+            torch.cuda.synchronize()
+        finally:
+            op.close()
+        _check(got, out4, si, gmap, dmap)
+        assert np.array_equal(ser.cpu().numpy().view(np.uint64), out4)

@@ -1,0 +1,110 @@
+"""The frame-range sharded series (dips_amd.shard) with the HIP operator as
+the per-rank compute: two processes on the one GPU of the box, gloo as the
+process group (RCCL refuses two ranks on one device, "Duplicate GPU
+detected"), the halo frame and the series staged through host tensors since
+gloo has no device send/recv.  Each rank runs DiffSeriesOperator.run_device
+on its shard under the bench's N > 1 wave cap (DIPS_SERIES_WAVES_PER_SIMD=4);
+the gathered series must equal one single-process launch over all frames."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+W, H, SEED = 256, 96, 0xD1B5
+TAU = 8 / 255
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _hip_compute(op):
+    """compute(frames, ref, series_out) over host tensors: upload, run the
+    HIP series kernel, download (the shard protocol's tensors stay on the
+    host for gloo)."""
+    def compute(frames, ref, series_out):
+        dev = frames.cuda()
+        rdev = ref.cuda() if ref is not None else None
+        ser = torch.zeros((frames.shape[0], 4), dtype=torch.int64, device="cuda")
+        op.run_device(dev, ser, ref=rdev)
+        torch.cuda.synchronize()
+        series_out.copy_(ser.cpu())
+    return compute
+
+
+def _worker(rank, world, port, n_total, mode, overlapped, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["DIPS_SERIES_WAVES_PER_SIMD"] = "4"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    op = None
+    try:
+        from dips_amd import DiffSeriesOperator, Mode, PixelFormat, shard
+        torch.cuda.set_device(0)
+        s, e = shard.frame_range(n_total, world, rank)
+        # this rank's frames generated on the device by the shared generator
+        op = DiffSeriesOperator(PixelFormat.RGB8, Mode(mode), TAU)
+        dev = torch.empty((e - s, H, W, 3), dtype=torch.uint8, device="cuda")
+        op.synth_device(dev, W, H, SEED, s)
+        torch.cuda.synchronize()
+        local = dev.cpu()
+        compute = _hip_compute(op)
+        if mode == 0:
+            ref = local[0].clone() if rank == 0 else torch.empty_like(local[0])
+            shard.broadcast_reference(ref)
+            full = shard.sharded_series(local, per_frame=False, n_total=n_total, compute=compute, reference=ref)
+        elif overlapped:
+            series = torch.zeros((local.shape[0], shard.SERIES_COLS), dtype=torch.int64)
+            shard.per_frame_overlapped(local, torch.empty_like(local[0]), series, compute)
+            full = shard.SeriesGather(n_total, torch.device("cpu"))(series)
+        else:
+            full = shard.sharded_series(local, per_frame=True, n_total=n_total, compute=compute)
+        if rank == 0:
+            result_q.put(full.numpy().copy())
+    finally:
+        if op is not None:
+            op.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,overlapped", [(0, False), (1, False), (1, True)])
+def test_sharded_hip_equals_single_launch(mode, overlapped):
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    world, n_total = 2, 37
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, mode, overlapped, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = q.get(timeout=300)
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    # one single-process launch over all frames (no wave cap)
+    op = DiffSeriesOperator(PixelFormat.RGB8, Mode(mode), TAU)
+    try:
+        allf = torch.empty((n_total, H, W, 3), dtype=torch.uint8, device="cuda")
+        op.synth_device(allf, W, H, SEED, 0)
+        one = torch.zeros((n_total, 4), dtype=torch.int64, device="cuda")
+        op.run_device(allf, one, ref=None if mode == 1 else allf[0])
+        torch.cuda.synchronize()
+    finally:
+        op.close()
+    want = one.cpu().numpy()
+    assert got.shape == want.shape
+    assert np.array_equal(got, want)
+    assert want[:, 0].any()  # non-trivial series

@@ -295,3 +295,24 @@ def test_v2_sj_lane_sum_rounds_exactly():
         sj = (a[:, k] * k_sj + sj.astype(np.float64)).astype(np.float32)
     want = np.abs(j[p] - j[q]).sum(axis=1)
     assert np.array_equal(np.trunc(sj).astype(np.int64), want)
+
+
+def test_tau_boundary_fixtures_straddle_tau():
+    """The *_tauedge fixtures hold pixels whose f32 |dI| is exactly f32(tau)
+    and one ulp either side: moving tau down one ulp adds the 'equal' pixels
+    to the count, moving it up one ulp drops the 'above' pixels -- so the
+    fixtures pin the strict '>' of the threshold (series_v2.hip, the gray
+    kernel and dips_oracle.c alike)."""
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        manifest = json.load(f)
+    cases = [c for c in manifest["series"] if c.get("tau_boundary")]
+    assert len(cases) == 14
+    for case in cases:
+        z = _load_golden(case["file"])
+        t = np.float32(case["tau"])
+        counts = []
+        for tau in (np.nextafter(t, np.float32(0)), t, np.nextafter(t, np.float32(1))):
+            out4, _, _ = oracle.series(z["frames"], mode=case["mode"], chroma=case["chroma"], tau=float(tau))
+            counts.append(out4[1, 2])
+        assert counts[0] > counts[1] > counts[2], (case["file"], counts)
+        assert z["out4"][1, 2] == counts[1]
