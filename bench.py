@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--check", action="store_true",
                     help="rank 0 recomputes the series of all N*F frames in one single-device launch "
                          "and requires the gathered series to equal it (functional check of the N>1 path)")
+    ap.add_argument("--no-map", action="store_true", help="skip the map_variant measurement")
+    ap.add_argument("--map-frames", type=int, default=2500,
+                    help="frames of the map_variant launch (frames + maps stay resident beside the batch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU work of the cpu_baseline sample")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -64,9 +67,28 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(frames_dev, series_dev, mode: int, tau: float, target_s: float):
-    """The oracle ('port' of the reference semantics) timed on this host's
-    cores on a bounded prefix of the same frames (per-frame cost is constant)."""
+def _time_oracle(lib, frames, mode, tau, threads, target_s, max_passes=400):
+    """Run the oracle series over `frames` on `threads` host threads until
+    about target_s seconds have been timed; returns (frames/s, passes, s, out4)."""
+    from oracle import oracle
+    passes, out4 = 0, None
+    t = time.perf_counter()
+    while True:
+        out4, _, _ = oracle.series(frames, mode=mode, tau=tau, nthreads=threads, lib=lib)
+        passes += 1
+        dt = time.perf_counter() - t
+        if dt >= target_s or passes >= max_passes:
+            break
+    return frames.shape[0] * passes / dt, passes, dt, out4
+
+
+def cpu_baseline(frames_dev, series_dev, mode: int, tau: float, target_s: float, op_gray=None):
+    """The oracle ('port' of the reference semantics; the reference itself has
+    no CPU loop) timed on this host's cores on a bounded
+    prefix of the same frames (per-frame cost is constant): all usable cores
+    (the headline baseline), the box's CPU share, and one core
+    ("1 thread and all cores"); plus configs[0] (640x480 gray8,
+    300 frames, 'overall') at one core and all cores."""
     from oracle import oracle
     try:
         path = oracle.build(native=True)
@@ -75,38 +97,59 @@ def cpu_baseline(frames_dev, series_dev, mode: int, tau: float, target_s: float)
     except Exception:  # pragma: no cover - no compiler on the box
         lib = oracle.load()
         build = "gcc -O3 -ffp-contract=off (prebuilt)"
-    threads = max(1, min(16, os.cpu_count() or 1))
-    # bounded host sample: 12 frames per thread (~3.6 GB at 4K RGB8), passed
-    # over repeatedly until about `target_s` of CPU work has been timed
-    n = min(frames_dev.shape[0], threads * 12)
+    host = _host_cpu()
+    all_threads = max(1, host["usable_cpus"] or os.cpu_count() or 1)
+    share = max(1, min(all_threads, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    # bounded host sample: enough frames for one per thread (<= 384 4K
+    # frames, 9.6 GB), passed over repeatedly until ~target_s is timed
+    n = min(frames_dev.shape[0], max(64, min(all_threads, 384)))
     sample = frames_dev[:n].cpu().numpy()
-    passes = 0
-    out4 = None
-    t = time.perf_counter()
-    while True:
-        out4, _, _ = oracle.series(sample, mode=mode, tau=tau, nthreads=threads, lib=lib)
-        passes += 1
-        dt = time.perf_counter() - t
-        if dt >= target_s or passes >= 50:
-            break
-    n_done = n * passes
+    v_all, p_all, dt_all, out4 = _time_oracle(lib, sample, mode, tau, all_threads, target_s)
     # the same sample doubles as a parity check of the timed GPU series
     gpu = series_dev[:n].cpu().numpy().view(np.uint64)
     matches = bool(np.array_equal(gpu, out4))
-    # one core as well (1 thread and all cores), a shorter sample
-    n1 = min(n, 8)
-    t1 = time.perf_counter()
-    out1, _, _ = oracle.series(sample[:n1], mode=mode, tau=tau, nthreads=1, lib=lib)
-    dt1 = time.perf_counter() - t1
-    matches = matches and bool(np.array_equal(out1, out4[:n1]))
-    return {"value": round(n_done / dt, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} frames of the same synthetic 4K RGB8 batch x {passes} passes, "
-                      f"series only (oracle/dips_oracle.c, {build}, {threads} threads over frame "
-                      f"ranges), {dt:.2f} s",
-            "single_core": {"value": round(n1 / dt1, 3), "unit": "frames/s", "cores": 1,
-                            "sample": f"first {n1} frames, one pass, {dt1:.2f} s"},
-            "host": _host_cpu(),
-            "series_matches_gpu": matches}
+    v_share, p_share, dt_share, o2 = _time_oracle(lib, sample[: min(n, 4 * share)], mode, tau, share,
+                                                  max(2.0, target_s / 4))
+    matches = matches and bool(np.array_equal(o2, out4[: o2.shape[0]]))
+    # one core: 4 frames a pass (mode 'per-frame' needs the frame before
+    # each, so the pass is the prefix), at least 2.5 s
+    v1, p1, dt1, o1 = _time_oracle(lib, sample[:4], mode, tau, 1, 2.5)
+    matches = matches and bool(np.array_equal(o1, out4[:4]))
+    # the reported baseline is the fastest thread count measured (on the
+    # GPU boxes the cgroup CPU quota makes all 256 visible CPUs slower than
+    # the box's share); every figure is kept beside it
+    all_cores = {"value": round(v_all, 3), "unit": "frames/s", "cores": all_threads,
+                 "sample": f"first {n} frames x {p_all} passes, {dt_all:.2f} s"}
+    box_share = {"value": round(v_share, 3), "unit": "frames/s", "cores": share,
+                 "sample": f"first {min(n, 4 * share)} frames x {p_share} passes, {dt_share:.2f} s"}
+    best = all_cores if v_all >= v_share else box_share
+    res = {"value": best["value"], "unit": "frames/s", "cores": best["cores"], "kind": "port",
+           "sample": f"synthetic 4K RGB8 frames of the same batch, series only (oracle/dips_oracle.c, {build}, "
+                     f"threads over frame ranges): {best['sample']}; the fastest of all usable cores "
+                     f"({all_threads} threads) and the box's share ({share} threads)",
+           "all_cores": all_cores,
+           "box_share": box_share,
+           "single_core": {"value": round(v1, 3), "unit": "frames/s", "cores": 1,
+                           "sample": f"first 4 frames x {p1} passes, {dt1:.2f} s"},
+           "host": host,
+           "series_matches_gpu": matches}
+    # configs[0]: the reference's own CPU-runnable case (BASELINE.json configs[0])
+    try:
+        c0 = oracle.synth(1, 640, 480, SEED, 0, 300, lib=lib)
+        r1, q1, d1, w1 = _time_oracle(lib, c0, 0, 0.0, 1, 2.5)
+        ra, qa, da, wa = _time_oracle(lib, c0, 0, 0.0, min(all_threads, 300), 2.5)
+        cfg0 = {"workload": "640x480 gray8 synthetic 300-frame clip, 'overall', tau=0 (BASELINE.json configs[0])",
+                "single_core": {"value": round(r1, 1), "unit": "frames/s", "cores": 1,
+                                "sample": f"300 frames x {q1} passes, {d1:.2f} s"},
+                "all_cores": {"value": round(ra, 1), "unit": "frames/s", "cores": min(all_threads, 300),
+                              "sample": f"300 frames x {qa} passes, {da:.2f} s"},
+                "threads_agree": bool(np.array_equal(w1, wa))}
+        if op_gray is not None:
+            cfg0["gpu"] = op_gray(c0, wa)
+        res["config0"] = cfg0
+    except Exception as e:  # report, never hide
+        res["config0"] = {"failed": str(e)}
+    return res
 
 
 def _host_cpu() -> dict:
@@ -124,7 +167,98 @@ def _host_cpu() -> dict:
         usable = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         usable = None
-    return {"model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"model": model, "nproc": os.cpu_count(), "usable_cpus": usable, "cgroup_cpu_quota": quota}
+
+
+def _lib_sha256() -> str:
+    """sha256 of the loaded HIP library: profiles/pmc_traffic.json is used
+    for roofline.traffic only when it was collected with this very build."""
+    import hashlib
+    from dips_amd import _lib as L
+    path = L.LIB_PATH
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def _config0_gpu(torch, frames_host, want):
+    """configs[0] on the GPU beside its CPU figures: the 300-frame 640x480
+    gray8 clip resident in HBM, 'overall', tau 0; series checked against the
+    oracle's."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    op = DiffSeriesOperator(PixelFormat.Gray8, Mode.Overall, 0.0, time_kernel=True)
+    try:
+        dev = torch.from_numpy(frames_host).cuda()
+        ser = torch.zeros((dev.shape[0], 4), dtype=torch.int64, device="cuda")
+        op.run_device(dev, ser)
+        torch.cuda.synchronize()
+        op.kernel_time(reset=True)
+        reps = 20
+        t = time.perf_counter()
+        for _ in range(reps):
+            op.run_device(dev, ser)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t) / reps
+        kms, n = op.kernel_time()
+        kms /= max(n, 1)
+        ok = bool(np.array_equal(ser.cpu().numpy().view(np.uint64), want))
+    finally:
+        op.close()
+    nb = frames_host.size
+    return {"frames_per_s": round(frames_host.shape[0] / wall, 1), "kernel_ms": round(kms, 4),
+            "kernel_GBps": round(nb / (kms / 1e3) / 1e9, 1), "series_matches_oracle": ok,
+            "note": "92 MB batch: launch-bound (a 300-frame 640x480 clip is ~0.03 ms of HBM streaming)"}
+
+
+def _map_variant(torch, op_cls, frames, n, W, H, mode_pf, tau):
+    """The north star's bit-exact output D_t = |F_t - R| materialised: the
+    MAP=true series kernel over n resident frames (read F, write D), timed by
+    the library's hipEvents; the series must equal the no-map run and the
+    maps of two frames are checked against a torch recomputation."""
+    from dips_amd import Mode, PixelFormat
+    op = op_cls(PixelFormat.RGB8, Mode.PerFrame if mode_pf else Mode.Overall, tau, time_kernel=True)
+    fb = W * H * 3
+    try:
+        fr = frames[:n]
+        dmap = torch.empty_like(fr)
+        ser_m = torch.zeros((n, 4), dtype=torch.int64, device=fr.device)
+        ser_n = torch.zeros((n, 4), dtype=torch.int64, device=fr.device)
+        op.run_device(fr, ser_m, map_out=dmap)  # warm
+        torch.cuda.synchronize()
+        op.kernel_time(reset=True)
+        steps = 3
+        t = time.perf_counter()
+        for _ in range(steps):
+            op.run_device(fr, ser_m, map_out=dmap)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t) / steps
+        each = op.kernel_times()
+        op.run_device(fr, ser_n)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(ser_m, ser_n))
+        ok = True
+        for k in (1, n - 1):
+            r = fr[k - 1] if mode_pf else fr[0]
+            want = (fr[k].to(torch.int16) - r.to(torch.int16)).abs().to(torch.uint8)
+            ok = ok and bool(torch.equal(dmap[k], want))
+        kms = float(np.median(each))
+        algo = 2 * n * fb
+        return {"kernel": f"series_v2_kernel<3,0,4,{'true' if mode_pf else 'false'},true>",
+                "frames": n, "frames_per_s": round(n / (kms / 1e3), 1), "wall_frames_per_s": round(n / wall, 1),
+                "kernel_ms_median": round(kms, 4), "launches": len(each),
+                "algorithmic_bytes_per_launch": algo, "achieved_GBps": round(algo / (kms / 1e3) / 1e9, 1),
+                "frac_of_8TBps": round(algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "bytes_note": "2*W*H*C per frame: F_t read once + D_t written once (R is the previous frame, "
+                              "already in registers)",
+                "series_equals_nomap_run": same, "map_matches_torch": ok}
+    finally:
+        op.close()
 
 
 def main():
@@ -235,13 +369,18 @@ def main():
         achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
         traffic = None
         pmc_note = None
+        lib_sha = _lib_sha256()
         if os.path.exists(args.pmc_json):
             try:
                 with open(args.pmc_json) as f:
                     pmc = json.load(f)
-                if (pmc.get("width"), pmc.get("height"), pmc.get("frames"), pmc.get("mode")) == (W, H, F, args.mode):
+                same_run = (pmc.get("width"), pmc.get("height"), pmc.get("frames"), pmc.get("mode")) == (W, H, F, args.mode)
+                if same_run and pmc.get("lib_sha256") == lib_sha:
                     traffic = pmc.get("hbm_bytes_per_launch")
                     pmc_note = pmc.get("source")
+                else:
+                    pmc_note = ("traffic null: profiles/pmc_traffic.json was collected with another build of "
+                                "libdips_hip.so or another workload")
             except Exception:
                 traffic = None
         value = world * F * args.steps / elapsed_max
@@ -268,10 +407,18 @@ def main():
             del host
         except Exception as e:  # report, never hide
             pcie = {"skipped": str(e)}
+        mapv = None
+        if world == 1 and not args.no_map:
+            try:
+                mapv = _map_variant(torch, DiffSeriesOperator, frames, min(F, args.map_frames), W, H,
+                                    mode == Mode.PerFrame, args.tau)
+            except Exception as e:  # report, never hide
+                mapv = {"skipped": str(e)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(frames, series, int(mode), args.tau, args.cpu_seconds)
+                cpu = cpu_baseline(frames, series, int(mode), args.tau, args.cpu_seconds,
+                                   op_gray=lambda fr, want: _config0_gpu(torch, fr, want))
             except Exception as e:  # report, never hide
                 cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port",
                        "sample": f"failed: {e}"}
@@ -316,9 +463,11 @@ def main():
                 "partial_bytes_per_launch": int(pbytes) * F,
                 "waves": int(waves),
                 **({"traffic_source": pmc_note} if pmc_note else {}),
+                "lib_sha256": lib_sha,
             },
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
+            "map_variant": mapv,
         }
         print(json.dumps(out), flush=True)
     op.close()

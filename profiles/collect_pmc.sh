@@ -13,7 +13,12 @@ mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o run -- \
     python3 bench.py --frames-per-gpu $F --steps 2 --warmup 1 --mode $MODE --no-cpu-baseline --no-pcie \
-    > $OUT/$c.log 2>&1
+    --map-frames 2500 > $OUT/$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
-python3 tools/pmc_to_json.py $OUT $F $MODE gpurun_out/pmc_traffic.json  # copy into profiles/ after merge-back
+PF=$([ "$MODE" = per-frame ] && echo true || echo false)
+python3 tools/pmc_to_json.py $OUT $F $MODE gpurun_out/pmc_traffic.json \
+  "series_v2_kernel<3, 0, 4, $PF, false>" && \
+python3 tools/pmc_to_json.py $OUT 2500 $MODE gpurun_out/pmc_traffic_map.json \
+  "series_v2_kernel<3, 0, 4, $PF, true>" $((3840 * 2160 * 3 * 2))
+# copy gpurun_out/pmc_traffic*.json into profiles/ after merge-back

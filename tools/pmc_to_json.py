@@ -20,6 +20,15 @@ def per_dispatch(d, counter, kernel):
     return vals
 
 
+def lib_sha256() -> str:
+    """sha256 of the library the counters were collected with (bench.py uses
+    the traffic only for this very build)."""
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "dips_amd", "lib", "libdips_hip.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def main():
     # usage: pmc_to_json.py DIR FRAMES MODE OUT [KERNEL BYTES_PER_FRAME]
     d, frames, mode, out = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
@@ -32,8 +41,8 @@ def main():
         raise SystemExit(f"no {kernel} rows (fetch {len(fetch)}, write {len(write)})")
     # the largest dispatches are the timed full-batch launches (a run may also
     # hold short parity-check launches of the same kernel)
-    full_f = [v for v in fetch if v >= 0.5 * max(fetch)]
-    full_w = [v for v in write if v >= 0.5 * max(write)]
+    full_f = [v for v in fetch if v >= 0.9 * max(fetch)]
+    full_w = [v for v in write if v >= 0.9 * max(write)]
     fk = sum(full_f) / len(full_f)
     wk = sum(full_w) / len(full_w)
     algo = frames * bpf
@@ -47,6 +56,8 @@ def main():
         "algorithmic_bytes_per_launch": algo,
         "traffic_over_algorithmic": (2 * fk * 1024 + wk * 1024) / algo,
         "dispatches": [len(full_f), len(full_w)],
+        "kernel": kernel,
+        "lib_sha256": lib_sha256(),
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
