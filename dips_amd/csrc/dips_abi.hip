@@ -152,6 +152,8 @@ int occupancy_blocks(dips_handle* h, const void* kernel) {
 struct FastGeom {
     bool ok = false;
     uint64_t n_tiles = 0, items = 0, n_waves = 0, blocks = 0;
+    uint64_t vec_bytes = 0;  // whole vecs of a frame (the vectorised kernel's range)
+    uint64_t tail_px0 = 0;   // first pixel of the ragged tail (npx: none)
 };
 
 FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, int C, bool pf,
@@ -160,9 +162,15 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t fb = npx * (uint64_t)C;
     const int ppv = dips::pixels_per_vec(C);
-    if (npx % (uint64_t)ppv != 0 || fb >= (1ull << 31) || n_frames == 0) return g;
-    const uint64_t U = (uint64_t)dips::fast_unroll(C);
+    // any alignment and pixel count: the vectorised kernel takes the whole
+    // vecs of every frame (unaligned frames through unaligned buffer loads,
+    // exact on gfx950: tools/unaligned_probe.hip), the generic kernel the
+    // < ppv trailing pixels
     const uint64_t nvec = npx / (uint64_t)ppv;
+    if (nvec == 0 || fb >= (1ull << 31) || n_frames == 0) return g;
+    const uint64_t U = (uint64_t)dips::fast_unroll(C);
+    g.vec_bytes = nvec * (uint64_t)ppv * (uint64_t)C;
+    g.tail_px0 = nvec * (uint64_t)ppv;
     g.n_tiles = (nvec + 64 * U - 1) / (64 * U);
     g.items = g.n_tiles * n_frames;
     const void* k = dips::series_fast_kernel_ptr(C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map);
@@ -194,12 +202,31 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     const uint64_t fb = npx * (uint64_t)C;
     DIPS_HIP(h, hipMemsetAsync(series, 0, sizeof(dips_series_entry) * (size_t)n_frames, s));
 
-    auto aligned4 = [](const void* q) { return ((uintptr_t)q & 3u) == 0; };
     FastGeom g;
-    if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC) && aligned4(frames) && aligned4(ref0) && (!map || aligned4(map)))
-        g = fast_geometry(h, width, height, n_frames, C, pf, map != nullptr);
+    if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC)) g = fast_geometry(h, width, height, n_frames, C, pf, map != nullptr);
+    auto launch_generic = [&](uint64_t px0) -> dips_status {
+        const uint64_t bpf = (npx - px0 + 255u) / 256u;
+        if (bpf * (uint64_t)n_frames >= (1ull << 31))
+            return fail(h, DIPS_ERR_INVALID, "frame batch too large for the generic kernel; split the batch");
+        dips::GenericArgs a{};
+        a.frames = frames;
+        a.ref0 = ref0;
+        a.dmap = map;
+        a.series = series;
+        a.frame_bytes = fb;
+        a.n_px = npx;
+        a.px0 = px0;
+        a.n_frames = n_frames;
+        a.blocks_per_frame = (uint32_t)bpf;
+        a.mode = h->p.mode;
+        a.chroma = C == 1 ? 0u : h->p.chroma_filter;
+        a.tau = h->p.tau;
+        DIPS_HIP(h, dips::launch_series_generic(a, C, s));
+        return DIPS_OK;
+    };
 
     const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
+    dips_status st = DIPS_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing) {
         e0 = take_event(h);
@@ -216,29 +243,22 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         a.partials = h->partials.as<uint64_t>();
         a.items = g.items;
         a.frame_bytes = (uint32_t)fb;
+        a.vec_bytes = (uint32_t)g.vec_bytes;
         a.n_frames = n_frames;
         a.n_tiles = (uint32_t)g.n_tiles;
         a.n_waves = (uint32_t)g.n_waves;
         a.thr = dips::series_threshold(C, h->p.tau);
         DIPS_HIP(h, dips::launch_series_fast(a, C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map != nullptr,
                                              (uint32_t)g.blocks, s));
+        // the ragged tail (< pixels_per_vec pixels per frame): its sums go
+        // straight into the series by atomics, so the order is free
+        if (g.tail_px0 < npx) {
+            st = launch_generic(g.tail_px0);
+            if (st != DIPS_OK) return st;
+        }
     } else {
-        const uint64_t bpf = (npx + 255u) / 256u;
-        if (bpf * (uint64_t)n_frames >= (1ull << 31))
-            return fail(h, DIPS_ERR_INVALID, "frame batch too large for the generic kernel; split the batch");
-        dips::GenericArgs a{};
-        a.frames = frames;
-        a.ref0 = ref0;
-        a.dmap = map;
-        a.series = series;
-        a.frame_bytes = fb;
-        a.n_px = npx;
-        a.n_frames = n_frames;
-        a.blocks_per_frame = (uint32_t)bpf;
-        a.mode = h->p.mode;
-        a.chroma = C == 1 ? 0u : h->p.chroma_filter;
-        a.tau = h->p.tau;
-        DIPS_HIP(h, dips::launch_series_generic(a, C, s));
+        st = launch_generic(0);
+        if (st != DIPS_OK) return st;
     }
     if (timing) {
         DIPS_HIP(h, hipEventRecord(e1, s));
@@ -584,6 +604,7 @@ dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_
     a.k = h->p.sensitivity;
     a.kneg_half = -h->p.sensitivity * 0.5f;
     const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
+    dips_status st = DIPS_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing) {
         e0 = take_event(h);

@@ -28,7 +28,9 @@ struct SeriesArgs {
     uint8_t* dmap;           // optional |F - R| map (same layout as frames)
     uint64_t* partials;      // [n_tiles][n_frames] x 16-byte records
     uint64_t items;          // n_tiles * n_frames
-    uint32_t frame_bytes;
+    uint32_t frame_bytes;    // frame stride in bytes (W * H * C; any alignment)
+    uint32_t vec_bytes;      // bytes of whole vecs per frame (the descriptor range; the
+                             // < pixels_per_vec trailing pixels go to the generic kernel)
     uint32_t n_frames;
     uint32_t n_tiles;
     uint32_t n_waves;
@@ -42,6 +44,7 @@ struct GenericArgs {
     dips_series_entry* series;
     uint64_t frame_bytes;
     uint64_t n_px;
+    uint64_t px0;            // first pixel of each frame to process (the fast kernel's ragged tail)
     uint32_t n_frames;
     uint32_t blocks_per_frame;
     uint32_t mode;

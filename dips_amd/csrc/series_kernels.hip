@@ -151,7 +151,7 @@ __device__ __forceinline__ void frame_accumulate(const SeriesArgs& a, const RefS
 #pragma unroll
     for (int u = 0; u < U; ++u) process_vec<C, CH, PF, MAP>(ref[u], next[u], cur[u], a.thr, acc, map[u], lut);
     if constexpr (MAP) {
-        const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.frame_bytes);
+        const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.vec_bytes);
 #pragma unroll
         for (int u = 0; u < U; ++u) store_vec<C>(rm, voff[u], map[u]);
     }
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
     // then provably wave-uniform (scalar registers, no waterfall loops).
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (wave >= a.n_waves) return;
-    const uint32_t fb = a.frame_bytes;
+    const uint32_t fb = a.frame_bytes, vb = a.vec_bytes;
 
     uint64_t i = (uint64_t)wave * a.items / a.n_waves;
     const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
         const uint8_t* rp = PF ? (t == 0 ? a.ref0 : a.frames + (uint64_t)(t - 1) * fb) : a.ref0;
         RefState<C> sa[U], sb[U];
         {
-            const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, fb);
+            const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, vb);
             uint32_t d[U][F::NDW];
 #pragma unroll
             for (int u = 0; u < U; ++u) load_vec<C>(rr, voff[u], d[u]);
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             const uint32_t tl = min(t + (uint32_t)d, tlast);
-            const __amdgpu_buffer_rsrc_t rf = make_rsrc(a.frames + (uint64_t)tl * fb, fb);
+            const __amdgpu_buffer_rsrc_t rf = make_rsrc(a.frames + (uint64_t)tl * fb, vb);
 #pragma unroll
             for (int u = 0; u < U; ++u) load_vec<C>(rf, voff[u], buf[d][u]);
         }
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
                 __builtin_amdgcn_sched_barrier(0);
                 {
                     const uint32_t tl = min(t + (uint32_t)(d + D), tlast);
-                    const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.frames + (uint64_t)tl * fb, fb);
+                    const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.frames + (uint64_t)tl * fb, vb);
 #pragma unroll
                     for (int u = 0; u < U; ++u) load_vec<C>(rn, voff[u], buf[d][u]);
                 }
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
                 __builtin_amdgcn_sched_barrier(0);
                 {
                     const uint32_t tl = min(t + (uint32_t)(d + 1 + D), tlast);
-                    const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.frames + (uint64_t)tl * fb, fb);
+                    const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.frames + (uint64_t)tl * fb, vb);
 #pragma unroll
                     for (int u = 0; u < U; ++u) load_vec<C>(rn, voff[u], buf[d + 1][u]);
                 }
@@ -372,7 +372,7 @@ template <int C>
 __global__ __launch_bounds__(256) void series_generic_kernel(GenericArgs a) {
     __shared__ uint64_t red[4][4];
     const uint32_t t = blockIdx.x / a.blocks_per_frame;
-    const uint64_t p = (uint64_t)(blockIdx.x - t * a.blocks_per_frame) * 256u + threadIdx.x;
+    const uint64_t p = a.px0 + (uint64_t)(blockIdx.x - t * a.blocks_per_frame) * 256u + threadIdx.x;
     const uint64_t fb = a.frame_bytes;
     const uint8_t* F = a.frames + (uint64_t)t * fb;
     const uint8_t* R = a.mode == 1u ? (t == 0 ? a.ref0 : a.frames + (uint64_t)(t - 1) * fb) : a.ref0;

@@ -78,7 +78,7 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
         if constexpr (PF) st[u] = n;
     }
     if constexpr (MAP) {
-        const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.frame_bytes);
+        const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.vec_bytes);
 #pragma unroll
         for (int u = 0; u < U; ++u) store_vec<C>(rm, voff + (uint32_t)(u * 64 * F::VB), map[u]);
     }
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (wave >= a.n_waves) return;
-    const uint32_t fb = a.frame_bytes;
+    const uint32_t fb = a.frame_bytes, vb = a.vec_bytes;
     // record dword offsets of the lanes that store reduced values; other
     // lanes point past the descriptor and their stores are dropped
     const uint32_t rec_off8 = (lane & 7u) == 0u ? (lane >> 5) * 16u + ((lane >> 3) & 3u) * 4u : 0x80000000u;
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v
             // segment's first frame -- the kernel's compute-only time
             tf = t0;
 #endif
-            const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)min(tf, tlast) * fb, fb);
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)min(tf, tlast) * fb, vb);
 #pragma unroll
             for (int u = 0; u < U; ++u) load_vec<C>(r, voff + (uint32_t)(u * 64 * F::VB), dst[u]);
         };
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v
         St2 st[U];
         {
             const uint8_t* rp = PF ? (t0 == 0 ? a.ref0 : a.frames + (uint64_t)(t0 - 1) * fb) : a.ref0;
-            const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, fb);
+            const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, vb);
             uint32_t (&dref)[U][F::NDW] = PF ? buf[0] : rb;
 #pragma unroll
             for (int u = 0; u < U; ++u) load_vec<C>(rr, voff + (uint32_t)(u * 64 * F::VB), dref[u]);

@@ -315,3 +315,51 @@ def test_config0_gray8_full_clip_matches_oracle():
             op.close()
         _check(got, out4, si, gmap, dmap)
         assert np.array_equal(ser.cpu().numpy().view(np.uint64), out4)
+
+
+RAGGED_SHAPES = [(37, 23), (5, 3), (1, 1), (641, 3), (17, 1)]
+
+
+@pytest.mark.parametrize("c", [1, 3, 4])
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("offsets", [(0, 0, 0), (1, 2, 3), (3, 1, 2), (2, 3, 1)])
+def test_unaligned_device_batches(c, mode, offsets):
+    """The vectorised kernel on frame batches, references and maps at byte
+    offsets 1-3 from an aligned address and with ragged pixel counts (frame
+    strides that are not a multiple of 4, < pixels_per_vec trailing pixels
+    per frame handled by the generic kernel) -- against the oracle.  These
+    shapes ran entirely on series_generic_kernel before (4 % of 8 TB/s,
+    profiles/r02_fallback_rate_before.jsonl)."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    fo, ro, mo = offsets
+    for (w, h) in [(64, 48)] + RAGGED_SHAPES:
+        for tau, chroma in [(0.0, 0), (8 / 255, 0 if c == 1 else 2)]:
+            n = 9
+            frames = _frames(c, w, h, n, 5 + w, "random" if w % 2 else "synth")
+            ref = _frames(c, w, h, 1, 77, "random")[0]
+            fb = frames[0].size
+            dev = torch.device("cuda")
+            fbuf = torch.zeros(n * fb + 8, dtype=torch.uint8, device=dev)
+            rbuf = torch.zeros(fb + 8, dtype=torch.uint8, device=dev)
+            mbuf = torch.full((n * fb + 8,), 0xA5, dtype=torch.uint8, device=dev)
+            fdev = fbuf[fo:fo + n * fb].view(frames.shape)
+            fdev.copy_(torch.from_numpy(frames))
+            rdev = rbuf[ro:ro + fb].view(ref.shape)
+            rdev.copy_(torch.from_numpy(ref))
+            mdev = mbuf[mo:mo + n * fb].view(frames.shape)
+            series = torch.zeros((n, 4), dtype=torch.int64, device=dev)
+            op = DiffSeriesOperator(PixelFormat(c), Mode(mode), tau, chroma)
+            try:
+                op.run_device(fdev, series, ref=rdev if mode == 0 else None, map_out=mdev)
+                torch.cuda.synchronize()
+            finally:
+                op.close()
+            out4, _, dmap = oracle.series(frames, mode=mode, chroma=chroma, tau=tau,
+                                          ref=ref if mode == 0 else None, want_map=True)
+            got = series.cpu().numpy().view(np.uint64)
+            assert np.array_equal(got, out4), ((w, h), tau, got, out4)
+            m = mbuf.cpu().numpy()
+            assert np.array_equal(m[mo:mo + n * fb].reshape(frames.shape), dmap), (w, h)
+            # nothing written outside the map
+            assert (m[:mo] == 0xA5).all() and (m[mo + n * fb:] == 0xA5).all()

@@ -31,6 +31,8 @@ CASES = [
     ("1920x1080 RGB8 forced generic kernel", 1920, 1080, 3, 0, True),
     ("1920x1080 RGBA8 batch at +2 bytes", 1920, 1080, 4, 2, False),
     ("641x479 gray8 (odd pixel count)", 641, 479, 1, 0, False),
+    ("640x480 gray8 aligned", 640, 480, 1, 0, False),
+    ("1920x1080 RGBA8 aligned", 1920, 1080, 4, 0, False),
 ]
 
 
@@ -74,9 +76,11 @@ def main():
             ok = bool(np.array_equal(series[:3].cpu().numpy().view(np.uint64), want))
         finally:
             op.close()
-        aligned_fast = off % 4 == 0 and (W * H) % (16 if C == 1 else 4) == 0 and not generic
+        ppv = 16 if C == 1 else 4
+        kernel = "generic" if generic or not waves else (
+            "vectorised + generic tail" if (W * H) % ppv else "vectorised")
         print(json.dumps({"case": name, "frames": F, "mode": args.mode,
-                          "kernel": "fast" if aligned_fast and waves else "generic",
+                          "byte_offset": off, "frame_bytes_mod4": fb % 4, "kernel": kernel,
                           "frames_per_s": round(F / wall, 1), "kernel_ms": round(kms, 4),
                           "kernel_GBps": round(F * fb / (kms / 1e3) / 1e9, 1),
                           "frac_of_8TBps": round(F * fb / (kms / 1e3) / 8e12, 4),
