@@ -196,6 +196,171 @@ __global__ __launch_bounds__(256) void compat_batch_kernel(CompatBatchArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// The epilogue as a table.  In steady state (t >= 7, W = 1) the output texel
+// of compute_main is a function of two bytes only: the start-texture byte S
+// and the upper-median byte m (diff = u(S) - u(m), :192, :213; everything
+// after is a pure function of diff and the properties).  compat_lut_kernel
+// evaluates the specification (dips_math.h visual_epilogue) once per (S, m)
+// and keeps R | G << 8; B and A follow: A = 255, and B = m' = min(R, G)
+// because the colour branch stores (chroma + m', m', m') or (m', chroma + m',
+// m') with chroma >= 0, q() is monotone and NaN stores as 0 (so NaN channels
+// never exceed m'), and the gray branch stores R = G = B.  The batch kernel keeps the 128 KiB table
+// in LDS (one 1024-thread workgroup per CU) and replaces the per-pixel
+// filter / sigmoid / colour arithmetic with one ds_read_u16 per pixel, for
+// every filter, sensitivity and colour setting alike.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void compat_lut_kernel(uint16_t* __restrict__ lut, uint32_t filter, float k,
+                                                         uint32_t colorize) {
+    const uint32_t idx = blockIdx.x * 256u + threadIdx.x;  // S * 256 + m
+    const float diff = unorm_load(idx >> 8) - unorm_load(idx & 0xFFu);
+    lut[idx] = (uint16_t)(visual_epilogue(diff, filter, k, colorize != 0u) & 0xFFFFu);
+}
+
+// RGBA texel (R, G, min(R, G), 255) of a table entry R | G << 8: the u16
+// halves of (R, G, R, FF) and (R, G, G, FF) are equal in the low half and
+// (R | FF00, G | FF00) in the high one, so one packed u16 min finishes it.
+__device__ __forceinline__ uint32_t lut_texel(uint32_t e) {
+    const u16x2 x = as_u16x2(__builtin_amdgcn_perm(e, e, 0x0D000100u));
+    const u16x2 y = as_u16x2(__builtin_amdgcn_perm(e, e, 0x0D010100u));
+    return as_u32(umin(x, y));
+}
+
+constexpr int kLutWaves = (int)kCompatLutWaves;
+
+template <int CH, int U>
+__global__ __launch_bounds__(64 * kLutWaves) void compat_batch_lut_kernel(CompatBatchArgs a) {
+    __shared__ uint32_t lds[32768];  // 65536 u16 entries (128 KiB)
+    {
+        const u32x4* src = reinterpret_cast<const u32x4*>(a.lut);
+        u32x4* dst = reinterpret_cast<u32x4*>(lds);
+        for (uint32_t i = threadIdx.x; i < 8192u; i += 64u * kLutWaves) dst[i] = src[i];
+    }
+    __syncthreads();
+    const uint16_t* tab = reinterpret_cast<const uint16_t*>(lds);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t item = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)kLutWaves + (threadIdx.x >> 6));
+    if (item >= a.n_tiles * a.n_chunks) return;
+    const uint32_t c = item / a.n_tiles;
+    const uint32_t tile = item - c * a.n_tiles;
+    const uint32_t t0 = c * a.chunk;
+    const uint32_t t1 = min(t0 + a.chunk, a.n_frames);
+    const uint32_t fb = a.frame_bytes;
+    uint32_t voff[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t vec = (tile * U + (uint32_t)u) * 64u + lane;
+        voff[u] = vec < a.n_vec ? vec * 16u : 0x80000000u;  // out of range: loads 0, stores dropped
+    }
+
+    // S << 8 of the start texture's R bytes, as u16x2 planes: S * 256 + m is
+    // then one OR per pixel pair
+    uint32_t s8[U][2];
+    {
+        const __amdgpu_buffer_rsrc_t r = make_rsrc(a.start, fb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint32_t d[4], p[2];
+            load_vec<4>(r, voff[u], d);
+            r_planes(d, p);
+            s8[u][0] = p[0] << 8;
+            s8[u][1] = p[1] << 8;
+        }
+    }
+    uint32_t q1[U][2], q2[U][2], q3[U][2];
+    auto prev_q = [&](int j, uint32_t (&dst)[U][2]) {
+        if (c == 0) {
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(a.pre[j], fb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                uint32_t d[4];
+                load_vec<4>(r, voff[u], d);
+                r_planes(d, dst[u]);
+            }
+        } else {
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)(t0 - 1 - j) * fb, fb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                uint32_t d[4];
+                load_vec<4>(r, voff[u], d);
+                St2 s;
+                derive_v2<4, CH>(d, s);
+                quantise_planes(s, dst[u]);
+            }
+        }
+    };
+    prev_q(0, q1);
+    prev_q(1, q2);
+    prev_q(2, q3);
+
+    auto load_frame = [&](uint32_t t, uint32_t (&d)[U][4]) {
+        const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)t * fb, fb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_vec<4>(r, voff[u], d[u]);
+    };
+    auto process = [&](uint32_t t, const uint32_t (&d)[U][4]) {
+        const __amdgpu_buffer_rsrc_t ro = make_rsrc(a.out + (uint64_t)t * fb, fb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            St2 s;
+            derive_v2<4, CH>(d[u], s);
+            uint32_t q0[2];
+            quantise_planes(s, q0);
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t x = s8[u][k] | upper4(q0[k], q1[u][k], q2[u][k], q3[u][k]);
+                o[2 * k] = lut_texel(tab[x & 0xFFFFu]);
+                o[2 * k + 1] = lut_texel(tab[x >> 16]);
+                q3[u][k] = q2[u][k];
+                q2[u][k] = q1[u][k];
+                q1[u][k] = q0[k];
+            }
+            store_vec<4>(ro, voff[u], o);
+        }
+    };
+
+    uint32_t buf[2][U][4];
+    uint32_t t = t0;
+    load_frame(t, buf[0]);
+    while (true) {
+        if (t + 1 < t1) load_frame(t + 1, buf[1]);
+        process(t, buf[0]);
+        if (++t >= t1) break;
+        if (t + 1 < t1) load_frame(t + 1, buf[0]);
+        process(t, buf[1]);
+        if (++t >= t1) break;
+    }
+
+    if (c + 1 == a.n_chunks) {
+        uint32_t q4[U][2];
+        if (a.post[3] != nullptr) {
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)(a.n_frames - 4) * fb, fb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                uint32_t d[4];
+                load_vec<4>(r, voff[u], d);
+                St2 s;
+                derive_v2<4, CH>(d, s);
+                quantise_planes(s, q4[u]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (a.post[j] == nullptr) continue;
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(a.post[j], fb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t(&p)[2] = j == 0 ? q1[u] : (j == 1 ? q2[u] : (j == 2 ? q3[u] : q4[u]));
+                uint32_t o[4];
+                gray_pair(p[0], o[0], o[1]);
+                gray_pair(p[1], o[2], o[3]);
+                store_vec<4>(r, voff[u], o);
+            }
+        }
+    }
+}
+
 template <int CH, int FILT, bool FAST>
 const void* cb_ptr_fc(bool colorize) {
     return colorize ? reinterpret_cast<const void*>(&compat_batch_kernel<CH, FILT, 1, FAST, kUnrollCompatBatch>)
@@ -221,6 +386,29 @@ const void* compat_batch_kernel_ptr(int chroma, int filter, bool colorize, bool 
         case 3: return cb_ptr_c<3>(filter, colorize, fast);
         default: return nullptr;
     }
+}
+
+const void* compat_batch_lut_kernel_ptr(int chroma) {
+    switch (chroma) {
+        case 0: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<0, kUnrollCompatLut>);
+        case 1: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<1, kUnrollCompatLut>);
+        case 2: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<2, kUnrollCompatLut>);
+        case 3: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<3, kUnrollCompatLut>);
+        default: return nullptr;
+    }
+}
+
+hipError_t launch_compat_lut(uint16_t* lut, uint32_t filter, float k, bool colorize, hipStream_t s) {
+    hipLaunchKernelGGL(compat_lut_kernel, dim3(256), dim3(256), 0, s, lut, filter, k, colorize ? 1u : 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_batch_lut(const CompatBatchArgs& a, int chroma, uint32_t blocks, hipStream_t s) {
+    const void* k = compat_batch_lut_kernel_ptr(chroma);
+    if (!k || blocks == 0 || !a.lut) return hipErrorInvalidValue;
+    CompatBatchArgs args = a;
+    void* params[] = {&args};
+    return hipLaunchKernel(k, dim3(blocks), dim3(64 * kLutWaves), params, 0, s);
 }
 
 hipError_t launch_compat_batch(const CompatBatchArgs& a, int chroma, int filter, bool colorize, bool fast,

@@ -81,6 +81,10 @@ struct dips_handle {
     dips_host::PieceEvents up_pieces;  // per-stripe upload completion (striped frame_callback)
     HostPinned io_out;                 // readback staging of the striped frame_callback
     int cb_occupancy = 0;
+    DevBuf cb_lut;            // epilogue table of compat_batch_lut_kernel (128 KiB)
+    bool cb_lut_valid = false;
+    uint32_t cb_lut_filter = 0, cb_lut_col = 0;
+    float cb_lut_k = 0.0f;
 };
 
 namespace {
@@ -372,6 +376,7 @@ void dips_destroy(dips_handle* h) {
     h->io_out.release();
     h->raw.release();
     h->filtered.release();
+    h->cb_lut.release();
     h->start.release();
     h->out.release();
     h->io.release();
@@ -558,18 +563,29 @@ dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_
     const size_t fb = (size_t)width * height * 4u;
     const uint64_t npx = (uint64_t)width * height;
     const bool fast = dips::alt_fast_epilogue_ok(h->p.filter_type, h->p.sensitivity);
-    const void* k = dips::compat_batch_kernel_ptr((int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0,
-                                                  fast);
+    // the epilogue-table kernel (default) or the per-pixel arithmetic one
+    // (DIPS_COMPAT_LUT=0: kept for A/B runs and as a cross-check in the tests)
+    bool lut = true;
+    if (const char* e = std::getenv("DIPS_COMPAT_LUT"))
+        if (e[0] == '0') lut = false;
+    const void* k = lut ? dips::compat_batch_lut_kernel_ptr((int)h->p.chroma_filter)
+                        : dips::compat_batch_kernel_ptr((int)h->p.chroma_filter, (int)h->p.filter_type,
+                                                        h->p.colorize != 0, fast);
     if (!k) return fail(h, DIPS_ERR_INVALID, "no batch kernel for these parameters");
-    if (h->cb_occupancy == 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess || nb < 1) nb = 1;
-        h->cb_occupancy = nb;
+    uint64_t resident = 0;
+    if (lut) {
+        resident = (uint64_t)dips::kCompatLutWaves * (uint64_t)h->cu_count;  // one workgroup per CU (LDS)
+    } else {
+        if (h->cb_occupancy == 0) {
+            int nb = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess || nb < 1) nb = 1;
+            h->cb_occupancy = nb;
+        }
+        resident = (uint64_t)h->cb_occupancy * 4u * (uint64_t)h->cu_count;
     }
     const uint64_t n_vec = npx / 4u;
-    const uint64_t U = dips::kUnrollCompatBatch;
+    const uint64_t U = lut ? (uint64_t)dips::kUnrollCompatLut : (uint64_t)dips::kUnrollCompatBatch;
     const uint64_t n_tiles = (n_vec + 64u * U - 1) / (64u * U);
-    const uint64_t resident = (uint64_t)h->cb_occupancy * 4u * (uint64_t)h->cu_count;
     uint64_t n_chunks = (resident + n_tiles - 1) / n_tiles;
     n_chunks = std::min<uint64_t>(n_chunks, (m + 15u) / 16u);
     n_chunks = std::max<uint64_t>(n_chunks, 1);
@@ -603,6 +619,21 @@ dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_
     a.n_tiles = (uint32_t)n_tiles;
     a.k = h->p.sensitivity;
     a.kneg_half = -h->p.sensitivity * 0.5f;
+    if (lut) {
+        // (re)build the table when the properties changed since the last batch
+        const uint32_t col = h->p.colorize != 0 ? 1u : 0u;
+        if (!h->cb_lut_valid || h->cb_lut_filter != h->p.filter_type || h->cb_lut_col != col ||
+            !(h->cb_lut_k == h->p.sensitivity)) {
+            DIPS_HIP(h, h->cb_lut.ensure(65536u * sizeof(uint16_t)));
+            DIPS_HIP(h, dips::launch_compat_lut(h->cb_lut.as<uint16_t>(), h->p.filter_type, h->p.sensitivity,
+                                                col != 0, h->stream));
+            h->cb_lut_valid = true;
+            h->cb_lut_filter = h->p.filter_type;
+            h->cb_lut_col = col;
+            h->cb_lut_k = h->p.sensitivity;
+        }
+        a.lut = h->cb_lut.as<uint16_t>();
+    }
     const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
     dips_status st = DIPS_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -615,8 +646,13 @@ dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_
     if (filter_src)
         DIPS_HIP(h, dips::launch_compat_filter_frames(filter_src, const_cast<uint8_t*>(bf), width, height, m,
                                                       h->p.spatial_window_size, h->p.chroma_filter, h->stream));
-    DIPS_HIP(h, dips::launch_compat_batch(a, (int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0, fast,
-                                          (uint32_t)((n_tiles * n_chunks + 3u) / 4u), h->stream));
+    if (lut)
+        DIPS_HIP(h, dips::launch_compat_batch_lut(
+                        a, (int)h->p.chroma_filter,
+                        (uint32_t)((n_tiles * n_chunks + dips::kCompatLutWaves - 1) / dips::kCompatLutWaves), h->stream));
+    else
+        DIPS_HIP(h, dips::launch_compat_batch(a, (int)h->p.chroma_filter, (int)h->p.filter_type, h->p.colorize != 0,
+                                              fast, (uint32_t)((n_tiles * n_chunks + 3u) / 4u), h->stream));
     if (timing) {
         DIPS_HIP(h, hipEventRecord(e1, h->stream));
         h->ev_pending.emplace_back(e0, e1);

@@ -91,8 +91,15 @@ struct CompatBatchArgs {
     uint32_t n_frames, chunk, n_chunks, n_tiles;
     float k;                 // sensitivity (SIGMOID_HORIZONTAL_SCALAR)
     float kneg_half;         // -k / 2
+    const uint16_t* lut;     // epilogue table (compat_batch_lut_kernel): 65536 x (R | G << 8)
 };
 constexpr int kUnrollCompatBatch = 2;
+constexpr int kUnrollCompatLut = 2;  // U = 4 measured equal (profiles/r02_compat_lut_bench2.jsonl)
+constexpr uint32_t kCompatLutWaves = 16;  // waves per workgroup of compat_batch_lut_kernel (one per CU)
+// the epilogue table of the current properties: lut[S * 256 + m]
+hipError_t launch_compat_lut(uint16_t* lut, uint32_t filter, float k, bool colorize, hipStream_t s);
+const void* compat_batch_lut_kernel_ptr(int chroma);
+hipError_t launch_compat_batch_lut(const CompatBatchArgs& a, int chroma, uint32_t blocks, hipStream_t s);
 const void* compat_batch_kernel_ptr(int chroma, int filter, bool colorize, bool fast);
 hipError_t launch_compat_batch(const CompatBatchArgs& a, int chroma, int filter, bool colorize, bool fast,
                                uint32_t blocks, hipStream_t s);

@@ -426,3 +426,30 @@ def test_handles_on_concurrent_threads(monkeypatch):
         ref = oracle.AltCompute(2, w, h)
         want = np.stack([ref.send_frame(f, t == 2) for t, f in enumerate(clips[k])])
         assert np.array_equal(results[k], want), k
+
+
+@pytest.mark.parametrize("colorize", [False, True])
+@pytest.mark.parametrize("filt", [0, 1, 255])
+@pytest.mark.parametrize("sens", [5.0, -3.0, 0.0, 200.0, 1e-30])
+def test_batch_epilogue_table_equals_arithmetic_and_oracle(colorize, filt, sens, monkeypatch):
+    """compat_batch_lut_kernel (the epilogue as a 65536-entry (S, m) table in
+    LDS, the default) against compat_batch_kernel (the per-pixel arithmetic,
+    DIPS_COMPAT_LUT=0) and the oracle, on random frames that reach many (S, m)
+    pairs, for every filter, negative / zero / huge / tiny sensitivities (the
+    inverse sigmoid's inf and NaN texels included) and both colour modes."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+    w, h, n = 96, 64, 30
+    frames = _frames(w, h, n, 1234 + filt)
+    frames[15] = frames[14]
+    params = (colorize, 1, sens, filt, 0)
+    want = _oracle_callbacks(frames, params)
+    outs = {}
+    for lut in ("1", "0"):
+        monkeypatch.setenv("DIPS_COMPAT_LUT", lut)
+        cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter.None_)
+        try:
+            outs[lut] = cs.frame_callback_batch(w, h, frames)
+        finally:
+            cs.close()
+    assert np.array_equal(outs["1"], outs["0"]), np.argwhere(outs["1"] != outs["0"])[:4]
+    assert np.array_equal(outs["1"], want), np.argwhere(outs["1"] != want)[:4]

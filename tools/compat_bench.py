@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--kernels", default="lut,arith",
+                    help="lut: compat_batch_lut_kernel (epilogue table, default); arith: compat_batch_kernel")
     args = ap.parse_args()
     import torch
     from dips_amd import ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, PixelFormat
@@ -40,8 +42,11 @@ def main():
     op.synth_device(frames, W, H, 0xD1B5, 0)
     op.close()
     out = torch.empty_like(frames)
-    for name, props in [("default (gray, Unfiltered)", (False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)),
-                        ("colorize + sigmoid k=5", (True, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_))]:
+    cases = [("default (gray, Unfiltered)", (False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)),
+             ("colorize + sigmoid k=5", (True, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)),
+             ("colorize + inverse sigmoid k=5", (True, 1, 5.0, DiPsFilter.InverseSigmoid, ChromaFilter.None_))]
+    for (name, props), kern in [(c, k) for c in cases for k in args.kernels.split(",")]:
+        os.environ["DIPS_COMPAT_LUT"] = "0" if kern == "arith" else "1"
         cs = ComputeState(*props, time_kernel=True)
         cs.frame_callback_batch_device(frames[:7], out[:7])  # warm-up frames of the stream
         for _ in range(args.warmup):
@@ -73,6 +78,8 @@ def main():
         achieved = algo / (kernel_ms / 1e3) / 1e9
         print(json.dumps({
             "metric": "dips ComputeState batch frames/s + achieved HBM GB/s, 4K RGBA8", "properties": name,
+            "kernel": {"lut": "compat_batch_lut_kernel (epilogue table in LDS)",
+                       "arith": "compat_batch_kernel (per-pixel epilogue arithmetic)"}[kern],
             "value": round(F * args.steps / elapsed, 2), "unit": "frames/s", "kernel_ms": round(kernel_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": algo},
