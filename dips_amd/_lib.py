@@ -167,6 +167,7 @@ def load() -> ctypes.CDLL:
             "dips_alt_snapshot_texture": ([_vp, _u8p, ctypes.c_size_t], st),
             "dips_alt_kernel_time": ([_vp, P(ctypes.c_double), P(u64)], st),
             "dips_alt_kernel_time_reset": ([_vp], st),
+            "dips_alt_lut_selfcheck": ([_vp, P(u64)], st),
         }
         del i32, f32
         for name, (args, res) in sig.items():

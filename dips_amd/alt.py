@@ -222,6 +222,13 @@ class DiPsCompute:
             hd.check(hd._lib.dips_alt_kernel_time_reset(hd.ptr))
         return ms.value, cnt.value
 
+    def lut_selfcheck(self) -> int:
+        """Mismatches of the batch kernel's epilogue table against the
+        specification over every (snapshot byte, max, min) -- 0 expected."""
+        n = ctypes.c_uint64()
+        self._host.check(self._host._lib.dips_alt_lut_selfcheck(self._host.ptr, ctypes.byref(n)))
+        return n.value
+
     def snapshot_texture(self) -> np.ndarray:
         out = np.empty((self.rows, self.cols), dtype=np.uint8)
         self._host.check(self._host._lib.dips_alt_snapshot_texture(self._host.ptr, out.ctypes.data, out.nbytes))

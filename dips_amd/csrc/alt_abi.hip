@@ -17,9 +17,93 @@
 #include <vector>
 
 #include "../../include/dips_hip.h"
+#include "alt_lut.h"
 #include "dips_kernels.h"
 #include "host_buffers.h"
 #include "host_stream.h"
+
+namespace dips {
+
+// The exact two-level index of alt_lut.h.  The value set is enumerated with
+// the device's f32 arithmetic: u(c) = c / 255 (IEEE division, correctly
+// rounded like __fdiv_rn), I = (u(max) + u(min)) / 2, diff = u(S) - I, and the
+// cluster from fmaf(diff, 510, 1.5 * 2^23) like v_fma_f32.
+const AltLutIndex& alt_lut_index() {
+    static AltLutIndex idx;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        float u[256];
+        for (int c = 0; c < 256; ++c) u[c] = (float)c / 255.0f;
+        std::vector<float> iv;
+        iv.reserve(32896);
+        for (int mx = 0; mx < 256; ++mx)
+            for (int mn = 0; mn <= mx; ++mn) iv.push_back((u[mx] + u[mn]) / 2.0f);
+        std::sort(iv.begin(), iv.end());
+        iv.erase(std::unique(iv.begin(), iv.end()), iv.end());
+        std::vector<uint32_t> bits;
+        bits.reserve(256 * iv.size());
+        for (int s = 0; s < 256; ++s)
+            for (float i : iv) {
+                const float d = u[s] - i;
+                uint32_t b;
+                std::memcpy(&b, &d, 4);
+                bits.push_back(b);
+            }
+        std::sort(bits.begin(), bits.end());
+        bits.erase(std::unique(bits.begin(), bits.end()), bits.end());
+        // clusters
+        std::vector<std::vector<uint32_t>> cl(kAltLutClusters);
+        for (uint32_t b : bits) {
+            float d;
+            std::memcpy(&d, &b, 4);
+            const float t = std::fmaf(d, 510.0f, kAltLutRound);
+            uint32_t tb;
+            std::memcpy(&tb, &t, 4);
+            const uint32_t c = tb - (0x4B400000u - 510u);  // |diff| <= 1: always in range
+            if (c < (uint32_t)kAltLutClusters) cl[c].push_back(b);
+        }
+        uint32_t off = 0;
+        idx.diffs.clear();
+        idx.slots.clear();
+        for (int c = 0; c < kAltLutClusters; ++c) {
+            const auto& m = cl[c];
+            uint32_t best_sh = 0, best_span = 0, best_base = 0;
+            bool found = false;
+            for (uint32_t sh = 0; sh < 32 && !m.empty(); ++sh) {
+                std::vector<uint32_t> v;
+                for (uint32_t b : m) v.push_back(b >> sh);
+                std::sort(v.begin(), v.end());
+                if (std::adjacent_find(v.begin(), v.end()) != v.end()) continue;  // not injective
+                const uint32_t span = v.back() - v.front() + 1;
+                if (!found || span < best_span) {
+                    found = true;
+                    best_sh = sh;
+                    best_span = span;
+                    best_base = v.front();
+                }
+            }
+            if (m.empty()) {  // no member: never read
+                idx.l1[2 * c] = 0;
+                idx.l1[2 * c + 1] = 0;
+                continue;
+            }
+            // byte address = ((bits >> sh) << 1) + x = 2 * (off + (bits >> sh) - base)
+            idx.l1[2 * c] = 2u * off - 2u * best_base;
+            idx.l1[2 * c + 1] = best_sh;
+            for (uint32_t b : m) {
+                float d;
+                std::memcpy(&d, &b, 4);
+                idx.diffs.push_back(d);
+                idx.slots.push_back((uint16_t)(off + (b >> best_sh) - best_base));
+            }
+            off += best_span;
+        }
+        idx.l2_entries = off;
+    });
+    return idx;
+}
+
+}  // namespace dips
 
 namespace {
 
@@ -62,6 +146,13 @@ struct dips_alt_handle {
     int meta_turn = 0;
     int occupancy = 0;
     int occupancy_pre = 0;  // the prefiltered (W > 1) batch kernel
+    int occupancy_lut = 0, occupancy_lut_pre = 0;  // the epilogue-table forms
+    // epilogue table (alt_lut.h): the index (uploaded once) and the u16
+    // contents for the current properties
+    DevBuf lut_l1, lut_diffs, lut_slots, lut_l2;
+    bool lut_index_ready = false, lut_valid = false;
+    uint32_t lut_filter = 0, lut_col = 0;
+    float lut_k = 0.0f;
     DevBuf filtered;        // W > 1 batch: filtered f32 intensities of a chunk of frames (+ the one before)
 
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
@@ -160,6 +251,40 @@ bool window_eligible(const dips_alt_handle* h, const uint8_t* frames, const uint
            h->n_px() % 4u == 0 && ((uintptr_t)frames & 3u) == 0 && ((uintptr_t)out & 15u) == 0;
 }
 
+// The epilogue table of alt_lut.h for the handle's properties: the index is
+// uploaded once, the u16 contents are refilled when the properties change.
+dips_status ensure_lut(dips_alt_handle* h, hipStream_t s) {
+    const dips::AltLutIndex& ix = dips::alt_lut_index();
+    {
+        if (!h->lut_index_ready) {
+            ALT_HIP(h, h->lut_l1.ensure(sizeof(ix.l1)));
+            ALT_HIP(h, h->lut_diffs.ensure(ix.diffs.size() * sizeof(float)));
+            ALT_HIP(h, h->lut_slots.ensure(ix.slots.size() * sizeof(uint16_t)));
+            ALT_HIP(h, h->lut_l2.ensure((size_t)dips::kAltLutL2Max * sizeof(uint16_t)));
+            ALT_HIP(h, hipMemcpyAsync(h->lut_l1.p, ix.l1, sizeof(ix.l1), hipMemcpyHostToDevice, s));
+            ALT_HIP(h, hipMemcpyAsync(h->lut_diffs.p, ix.diffs.data(), ix.diffs.size() * sizeof(float),
+                                      hipMemcpyHostToDevice, s));
+            ALT_HIP(h, hipMemcpyAsync(h->lut_slots.p, ix.slots.data(), ix.slots.size() * sizeof(uint16_t),
+                                      hipMemcpyHostToDevice, s));
+            ALT_HIP(h, hipMemsetAsync(h->lut_l2.p, 0, (size_t)dips::kAltLutL2Max * sizeof(uint16_t), s));
+            ALT_HIP(h, hipStreamSynchronize(s));  // once per handle
+            h->lut_index_ready = true;
+        }
+        const uint32_t col = h->p.colorize != 0 ? 1u : 0u;
+        if (!h->lut_valid || h->lut_filter != h->p.filter_type || h->lut_col != col ||
+            !(h->lut_k == h->p.sigmoid_horizontal_scalar)) {
+            ALT_HIP(h, dips::launch_alt_lut_fill(h->lut_l2.as<uint16_t>(), h->lut_diffs.as<float>(),
+                                                 h->lut_slots.as<uint16_t>(), (uint32_t)ix.diffs.size(),
+                                                 h->p.filter_type, h->p.sigmoid_horizontal_scalar, col != 0, s));
+            h->lut_valid = true;
+            h->lut_filter = h->p.filter_type;
+            h->lut_col = col;
+            h->lut_k = h->p.sigmoid_horizontal_scalar;
+        }
+    }
+    return DIPS_OK;
+}
+
 // prev0 / prefiltered: frames and prev0 hold f32 intensities (chroma -1
 // kernel); otherwise prev0 = the slot of the frame before frames[0].
 dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags, uint8_t* out,
@@ -167,13 +292,23 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
     const bool pre = prev0 != nullptr;
     const int chroma = pre ? -1 : (int)h->p.chroma_filter;
     const bool fast = dips::alt_fast_epilogue_ok(h->p.filter_type, h->p.sigmoid_horizontal_scalar);
-    const void* k = dips::alt_batch_kernel_ptr(chroma, (int)h->p.filter_type, h->p.colorize != 0, fast);
+    // the epilogue-table kernel (default) or the per-pixel arithmetic one
+    // (DIPS_ALT_LUT=0: kept for A/B runs and as a cross-check in the tests)
+    bool lut = true;
+    if (const char* e = std::getenv("DIPS_ALT_LUT"))
+        if (e[0] == '0') lut = false;
+    const void* k = lut ? dips::alt_batch_lut_kernel_ptr(chroma)
+                        : dips::alt_batch_kernel_ptr(chroma, (int)h->p.filter_type, h->p.colorize != 0, fast);
     if (!k) return fail(h, DIPS_ERR_INVALID, "no batch kernel for these parameters");
-    int& occ = pre ? h->occupancy_pre : h->occupancy;
+    int& occ = lut ? (pre ? h->occupancy_lut_pre : h->occupancy_lut) : (pre ? h->occupancy_pre : h->occupancy);
     if (occ == 0) {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess || nb < 1) nb = 1;
         occ = nb;
+    }
+    if (lut) {
+        const dips_status st = ensure_lut(h, s);
+        if (st != DIPS_OK) return st;
     }
     const uint64_t n_vec = h->n_px() / 4u;
     const uint64_t n_tiles = (n_vec + 64u * dips::kUnrollAlt - 1) / (64u * dips::kUnrollAlt);
@@ -239,6 +374,8 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
     a.last_snap = last;
     a.scalar = h->p.sigmoid_horizontal_scalar;
     a.kneg_half = -h->p.sigmoid_horizontal_scalar * 0.5f;
+    a.lut_l1 = lut ? h->lut_l1.as<uint32_t>() : nullptr;
+    a.lut_l2 = lut ? h->lut_l2.as<uint16_t>() : nullptr;
     const uint32_t blocks = (uint32_t)((n_tiles * n_chunks + 3u) / 4u);
 
     const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
@@ -249,7 +386,10 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
         if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
         ALT_HIP(h, hipEventRecord(e0, s));
     }
-    ALT_HIP(h, dips::launch_alt_batch(a, chroma, (int)h->p.filter_type, h->p.colorize != 0, fast, blocks, s));
+    if (lut)
+        ALT_HIP(h, dips::launch_alt_batch_lut(a, chroma, blocks, s));
+    else
+        ALT_HIP(h, dips::launch_alt_batch(a, chroma, (int)h->p.filter_type, h->p.colorize != 0, fast, blocks, s));
     if (timing) {
         ALT_HIP(h, hipEventRecord(e1, s));
         h->ev_pending.emplace_back(e0, e1);
@@ -432,6 +572,10 @@ void dips_alt_destroy(dips_alt_handle* h) {
     for (auto& s : h->slots) s.release();
     for (auto& s : h->snap) s.release();
     h->filtered.release();
+    h->lut_l1.release();
+    h->lut_diffs.release();
+    h->lut_slots.release();
+    h->lut_l2.release();
     h->out1.release();
     h->pipe.release();
     h->pieces.release();
@@ -590,6 +734,27 @@ dips_status dips_alt_kernel_time_reset(dips_alt_handle* h) {
     if (st != DIPS_OK) return st;
     h->t_ms = 0.0;
     h->t_launches = 0;
+    return DIPS_OK;
+}
+
+dips_status dips_alt_lut_selfcheck(dips_alt_handle* h, uint64_t* mismatches) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!mismatches) return fail(h, DIPS_ERR_INVALID, "lut_selfcheck: null argument");
+    st = ensure_lut(h, h->stream);
+    if (st != DIPS_OK) return st;
+    DevBuf bad;
+    ALT_HIP(h, bad.ensure(sizeof(unsigned long long)));
+    ALT_HIP(h, hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), h->stream));
+    const hipError_t e = dips::launch_alt_lut_check(h->lut_l1.as<uint32_t>(), h->lut_l2.as<uint16_t>(),
+                                                    h->p.filter_type, h->p.sigmoid_horizontal_scalar,
+                                                    h->p.colorize != 0, bad.as<unsigned long long>(), h->stream);
+    unsigned long long n = 0;
+    hipError_t e2 = e == hipSuccess ? hipMemcpyAsync(&n, bad.p, sizeof(n), hipMemcpyDeviceToHost, h->stream) : e;
+    if (e2 == hipSuccess) e2 = hipStreamSynchronize(h->stream);
+    bad.release();
+    if (e2 != hipSuccess) return hip_fail(h, e2, "lut_selfcheck");
+    *mismatches = n;
     return DIPS_OK;
 }
 

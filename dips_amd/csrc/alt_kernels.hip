@@ -23,6 +23,7 @@
 // (one trailing zero inside the sorted range) and sorted(v)[8] for n = 16
 // (index 16 clamped to 15 by naga's Restrict policy).  Intensities are >= 0,
 // so for n = 2 it is min(v0, v1) and for n = 1 it is 0.
+#include "alt_lut.h"
 #include "epilogue_fast.h"
 #include "intensity_v2.h"
 #include "window_net.h"
@@ -215,10 +216,32 @@ __device__ __forceinline__ float unorm_fma(uint32_t c) {
     return __builtin_fmaf(f, kUnormHi, f * kUnormLo);
 }
 
+// The epilogue texel of diff from the LDS copy of the table (alt_lut.h):
+// level 1 by the cluster rint(510 * diff), level 2 by the cluster's shifted
+// diff bits.  diff must be one of the table's values (it is: u(S) - I).
+__device__ __forceinline__ uint32_t alt_lut_texel(const uint32_t* l1, const uint16_t* l2, float diff) {
+    const float t = __builtin_fmaf(diff, 510.0f, kAltLutRound);
+    const uint32_t a1 = (__float_as_uint(t) << 3) - kAltLutL1Bias;
+    const uint2 e = *reinterpret_cast<const uint2*>(reinterpret_cast<const char*>(l1) + a1);
+    const uint32_t a2 = ((__float_as_uint(diff) >> e.y) << 1) + e.x;
+    return lut_texel(*reinterpret_cast<const uint16_t*>(reinterpret_cast<const char*>(l2) + a2));
+}
+
 // FAST: the branch-free epilogue of epilogue_fast.h (sigmoid with |k| <= 160,
-// or no filter); otherwise the specification's visual_epilogue.
-template <int CH, int FILT, int COL, bool FAST, int U>
+// or no filter); otherwise the specification's visual_epilogue.  LUT: the
+// epilogue table of alt_lut.h in LDS instead (FILT / COL / FAST unused).
+template <int CH, int FILT, int COL, bool FAST, int U, bool LUT = false>
 __global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
+    __shared__ uint32_t lut1[LUT ? 2 * kAltLutClusters : 2];
+    __shared__ uint16_t lut2[LUT ? kAltLutL2Max : 2];
+    if constexpr (LUT) {
+        // every wave of the group helps fill the table, then waits for it
+        for (uint32_t i = threadIdx.x; i < 2u * kAltLutClusters; i += 256u) lut1[i] = a.lut_l1[i];
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(a.lut_l2);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(lut2);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)kAltLutL2Max / 2u; i += 256u) dst[i] = src[i];
+        __syncthreads();
+    }
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (item >= a.n_tiles * a.n_chunks) return;
@@ -307,7 +330,9 @@ __global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
             } else {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    if constexpr (FAST)
+                    if constexpr (LUT)
+                        o[q] = alt_lut_texel(lut1, lut2, snapf[u][q] - med[q]);
+                    else if constexpr (FAST)
                         o[q] = epilogue_fast<FILT, COL != 0>(snapf[u][q] - med[q], a.kneg_half);
                     else
                         o[q] = visual_epilogue(snapf[u][q] - med[q], (uint32_t)FILT, a.scalar, COL != 0);
@@ -395,7 +420,62 @@ const void* batch_ptr_c(int filter, bool colorize, bool fast) {
     }
 }
 
+__global__ __launch_bounds__(256) void alt_lut_fill_kernel(uint16_t* __restrict__ l2, const float* __restrict__ diffs,
+                                                           const uint16_t* __restrict__ slots, uint32_t n,
+                                                           uint32_t filter, float k, uint32_t colorize) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) l2[slots[i]] = (uint16_t)(visual_epilogue(diffs[i], filter, k, colorize != 0u) & 0xFFFFu);
+}
+
+// Exhaustive check of the table for the current properties: every snapshot
+// byte S and every byte pair (max, min) -- all intensities of every chroma
+// mode and of the prefiltered path -- through alt_lut_texel against the
+// specification's texel.  blockIdx.y = S.
+__global__ __launch_bounds__(256) void alt_lut_check_kernel(const uint32_t* __restrict__ l1,
+                                                            const uint16_t* __restrict__ l2, uint32_t filter, float k,
+                                                            uint32_t colorize, unsigned long long* __restrict__ bad) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;  // mx * 256 + mn
+    const uint32_t mx = p >> 8, mn = p & 0xFFu;
+    if (mn > mx) return;
+    const float diff = unorm_load(blockIdx.y) - intensity_rgb(mx, mn, mn, 0u);
+    const uint32_t want = visual_epilogue(diff, filter, k, colorize != 0u);
+    if (alt_lut_texel(l1, l2, diff) != want) atomicAdd(bad, 1ull);
+}
+
 }  // namespace
+
+hipError_t launch_alt_lut_check(const uint32_t* l1, const uint16_t* l2, uint32_t filter, float k, bool colorize,
+                                unsigned long long* bad, hipStream_t s) {
+    hipLaunchKernelGGL(alt_lut_check_kernel, dim3(256, 256), dim3(256), 0, s, l1, l2, filter, k, colorize ? 1u : 0u,
+                       bad);
+    return hipGetLastError();
+}
+
+const void* alt_batch_lut_kernel_ptr(int chroma) {
+    switch (chroma) {
+#define DIPS_ALT_LUT_CH(C) \
+    case C: return reinterpret_cast<const void*>(&alt_batch_kernel<C, 0, 0, true, kUnrollAlt, true>);
+        DIPS_ALT_LUT_CH(0) DIPS_ALT_LUT_CH(1) DIPS_ALT_LUT_CH(2) DIPS_ALT_LUT_CH(3) DIPS_ALT_LUT_CH(kAltPrefiltered)
+#undef DIPS_ALT_LUT_CH
+        default: return nullptr;
+    }
+}
+
+hipError_t launch_alt_batch_lut(const AltBatchArgs& a, int chroma, uint32_t blocks, hipStream_t s) {
+    const void* k = alt_batch_lut_kernel_ptr(chroma);
+    if (!k || blocks == 0 || !a.lut_l1 || !a.lut_l2) return hipErrorInvalidValue;
+    AltBatchArgs args = a;
+    void* params[] = {&args};
+    return hipLaunchKernel(k, dim3(blocks), dim3(256), params, 0, s);
+}
+
+hipError_t launch_alt_lut_fill(uint16_t* lut_l2, const float* diffs, const uint16_t* slots, uint32_t n,
+                               uint32_t filter, float k, bool colorize, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(alt_lut_fill_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, lut_l2, diffs, slots, n, filter,
+                       k, colorize ? 1u : 0u);
+    return hipGetLastError();
+}
 
 hipError_t launch_alt_frame(const AltArgs& a, hipStream_t s) {
     switch (a.n_tex) {

@@ -217,15 +217,6 @@ __global__ __launch_bounds__(256) void compat_lut_kernel(uint16_t* __restrict__ 
     lut[idx] = (uint16_t)(visual_epilogue(diff, filter, k, colorize != 0u) & 0xFFFFu);
 }
 
-// RGBA texel (R, G, min(R, G), 255) of a table entry R | G << 8: the u16
-// halves of (R, G, R, FF) and (R, G, G, FF) are equal in the low half and
-// (R | FF00, G | FF00) in the high one, so one packed u16 min finishes it.
-__device__ __forceinline__ uint32_t lut_texel(uint32_t e) {
-    const u16x2 x = as_u16x2(__builtin_amdgcn_perm(e, e, 0x0D000100u));
-    const u16x2 y = as_u16x2(__builtin_amdgcn_perm(e, e, 0x0D010100u));
-    return as_u32(umin(x, y));
-}
-
 constexpr int kLutWaves = (int)kCompatLutWaves;
 
 template <int CH, int U>

@@ -635,7 +635,6 @@ dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_
         a.lut = h->cb_lut.as<uint16_t>();
     }
     const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
-    dips_status st = DIPS_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing) {
         e0 = take_event(h);

@@ -136,6 +136,8 @@ struct AltBatchArgs {                // a run of frames, N = 2, W = 1
     int32_t last_snap;               // last snapshot frame of the batch or -1
     float scalar;                    // SIGMOID_HORIZONTAL_SCALAR k
     float kneg_half;                 // -k / 2 (fast epilogue)
+    const uint32_t* lut_l1;          // epilogue table (alt_lut.h): level-1 {x, sh} per cluster
+    const uint16_t* lut_l2;          //   and the u16 texel entries (LUT kernel only)
 };
 
 hipError_t launch_alt_frame(const AltArgs& a, hipStream_t s);
@@ -155,6 +157,15 @@ hipError_t launch_alt_filter_frames(const uint8_t* frames, float* dst, uint32_t 
                                    int32_t window, uint32_t chroma, hipStream_t s);
 hipError_t launch_alt_batch(const AltBatchArgs& a, int chroma, int filter, bool colorize, bool fast, uint32_t blocks,
                             hipStream_t s);
+// the epilogue-table form (alt_lut.h): any filter / k / colour, same outputs
+const void* alt_batch_lut_kernel_ptr(int chroma);
+hipError_t launch_alt_batch_lut(const AltBatchArgs& a, int chroma, uint32_t blocks, hipStream_t s);
+// lut_l2[slots[i]] = R | G << 8 of visual_epilogue(diffs[i], filter, k, colorize)
+// exhaustive table check over every (S, max, min): mismatches added to *bad
+hipError_t launch_alt_lut_check(const uint32_t* l1, const uint16_t* l2, uint32_t filter, float k, bool colorize,
+                                unsigned long long* bad, hipStream_t s);
+hipError_t launch_alt_lut_fill(uint16_t* lut_l2, const float* diffs, const uint16_t* slots, uint32_t n,
+                               uint32_t filter, float k, bool colorize, hipStream_t s);
 // the fast epilogue's preconditions (epilogue_fast.h): sigmoid with a scalar
 // k of |k| <= 160 (0 or |k| >= 2^-60 so -k/2 is exact), or no filter
 inline bool alt_fast_epilogue_ok(uint32_t filter, float k) {

@@ -66,6 +66,18 @@ __device__ __forceinline__ uint32_t pack_colour(uint32_t hi, uint32_t m, bool ne
     return __builtin_amdgcn_perm(hi, m, neg ? 0x0D000004u : 0x0D000400u);
 }
 
+// RGBA texel (R, G, min(R, G), 255) of an epilogue-table entry R | G << 8
+// (compat_batch_lut_kernel, alt_lut.h): visual_epilogue stores B = min(R, G)
+// and A = 255 (compat_batch.hip).  The u16 halves of (R, G, R, FF) and
+// (R, G, G, FF) are equal in the low half and (R | FF00, G | FF00) in the
+// high one, so one packed u16 min finishes it.
+__device__ __forceinline__ uint32_t lut_texel(uint32_t e) {
+    typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+    const us2 x = __builtin_bit_cast(us2, __builtin_amdgcn_perm(e, e, 0x0D000100u));
+    const us2 y = __builtin_bit_cast(us2, __builtin_amdgcn_perm(e, e, 0x0D010100u));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(x, y));
+}
+
 // visual_epilogue(diff, FILT, k, COL) for finite diff in [-1, 1] and, with
 // FILT = 0, |k| <= kFastSigmoidMaxK; kneg_half = -k / 2 (exact).
 // FILT = 1 (inverse sigmoid) is not handled here.

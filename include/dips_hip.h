@@ -287,6 +287,13 @@ dips_status dips_alt_snapshot_texture(dips_alt_handle *h, uint8_t *out_gray, siz
 dips_status dips_alt_kernel_time(dips_alt_handle *h, double *total_ms, uint64_t *launches);
 dips_status dips_alt_kernel_time_reset(dips_alt_handle *h);
 
+/* Self-check of the batch kernel's epilogue table (alt_lut.h) for the
+ * handle's properties: every snapshot byte against every (max, min) byte
+ * pair -- all pixel intensities of every chroma mode -- through the table and
+ * through the specification's epilogue; *mismatches = the count of texels
+ * that differ (0 expected).  Synchronous; for tests. */
+dips_status dips_alt_lut_selfcheck(dips_alt_handle *h, uint64_t *mismatches);
+
 #ifdef __cplusplus
 }
 #endif

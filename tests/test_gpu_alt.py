@@ -329,3 +329,47 @@ def test_replay_resume_matches_one_loop(n_tex, markers):
             assert np.array_equal(out.cpu().numpy(), want[t0:]), t0
         finally:
             c.close()
+
+
+LUT_SCALARS = [5.0, 1.0, 4.0, 10.0, 0.0, -3.0, 200.0, 1e-30, 1e30]
+
+
+@pytest.mark.parametrize("filt", [0, 1, 255])
+@pytest.mark.parametrize("colorize", [False, True])
+def test_lut_selfcheck_exhaustive(filt, colorize):
+    """The batch kernel's epilogue table (alt_lut.h) against the
+    specification's epilogue for EVERY snapshot byte x (max, min) byte pair
+    -- all 2,993 distinct diff values of every chroma mode and of the
+    prefiltered path -- on the device, for sensitivities inside and far
+    outside the setter's [1, 10] clamp (0, negative, huge, tiny)."""
+    from dips_amd.alt import DiPsCompute
+    for k in LUT_SCALARS:
+        c = DiPsCompute(2, 8, 8, _props(colorize, 1, k, filt, 0))
+        try:
+            assert c.lut_selfcheck() == 0, (filt, colorize, k)
+        finally:
+            c.close()
+
+
+@pytest.mark.parametrize("filt,colorize", list(itertools.product([0, 1, 255], [False, True])))
+@pytest.mark.parametrize("window,chroma", [(1, 0), (1, 2), (1, 3), (3, 0), (5, 1)])
+def test_batch_lut_equals_arithmetic_and_oracle(filt, colorize, window, chroma, monkeypatch):
+    """alt_batch_kernel with the epilogue table (default) against its
+    per-pixel arithmetic form (DIPS_ALT_LUT=0) and the oracle's run loop, on
+    random frames with snapshots, W = 1 (RGBA8 frames) and W > 1
+    (prefiltered intensities)."""
+    from dips_amd.alt import DiPsRunner
+    w, h = 72, 40
+    frames = _frames(w, h, 36, 500 + filt + 7 * chroma + window)
+    markers = [4, 5, 20]
+    outs = {}
+    for lut in ("1", "0"):
+        monkeypatch.setenv("DIPS_ALT_LUT", lut)
+        r = DiPsRunner(h, w, _props(colorize, window, 4.0, filt, chroma), markers)
+        try:
+            outs[lut] = r(frames)
+        finally:
+            r.close()
+    assert np.array_equal(outs["1"], outs["0"]), np.argwhere(outs["1"] != outs["0"])[:4]
+    want = oracle.AltCompute(2, w, h, colorize, window, 4.0, filt, chroma).run(frames, markers)
+    assert np.array_equal(outs["1"], want), np.argwhere(outs["1"] != want)[:4]

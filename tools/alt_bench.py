@@ -38,7 +38,10 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=10)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "alt_pmc_traffic.json"),
                     help="HBM traffic per launch measured by profiles/collect_alt_pmc.sh")
+    ap.add_argument("--kernel", choices=["lut", "arith"], default="lut",
+                    help="lut: alt_batch_kernel with the epilogue table (default); arith: per-pixel epilogue")
     args = ap.parse_args()
+    os.environ["DIPS_ALT_LUT"] = "1" if args.kernel == "lut" else "0"
 
     import torch
     from dips_amd import DiffSeriesOperator, PixelFormat
@@ -99,7 +102,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      **({"traffic_source": traffic_src} if traffic_src else {}),
-                     "kernel": "alt_batch_kernel<0,0,1,true,2>",
+                     "kernel": ("alt_batch_kernel<0,0,0,true,2,LUT=true> (epilogue table in LDS)"
+                                if args.kernel == "lut" else "alt_batch_kernel<0,0,1,true,2> (arithmetic epilogue)"),
                      "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": algo},
         "cpu_baseline": {"value": round(n_cpu / cpu_s, 4), "unit": "frames/s", "cores": 1, "kind": "port",
                          "sample": f"first {n_cpu} frames, oracle/dips_oracle.c DiPsCompute, {cpu_s:.2f} s",
