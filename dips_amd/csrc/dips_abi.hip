@@ -81,6 +81,10 @@ struct dips_handle {
     dips_host::PieceEvents up_pieces;  // per-stripe upload completion (striped frame_callback)
     HostPinned io_out;                 // readback staging of the striped frame_callback
     int cb_occupancy = 0;
+    DevBuf gray_lut;          // T_d / T_c tables of series_gray_lut_kernel (128 KiB) for gray_lut_tau
+    bool gray_lut_valid = false;
+    float gray_lut_tau = 0.0f;
+    int gray_lut_layout = 0;
     DevBuf cb_lut;            // epilogue table of compat_batch_lut_kernel (128 KiB)
     bool cb_lut_valid = false;
     uint32_t cb_lut_filter = 0, cb_lut_col = 0;
@@ -196,6 +200,53 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
     return g;
 }
 
+// GRAY8 runs on the table kernel (series_gray.hip) unless DIPS_GRAY_LUT=0
+// (the f32 kernel series_fast_kernel; kept for A/B runs and as a cross-check).
+// table layout: 1 two byte tables, 2 one u16 table, 0 off (DIPS_GRAY_LUT)
+int gray_lut_layout() {
+    if (const char* e = std::getenv("DIPS_GRAY_LUT")) {
+        if (e[0] == '0') return 0;
+        if (e[0] == '1') return 1;
+    }
+    return 2;
+}
+bool gray_lut_enabled() { return gray_lut_layout() != 0; }
+
+FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames) {
+    FastGeom g;
+    const uint64_t npx = (uint64_t)width * height;
+    const uint64_t nvec = npx / 16u;
+    if (nvec == 0 || npx >= (1ull << 31) || n_frames == 0) return g;
+    const uint64_t U = (uint64_t)dips::kUnrollGrayLut;
+    g.vec_bytes = nvec * 16u;
+    g.tail_px0 = nvec * 16u;
+    g.n_tiles = (nvec + 64 * U - 1) / (64 * U);
+    g.items = g.n_tiles * n_frames;
+    // one 1024-thread group per CU (the tables fill its LDS): 4 waves per SIMD
+    uint64_t per_simd = dips::kGrayLutWaves / 4u;
+    if (const char* cap = std::getenv("DIPS_SERIES_WAVES_PER_SIMD")) {
+        const unsigned long c = std::strtoul(cap, nullptr, 10);
+        if (c >= 1 && c < per_simd) per_simd = c;
+    }
+    const uint64_t resident = per_simd * 4u * (uint64_t)h->cu_count;
+    g.n_waves = g.items < resident ? g.items : resident;
+    g.blocks = (g.n_waves + dips::kGrayLutWaves - 1) / dips::kGrayLutWaves;
+    g.ok = g.n_tiles < (1ull << 32) && g.blocks < (1ull << 31);
+    return g;
+}
+
+// The T_d / T_c tables of the GRAY8 table kernel for the handle's tau.
+dips_status ensure_gray_lut(dips_handle* h, hipStream_t s) {
+    const int layout = gray_lut_layout();
+    if (h->gray_lut_valid && h->gray_lut_tau == h->p.tau && h->gray_lut_layout == layout) return DIPS_OK;
+    DIPS_HIP(h, h->gray_lut.ensure(dips::kGrayLutBytes));
+    DIPS_HIP(h, dips::launch_gray_lut(h->gray_lut.as<uint8_t>(), h->p.tau, layout, s));
+    h->gray_lut_valid = true;
+    h->gray_lut_tau = h->p.tau;
+    h->gray_lut_layout = layout;
+    return DIPS_OK;
+}
+
 // Run the series on device pointers, asynchronously on `s`.
 dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
                               uint32_t n_frames, const uint8_t* ref0, dips_series_entry* series, uint8_t* map,
@@ -207,7 +258,10 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     DIPS_HIP(h, hipMemsetAsync(series, 0, sizeof(dips_series_entry) * (size_t)n_frames, s));
 
     FastGeom g;
-    if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC)) g = fast_geometry(h, width, height, n_frames, C, pf, map != nullptr);
+    const bool glut = C == 1 && gray_lut_enabled();
+    if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC))
+        g = glut ? gray_lut_geometry(h, width, height, n_frames)
+                 : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr);
     auto launch_generic = [&](uint64_t px0) -> dips_status {
         const uint64_t bpf = (npx - px0 + 255u) / 256u;
         if (bpf * (uint64_t)n_frames >= (1ull << 31))
@@ -236,8 +290,12 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         e0 = take_event(h);
         e1 = take_event(h);
         if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
-        DIPS_HIP(h, hipEventRecord(e0, s));
     }
+    if (g.ok && glut) {
+        st = ensure_gray_lut(h, s);  // before e0: the table is not part of the series launch
+        if (st != DIPS_OK) return st;
+    }
+    if (timing) DIPS_HIP(h, hipEventRecord(e0, s));
     if (g.ok) {
         DIPS_HIP(h, h->partials.ensure((size_t)g.items * 16u));
         dips::SeriesArgs a{};
@@ -252,8 +310,13 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         a.n_tiles = (uint32_t)g.n_tiles;
         a.n_waves = (uint32_t)g.n_waves;
         a.thr = dips::series_threshold(C, h->p.tau);
-        DIPS_HIP(h, dips::launch_series_fast(a, C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map != nullptr,
-                                             (uint32_t)g.blocks, s));
+        if (glut) {
+            a.lut = h->gray_lut.p;
+            DIPS_HIP(h, dips::launch_series_gray_lut(a, pf, map != nullptr, h->gray_lut_layout, (uint32_t)g.blocks, s));
+        } else {
+            DIPS_HIP(h, dips::launch_series_fast(a, C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map != nullptr,
+                                                 (uint32_t)g.blocks, s));
+        }
         // the ragged tail (< pixels_per_vec pixels per frame): its sums go
         // straight into the series by atomics, so the order is free
         if (g.tail_px0 < npx) {
@@ -269,7 +332,8 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         h->ev_pending.emplace_back(e0, e1);
     }
     if (g.ok)
-        DIPS_HIP(h, dips::launch_series_reduce(h->partials.as<uint64_t>(), n_frames, (uint32_t)g.n_tiles, C == 1, series, s));
+        DIPS_HIP(h, dips::launch_series_reduce(h->partials.as<uint64_t>(), n_frames, (uint32_t)g.n_tiles,
+                                               C == 1 ? (glut ? 2 : 1) : 0, series, s));
     return DIPS_OK;
 }
 
@@ -377,6 +441,7 @@ void dips_destroy(dips_handle* h) {
     h->raw.release();
     h->filtered.release();
     h->cb_lut.release();
+    h->gray_lut.release();
     h->start.release();
     h->out.release();
     h->io.release();
@@ -1019,7 +1084,9 @@ dips_status dips_series_geometry(dips_handle* h, uint32_t width, uint32_t height
     dips_status st = bind(h);
     if (st != DIPS_OK) return st;
     const int C = (int)h->p.format;
-    FastGeom g = fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false);
+    FastGeom g = C == 1 && gray_lut_enabled()
+                     ? gray_lut_geometry(h, width, height, n_frames)
+                     : fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false);
     if (waves) *waves = g.ok ? g.n_waves : 0;
     if (tiles) *tiles = g.ok ? g.n_tiles : 0;
     if (partial_bytes) *partial_bytes = g.ok ? g.n_tiles * 16u : 0;

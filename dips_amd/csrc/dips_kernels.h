@@ -12,6 +12,12 @@ namespace dips {
 constexpr int kUnrollRGB = 4;   // 1024 px / wave / frame for RGB8 and RGBA8
 constexpr int kUnrollGray = 2;  // 2048 px / wave / frame for GRAY8
 constexpr int kUnrollV2 = 4;    // series_v2_kernel (RGB8/RGBA8): 1024 px / wave / frame
+#ifndef DIPS_UNROLL_GRAY_LUT
+#define DIPS_UNROLL_GRAY_LUT 2
+#endif
+constexpr int kUnrollGrayLut = DIPS_UNROLL_GRAY_LUT;  // series_gray_lut_kernel: 64 * 16 * U px / wave / frame
+constexpr uint32_t kGrayLutWaves = 16;  // its waves per workgroup (one 1024-thread group per CU)
+constexpr size_t kGrayLutBytes = 131072;  // its T_d / T_c tables
 // Prefetch depth: frames of loads each wave keeps in flight.
 #ifndef DIPS_DEPTH_RGB
 #define DIPS_DEPTH_RGB 2
@@ -35,6 +41,7 @@ struct SeriesArgs {
     uint32_t n_tiles;
     uint32_t n_waves;
     float thr;               // threshold in kernel units: series_threshold()
+    const void* lut;         // GRAY8 table kernel: T_d / T_c bytes (series_gray.hip), 128 KiB
 };
 
 struct GenericArgs {
@@ -183,8 +190,14 @@ const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool 
 float series_threshold(int channels, float tau);
 hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, bool per_frame, bool map,
                               uint32_t blocks, hipStream_t s);
-hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, bool gray,
+// record layout: 0 RGB(A), 1 gray (series_fast_kernel), 2 gray table kernel (series_gray_lut_kernel)
+hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
                                 dips_series_entry* series, hipStream_t s);
+// GRAY8 table kernel, table layout 1 (two byte tables) or 2 (one u16 table)
+const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout);
+hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s);
+hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
+                                  hipStream_t s);
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
 hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, hipStream_t s);

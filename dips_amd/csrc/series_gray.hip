@@ -1,0 +1,259 @@
+// series_gray.hip -- the GRAY8 series kernel with the per-pixel statistics
+// as a table (series_gray_lut_kernel).
+//
+// For one gray byte pair (a = the frame's, b = the reference's) everything
+// the series needs is a function of (a, b) alone: with u(c) = c / 255
+// correctly rounded, dI = |RN(u(a) - u(b))| (dips_shader.wgsl:64-82 with
+// the three channels equal), the pixel is counted when dI > tau, and its
+// contribution to SI_fixed = sum dI * 2^32 is 2 V with V = dI * 2^31, an
+// integer.  Exhaustively over all 65,536 pairs (tests/test_oracle.py::
+// test_gray_si_decomposition):
+//     V = 8421504 * d + corr,   d = |a - b|,   corr in {0, 1, 2, 4, ..., 128}
+// (u(c) * 2^31 = 8421504 c + P(c) exactly, 8421504 = 65793 * 2^7 and P(c)
+// the largest power of two <= c, series_v2.hip; the f32 rounding of the
+// difference leaves a non-negative power-of-two remainder).  So per selected pixel the
+// kernel needs d and corr, each one byte, and per frame
+//     SI_fixed = 2 (8421504 * sum d + sum corr),   count = #selected.
+// gray_lut_kernel writes two byte tables for the current tau,
+//     T_d[a * 256 + b] = selected ? d : 0,   T_c[...] = selected ? corr : 0,
+// and the series kernel keeps both (128 KiB) in LDS, one 1024-thread group
+// per CU.  Per pixel: the table index from one v_perm_b32 per two pixels
+// (a, b bytes of the same position side by side), two ds_read_u8 into the
+// low and high halves of one register (d | corr << 16), one add into a
+// packed per-lane accumulator (sum d and sum corr stay below 2^16 for the
+// 32 pixels a lane sees per frame), and one compare whose mask the scalar
+// unit counts.  No f32, no f64: the exact f32 arithmetic of the reference is
+// folded into the table.  SAD is the byte SAD as before and SJ = 2 SAD.
+//
+// Records: {SAD, sum d, sum corr, count} per (tile, frame); series_reduce
+// (mode 2) forms SI_fixed = 2 (8421504 sum d + sum corr) in 64 bits.
+#include "series_common.h"
+
+namespace dips {
+
+constexpr uint32_t kGrayLutTcOffset = 65535u;  // T_c's byte offset in LDS (the ds offset field's maximum;
+                                               // T_d[65535] and T_c[0] share a byte: both are 0, a == b)
+constexpr uint32_t kGrayV = 8421504u;          // V = kGrayV * d + corr
+
+// The tables for threshold tau (65,536 spec evaluations), 131,072 bytes:
+// layout 1 -- T_d at byte 0 and T_c at byte kGrayLutTcOffset;
+// layout 2 -- one u16 table, entry d | corr << 8 at byte 2 idx.
+__global__ __launch_bounds__(256) void gray_lut_kernel(uint8_t* __restrict__ tab, float tau, uint32_t layout) {
+    const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t a = idx >> 8, b = idx & 0xFFu;
+    const float di = fabsf(unorm_load(a) - unorm_load(b));
+    const bool sel = di > tau;
+    const uint64_t v = (uint64_t)((double)di * 2147483648.0);  // exact: di is a multiple of 2^-31
+    const uint32_t d = a > b ? a - b : b - a;
+    const uint32_t corr = (uint32_t)(v - (uint64_t)kGrayV * d);  // in [0, 128] (exhaustive test)
+    if (layout == 2u) {
+        reinterpret_cast<uint16_t*>(tab)[idx] = sel ? (uint16_t)(d | corr << 8) : (uint16_t)0;
+    } else {
+        tab[idx] = sel ? (uint8_t)d : (uint8_t)0;
+        if (idx != 0u) tab[kGrayLutTcOffset + idx] = sel ? (uint8_t)corr : (uint8_t)0;
+    }
+}
+
+namespace {
+
+constexpr int kGrayWaves = 16;  // waves per workgroup (one group per CU holds the table)
+
+// Records of frames t, t+1 from their 8 reduced values (lanes 8v hold v);
+// the wave-wide counts go into value 3 (lanes 24 and 56).
+__device__ __forceinline__ void gstore_pair(__amdgpu_buffer_rsrc_t rpart, uint32_t t, uint32_t rec_off8, uint32_t lane,
+                                            uint32_t y, uint32_t cnt0, uint32_t cnt1) {
+    const uint32_t add = lane == 24u ? cnt0 : (lane == 56u ? cnt1 : 0u);
+    __builtin_amdgcn_raw_buffer_store_b32(y + add, rpart, rec_off8, t * 16u, 0);
+}
+
+__device__ __forceinline__ void gstore_one(__amdgpu_buffer_rsrc_t rpart, uint32_t t, uint32_t rec_off4, uint32_t lane,
+                                           uint32_t y, uint32_t cnt) {
+    const uint32_t add = lane == 48u ? cnt : 0u;
+    __builtin_amdgcn_raw_buffer_store_b32(y + add, rpart, rec_off4, t * 16u, 0);
+}
+
+// One frame of one tile against the reference bytes rb: the 4 per-lane
+// values {SAD, sum d, sum corr, 0} and the wave-wide count.
+template <int U, bool MAP, int LAYOUT>
+__device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* lds, const uint32_t (&rb)[U][4],
+                                           const uint32_t (&cur)[U][4], uint32_t voff, uint32_t t, uint32_t* vals,
+                                           uint32_t& cnt) {
+    uint32_t sad = 0, acc = 0, accd = 0, accc = 0, c = 0;
+    uint32_t map[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t f = cur[u][k], r = rb[u][k];
+            sad = __builtin_amdgcn_sad_u8(f, r, sad);
+            if constexpr (MAP) map[u][k] = absdiff_bytes(f, r);
+            // table indices f_i * 256 + r_i of pixels (0, 2) and (1, 3) as u16 pairs
+            const uint32_t i02 = __builtin_amdgcn_perm(f, r, 0x06020400u);
+            const uint32_t i13 = __builtin_amdgcn_perm(f, r, 0x07030501u);
+            if constexpr (LAYOUT == 2) {
+                // one u16 entry d | corr << 8 per pixel; two pixels' entries in
+                // one register, their d and corr summed by two v_dot4_u32_u8
+                const uint16_t* t16 = reinterpret_cast<const uint16_t*>(lds);
+                const uint32_t r02 = (uint32_t)t16[i02 & 0xFFFFu] | ((uint32_t)t16[i02 >> 16] << 16);
+                const uint32_t r13 = (uint32_t)t16[i13 & 0xFFFFu] | ((uint32_t)t16[i13 >> 16] << 16);
+                accd = __builtin_amdgcn_udot4(r02, 0x00010001u, accd, false);
+                accd = __builtin_amdgcn_udot4(r13, 0x00010001u, accd, false);
+                accc = __builtin_amdgcn_udot4(r02, 0x01000100u, accc, false);
+                accc = __builtin_amdgcn_udot4(r13, 0x01000100u, accc, false);
+                c += (uint32_t)__builtin_popcountll(__ballot((r02 & 0xFFFFu) != 0u)) +
+                     (uint32_t)__builtin_popcountll(__ballot(r02 > 0xFFFFu)) +
+                     (uint32_t)__builtin_popcountll(__ballot((r13 & 0xFFFFu) != 0u)) +
+                     (uint32_t)__builtin_popcountll(__ballot(r13 > 0xFFFFu));
+            } else {
+                const uint32_t ix[4] = {i02 & 0xFFFFu, i13 & 0xFFFFu, i02 >> 16, i13 >> 16};
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+                    const uint32_t e = (uint32_t)lds[ix[p]] | ((uint32_t)lds[kGrayLutTcOffset + ix[p]] << 16);
+                    acc += e;
+                    c += (uint32_t)__builtin_popcountll(__ballot(e != 0u));
+                }
+            }
+        }
+    }
+    if constexpr (LAYOUT == 2) acc = accd | (accc << 16);  // both < 2^16 (32 px per lane and frame)
+    if constexpr (MAP) {
+        const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.vec_bytes);
+#pragma unroll
+        for (int u = 0; u < U; ++u) store_vec<1>(rm, voff + (uint32_t)(u * 64 * 16), map[u]);
+    }
+    vals[0] = sad;
+    vals[1] = acc & 0xFFFFu;
+    vals[2] = acc >> 16;
+    vals[3] = 0u;
+    cnt = c;
+}
+
+template <int U, bool PF, bool MAP, int LAYOUT>
+__global__ __launch_bounds__(64 * kGrayWaves) void series_gray_lut_kernel(SeriesArgs a) {
+    __shared__ uint32_t lds32[32768];  // T_d at byte 0, T_c at byte kGrayLutTcOffset
+    {
+        const u32x4* src = reinterpret_cast<const u32x4*>(a.lut);
+        u32x4* dst = reinterpret_cast<u32x4*>(lds32);
+        for (uint32_t i = threadIdx.x; i < 8192u; i += 64u * kGrayWaves) dst[i] = src[i];
+    }
+    __syncthreads();
+    const uint8_t* lds = reinterpret_cast<const uint8_t*>(lds32);
+    static_assert(U * 64 * 16 <= 4096, "vec offsets must fit the 12-bit immediate");
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)kGrayWaves + (threadIdx.x >> 6));
+    if (wave >= a.n_waves) return;
+    const uint32_t fb = a.frame_bytes, vb = a.vec_bytes;
+    const uint32_t rec_off8 = (lane & 7u) == 0u ? (lane >> 5) * 16u + ((lane >> 3) & 3u) * 4u : 0x80000000u;
+    const uint32_t rec_off4 = (lane & 15u) == 0u ? (lane >> 4) * 4u : 0x80000000u;
+
+    uint64_t i = (uint64_t)wave * a.items / a.n_waves;
+    const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
+    while (i < iend) {
+        const uint32_t tile = (uint32_t)(i / a.n_frames);
+        const uint32_t t0 = (uint32_t)(i - (uint64_t)tile * a.n_frames);
+        const uint64_t remaining = iend - i;
+        const uint32_t tend =
+            (uint32_t)((uint64_t)a.n_frames < t0 + remaining ? (uint64_t)a.n_frames : t0 + remaining);
+        i += tend - t0;
+        const uint32_t n = tend - t0;
+        const uint32_t tlast = tend - 1;
+        const uint32_t voff = (tile * U * 64u + lane) * 16u;
+        const __amdgpu_buffer_rsrc_t rpart =
+            make_rsrc(a.partials + 2 * (uint64_t)tile * a.n_frames, a.n_frames * 16u);
+
+        auto load_frame = [&](uint32_t tf, uint32_t (&dst)[U][4]) {
+            const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)min(tf, tlast) * fb, vb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) load_vec<1>(r, voff + (uint32_t)(u * 64 * 16), dst[u]);
+        };
+
+        // ring as in series_v2_kernel: PF -- frame k of the segment in slot
+        // (k+1)&3, its reference in slot k&3; overall -- frame k in slot k&3
+        uint32_t buf[4][U][4];
+        uint32_t rb[U][4];
+        {
+            const uint8_t* rp = PF ? (t0 == 0 ? a.ref0 : a.frames + (uint64_t)(t0 - 1) * fb) : a.ref0;
+            const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, vb);
+            uint32_t (&dref)[U][4] = PF ? buf[0] : rb;
+#pragma unroll
+            for (int u = 0; u < U; ++u) load_vec<1>(rr, voff + (uint32_t)(u * 64 * 16), dref[u]);
+            if constexpr (PF) {
+                load_frame(t0, buf[1]);
+                load_frame(t0 + 1, buf[2]);
+                load_frame(t0 + 2, buf[3]);
+            } else {
+                load_frame(t0, buf[0]);
+                load_frame(t0 + 1, buf[1]);
+                load_frame(t0 + 2, buf[2]);
+                load_frame(t0 + 3, buf[3]);
+            }
+        }
+
+        uint32_t k = 0;
+        for (; k + 4 <= n; k += 4) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint32_t v[8], c0, c1;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int j = 2 * h + q;
+                    const uint32_t tf = t0 + k + (uint32_t)j;
+                    if constexpr (PF) {
+                        gray_frame<U, MAP, LAYOUT>(a, lds, buf[j], buf[(j + 1) & 3], voff, tf, v + 4 * q, q ? c1 : c0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        load_frame(tf + 3, buf[j]);
+                    } else {
+                        gray_frame<U, MAP, LAYOUT>(a, lds, rb, buf[j], voff, tf, v + 4 * q, q ? c1 : c0);
+                        __builtin_amdgcn_sched_barrier(0);
+                        load_frame(tf + 4, buf[j]);
+                    }
+                }
+                const uint32_t y = wave_sum8_lanes(v, lane);
+                gstore_pair(rpart, t0 + k + 2 * h, rec_off8, lane, y, c0, c1);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if (k + (uint32_t)j < n) {
+                uint32_t v[4], c;
+                const uint32_t tf = t0 + k + (uint32_t)j;
+                if constexpr (PF)
+                    gray_frame<U, MAP, LAYOUT>(a, lds, buf[j], buf[j + 1], voff, tf, v, c);
+                else
+                    gray_frame<U, MAP, LAYOUT>(a, lds, rb, buf[j], voff, tf, v, c);
+                const uint32_t y = wave_sum4_lanes(v);
+                gstore_one(rpart, tf, rec_off4, lane, y, c);
+            }
+        }
+    }
+}
+
+}  // namespace
+
+template <int L>
+static const void* gray_ptr(bool per_frame, bool map) {
+    return per_frame ? (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, true, true, L>)
+                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, true, false, L>))
+                     : (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, false, true, L>)
+                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, false, false, L>));
+}
+
+const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout) {
+    return layout == 2 ? gray_ptr<2>(per_frame, map) : gray_ptr<1>(per_frame, map);
+}
+
+hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
+    hipLaunchKernelGGL(gray_lut_kernel, dim3(256), dim3(256), 0, s, tab, tau, (uint32_t)layout);
+    return hipGetLastError();
+}
+
+hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
+                                  hipStream_t s) {
+    const void* k = series_gray_lut_kernel_ptr(per_frame, map, layout);
+    if (!k || !a.lut || blocks == 0) return hipErrorInvalidValue;
+    SeriesArgs args = a;
+    void* params[] = {&args};
+    return hipLaunchKernel(k, dim3(blocks), dim3(64 * kGrayWaves), params, 0, s);
+}
+
+}  // namespace dips

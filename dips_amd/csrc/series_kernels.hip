@@ -301,9 +301,11 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 // four wave sums of one (tile, frame):
 //   RGB(A): {SAD, SJ + count << 20, H, L}     SI_fixed = H << 15 + L
 //   gray:   {SAD + count << 20, H, L, 0}      SI_fixed = H << 16 + L, SJ = 2 SAD
+//   gray table kernel: {SAD, sum d, sum corr, count}
+//                                             SI_fixed = 2 (8421504 sum d + sum corr), SJ = 2 SAD
 // (H, L: the split of the exact per-lane fixed-point intensity sum).
 __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __restrict__ partials, uint32_t n_frames,
-                                                            uint32_t n_tiles, uint32_t tiles_per_block, uint32_t gray,
+                                                            uint32_t n_tiles, uint32_t tiles_per_block, uint32_t layout,
                                                             dips_series_entry* __restrict__ series) {
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
     if (t >= n_frames) return;
@@ -313,7 +315,12 @@ __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __re
     int64_t l = 0;
     for (uint32_t tile = tile0; tile < tile1; ++tile) {
         const u32x4 rec = *reinterpret_cast<const u32x4*>(partials + 2 * ((uint64_t)tile * n_frames + t));
-        if (gray) {
+        if (layout == 2u) {
+            sad += rec.x;
+            h += rec.y;  // sum d
+            l += rec.z;  // sum corr
+            cnt += rec.w;
+        } else if (layout == 1u) {
             sad += rec.x & 0xFFFFFu;
             cnt += rec.x >> 20;
             h += rec.y;
@@ -326,8 +333,8 @@ __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __re
             l += (int64_t)(int32_t)rec.w;
         }
     }
-    if (gray) sj = 2u * sad;
-    const uint64_t sif = (h << (gray ? 16 : 15)) + (uint64_t)l;
+    if (layout != 0u) sj = 2u * sad;
+    const uint64_t sif = layout == 2u ? 2u * (8421504u * h + (uint64_t)l) : (h << (layout == 1u ? 16 : 15)) + (uint64_t)l;
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].sad), (unsigned long long)sad);
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].sj), (unsigned long long)sj);
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].count), (unsigned long long)cnt);
@@ -543,11 +550,11 @@ hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, boo
     return hipLaunchKernel(k, dim3(blocks), dim3(256), params, 0, s);
 }
 
-hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, bool gray,
+hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
                                 dips_series_entry* series, hipStream_t s) {
     const uint32_t tpb = 64;
     dim3 grid((n_frames + 255u) / 256u, (n_tiles + tpb - 1u) / tpb);
-    hipLaunchKernelGGL(series_reduce_kernel, grid, dim3(256), 0, s, partials, n_frames, n_tiles, tpb, gray ? 1u : 0u,
+    hipLaunchKernelGGL(series_reduce_kernel, grid, dim3(256), 0, s, partials, n_frames, n_tiles, tpb, (uint32_t)layout,
                        series);
     return hipGetLastError();
 }

@@ -316,3 +316,26 @@ def test_tau_boundary_fixtures_straddle_tau():
             counts.append(out4[1, 2])
         assert counts[0] > counts[1] > counts[2], (case["file"], counts)
         assert z["out4"][1, 2] == counts[1]
+
+
+def test_gray_si_decomposition():
+    """The identity behind series_gray_lut_kernel (dips_amd/csrc/series_gray.hip),
+    exhaustively over all 65,536 gray byte pairs (a, b): with u(c) = c / 255
+    correctly rounded, V = |RN(u(a) - u(b))| * 2^31 is an integer and
+    V = 8421504 * |a - b| + corr with corr in {0, 1, 2, 4, ..., 128}, so a
+    selected pixel's SI_fixed contribution 2 V is carried exactly by the two
+    bytes (|a - b|, corr) of its table entry."""
+    F32 = np.float32
+    u = (np.arange(256, dtype=np.float64) / 255.0).astype(F32)
+    a, b = np.meshgrid(np.arange(256), np.arange(256), indexing="ij")
+    di = np.abs((u[a] - u[b]).astype(F32)).astype(np.float64)
+    v = di * 2.0 ** 31
+    assert np.all(v == np.floor(v))
+    v = v.astype(np.int64)
+    d = np.abs(a - b)
+    corr = v - 8421504 * d
+    assert set(np.unique(corr).tolist()) <= {0, 1, 2, 4, 8, 16, 32, 64, 128}
+    # the oracle's f32 dI is the same value: SI_fixed of a selected pixel = 2 V
+    frames = np.stack([b.astype(np.uint8), a.astype(np.uint8)])  # reference b, then frame a
+    out4, _, _ = oracle.series(frames, mode=1, tau=0.0)
+    assert int(out4[1, 3]) == int(2 * v.sum())

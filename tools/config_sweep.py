@@ -34,13 +34,20 @@ CONFIGS = [
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--only", default="", help="run the configs whose name contains this string")
+    ap.add_argument("--gray-kernel", choices=["lut16", "lut8", "f32"], default="lut16",
+                    help="GRAY8: series_gray_lut_kernel with the u16 table (default) or the two byte "
+                         "tables, or the f32 series_fast_kernel")
     args = ap.parse_args()
+    os.environ["DIPS_GRAY_LUT"] = {"lut16": "2", "lut8": "1", "f32": "0"}[args.gray_kernel]
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     from oracle import oracle
 
     dev = torch.device("cuda", 0)
     for name, W, H, C, F, mode, tau in CONFIGS:
+        if args.only and args.only not in name:
+            continue
         shape = (F, H, W) if C == 1 else (F, H, W, C)
         frames = torch.empty(shape, dtype=torch.uint8, device=dev)
         op = DiffSeriesOperator(PixelFormat(C), Mode(mode), tau, time_kernel=True)
@@ -60,7 +67,8 @@ def main():
         want, _, _ = oracle.series(host, mode=mode, tau=tau, nthreads=8)
         ok = bool(np.array_equal(series[:3].cpu().numpy().view(np.uint64), want))
         fb = W * H * C
-        print(json.dumps({"config": name, "frames_per_s": round(F / wall, 1),
+        print(json.dumps({"config": name, **({"gray_kernel": args.gray_kernel} if C == 1 else {}),
+                          "frames_per_s": round(F / wall, 1),
                           "kernel_ms": round(kms, 4), "kernel_GBps": round(F * fb / (kms / 1e3) / 1e9, 1),
                           "frac_of_8TBps": round(F * fb / (kms / 1e3) / 8e12, 4),
                           "first_frames_match_oracle": ok}), flush=True)

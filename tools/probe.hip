@@ -162,7 +162,7 @@ int main(int argc, char** argv) {
         vs.push_back({"series<U=" #U ",D=" #D ",PF=" #PF "> occ=" + std::to_string(occ) + " waves=" +  \
                           std::to_string(a.n_waves),                                                  \
                       [=]() { hipLaunchKernelGGL((series_fast_kernel<3, 0, U, D, PF, false>), dim3(blocks), dim3(256), 0, 0, a); \
-                              CK(launch_series_reduce(partials, F, a.n_tiles, false, series, 0)); }, {}, "PF=" #PF " tau=8.0f"}); \
+                              CK(launch_series_reduce(partials, F, a.n_tiles, 0, series, 0)); }, {}, "PF=" #PF " tau=8.0f"}); \
     }
 #define SERIES_V2U(PF, U) SERIES_V2X(PF, U, 8.0f)
 #define SERIES_V2X(PF, U, TAU255)                                                                             \
@@ -174,7 +174,7 @@ int main(int argc, char** argv) {
         a.thr = series_threshold(3, TAU255 / 255.0f);                                                 \
         vs.push_back({"v2<U=" #U ",PF=" #PF "> tau=" #TAU255 "/255 occ=" + std::to_string(occ) + " waves=" + std::to_string(a.n_waves), \
                       [=]() { hipLaunchKernelGGL((series_v2_kernel<3, 0, U, PF, false>), dim3(blocks), dim3(256), 0, 0, a); \
-                              CK(launch_series_reduce(partials, F, a.n_tiles, false, series, 0)); }, {}, "PF=" #PF " tau=" #TAU255}); \
+                              CK(launch_series_reduce(partials, F, a.n_tiles, 0, series, 0)); }, {}, "PF=" #PF " tau=" #TAU255}); \
     }
 #define SERIES_V2(PF) SERIES_V2U(PF, kUnrollV2)
     SERIES(4, 2, true)
