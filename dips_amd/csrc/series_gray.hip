@@ -94,8 +94,10 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
                 // one u16 entry d | corr << 8 per pixel; two pixels' entries in
                 // one register, their d and corr summed by two v_dot4_u32_u8
                 const uint16_t* t16 = reinterpret_cast<const uint16_t*>(lds);
-                const uint32_t r02 = (uint32_t)t16[i02 & 0xFFFFu] | ((uint32_t)t16[i02 >> 16] << 16);
-                const uint32_t r13 = (uint32_t)t16[i13 & 0xFFFFu] | ((uint32_t)t16[i13 >> 16] << 16);
+                const uint32_t r02 = __builtin_amdgcn_perm((uint32_t)t16[i02 >> 16], (uint32_t)t16[i02 & 0xFFFFu],
+                                                           0x05040100u);
+                const uint32_t r13 = __builtin_amdgcn_perm((uint32_t)t16[i13 >> 16], (uint32_t)t16[i13 & 0xFFFFu],
+                                                           0x05040100u);
                 accd = __builtin_amdgcn_udot4(r02, 0x00010001u, accd, false);
                 accd = __builtin_amdgcn_udot4(r13, 0x00010001u, accd, false);
                 accc = __builtin_amdgcn_udot4(r02, 0x01000100u, accc, false);

@@ -363,3 +363,26 @@ def test_unaligned_device_batches(c, mode, offsets):
             assert np.array_equal(m[mo:mo + n * fb].reshape(frames.shape), dmap), (w, h)
             # nothing written outside the map
             assert (m[:mo] == 0xA5).all() and (m[mo + n * fb:] == 0xA5).all()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.5, 1.0])
+def test_gray_kernels_agree(mode, tau, monkeypatch):
+    """GRAY8 on the table kernel (u16 table, the default; DIPS_GRAY_LUT=2),
+    its two-byte-table layout (=1) and the f32 series_fast_kernel (=0), with
+    and without the map, against the oracle -- random and synthetic frames,
+    ragged shape included."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    for (w, h), kind in [((256, 64), "random"), ((640, 48), "synth"), ((37, 23), "random")]:
+        frames = _frames(1, w, h, 9, 40 + w, kind)
+        out4, si, dmap = oracle.series(frames, mode=mode, tau=tau, want_map=True)
+        for layout in ("2", "1", "0"):
+            monkeypatch.setenv("DIPS_GRAY_LUT", layout)
+            op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
+            try:
+                got, gmap = op(frames, want_map=True)
+                got_nomap, _ = op(frames)
+            finally:
+                op.close()
+            _check(got, out4, si, gmap, dmap)
+            _check(got_nomap, out4, si)
