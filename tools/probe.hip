@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
         const uint64_t items = tiles * F;
         const uint64_t resident = (uint64_t)occ * cus * 4;
         a = SeriesArgs{};
-        a.frames = frames; a.ref0 = frames; a.frame_bytes = (uint32_t)fb; a.n_frames = F;
+        a.frames = frames; a.ref0 = frames; a.frame_bytes = (uint32_t)fb; a.vec_bytes = (uint32_t)fb; a.n_frames = F;
         a.n_tiles = (uint32_t)tiles; a.items = items; a.n_waves = (uint32_t)std::min<uint64_t>(items, resident);
         if (const char* ew = getenv("PROBE_WAVES")) a.n_waves = (uint32_t)std::min<uint64_t>(items, strtoull(ew, nullptr, 10));
         a.thr = 2.0f * 8.0f / 255.0f;
