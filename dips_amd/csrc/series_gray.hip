@@ -16,14 +16,17 @@
 //     SI_fixed = 2 (8421504 * sum d + sum corr),   count = #selected.
 // gray_lut_kernel writes two byte tables for the current tau,
 //     T_d[a * 256 + b] = selected ? d : 0,   T_c[...] = selected ? corr : 0,
-// and the series kernel keeps both (128 KiB) in LDS, one 1024-thread group
-// per CU.  Per pixel: the table index from one v_perm_b32 per two pixels
-// (a, b bytes of the same position side by side), two ds_read_u8 into the
-// low and high halves of one register (d | corr << 16), one add into a
-// packed per-lane accumulator (sum d and sum corr stay below 2^16 for the
-// 32 pixels a lane sees per frame), and one compare whose mask the scalar
-// unit counts.  No f32, no f64: the exact f32 arithmetic of the reference is
-// folded into the table.  SAD is the byte SAD as before and SJ = 2 SAD.
+// and the series kernel keeps them (128 KiB) in LDS, one 1024-thread group
+// per CU.  Layout 2 (the default): one u16 table e = d | corr << 8; per
+// pixel pair one v_perm_b32 builds the two indices a * 256 + b, two
+// ds_read_u16 fetch the entries (SDWA word-select shifts give the byte
+// addresses), one v_perm_b32 puts both in one register, and three SADs
+// (bytes, u16 halves, u16 halves minus 1) yield sum d, sum corr and the
+// count exactly.  Layout 1: two byte tables read into the halves of one
+// register (d | corr << 16) -- fewer VALU, but two random LDS reads per
+// pixel (LDS-bound).  No f32, no f64: the exact f32 arithmetic of the
+// reference is folded into the table.  SAD is the byte SAD as before and
+// SJ = 2 SAD.
 //
 // Records: {SAD, sum d, sum corr, count} per (tile, frame); series_reduce
 // (mode 2) forms SI_fixed = 2 (8421504 sum d + sum corr) in 64 bits.
@@ -91,21 +94,24 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
             const uint32_t i02 = __builtin_amdgcn_perm(f, r, 0x06020400u);
             const uint32_t i13 = __builtin_amdgcn_perm(f, r, 0x07030501u);
             if constexpr (LAYOUT == 2) {
-                // one u16 entry d | corr << 8 per pixel; two pixels' entries in
-                // one register, their d and corr summed by two v_dot4_u32_u8
+                // one u16 entry e = d | corr << 8 per pixel (0: not selected,
+                // else d >= 1), two pixels' entries in one register.  Three
+                // SAD sums per pixel pair carry everything:
+                //   sb = sum of bytes         = sum d + sum corr
+                //   s0 = sum e                = sum d + 256 sum corr
+                //   s1 = sum |e - 1|          = s0 + n - 2 count
+                // (n = pixels summed; |0 - 1| = 1 for an unselected pixel)
                 const uint16_t* t16 = reinterpret_cast<const uint16_t*>(lds);
                 const uint32_t r02 = __builtin_amdgcn_perm((uint32_t)t16[i02 >> 16], (uint32_t)t16[i02 & 0xFFFFu],
                                                            0x05040100u);
                 const uint32_t r13 = __builtin_amdgcn_perm((uint32_t)t16[i13 >> 16], (uint32_t)t16[i13 & 0xFFFFu],
                                                            0x05040100u);
-                accd = __builtin_amdgcn_udot4(r02, 0x00010001u, accd, false);
-                accd = __builtin_amdgcn_udot4(r13, 0x00010001u, accd, false);
-                accc = __builtin_amdgcn_udot4(r02, 0x01000100u, accc, false);
-                accc = __builtin_amdgcn_udot4(r13, 0x01000100u, accc, false);
-                c += (uint32_t)__builtin_popcountll(__ballot((r02 & 0xFFFFu) != 0u)) +
-                     (uint32_t)__builtin_popcountll(__ballot(r02 > 0xFFFFu)) +
-                     (uint32_t)__builtin_popcountll(__ballot((r13 & 0xFFFFu) != 0u)) +
-                     (uint32_t)__builtin_popcountll(__ballot(r13 > 0xFFFFu));
+                accc = __builtin_amdgcn_sad_u8(r02, 0u, accc);
+                accc = __builtin_amdgcn_sad_u8(r13, 0u, accc);
+                accd = __builtin_amdgcn_sad_u16(r02, 0u, accd);
+                accd = __builtin_amdgcn_sad_u16(r13, 0u, accd);
+                acc = __builtin_amdgcn_sad_u16(r02, 0x00010001u, acc);
+                acc = __builtin_amdgcn_sad_u16(r13, 0x00010001u, acc);
             } else {
                 const uint32_t ix[4] = {i02 & 0xFFFFu, i13 & 0xFFFFu, i02 >> 16, i13 >> 16};
 #pragma unroll
@@ -117,7 +123,15 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
             }
         }
     }
-    if constexpr (LAYOUT == 2) acc = accd | (accc << 16);  // both < 2^16 (32 px per lane and frame)
+    if constexpr (LAYOUT == 2) {
+        // sb = accc, s0 = accd, s1 = acc (all < 2^22 for 64 px per lane):
+        // sum corr = (s0 - sb) / 255, sum d = sb - sum corr,
+        // count = (s0 + n - s1) / 2
+        constexpr uint32_t n = (uint32_t)U * 16u;
+        const uint32_t sc = (accd - accc) / 255u;
+        c = (accd + n - acc) >> 1;
+        acc = (accc - sc) | (sc << 16);  // sum d < 2^15, sum corr < 2^14
+    }
     if constexpr (MAP) {
         const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.vec_bytes);
 #pragma unroll
@@ -126,8 +140,13 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
     vals[0] = sad;
     vals[1] = acc & 0xFFFFu;
     vals[2] = acc >> 16;
-    vals[3] = 0u;
-    cnt = c;
+    if constexpr (LAYOUT == 2) {
+        vals[3] = c;  // per-lane count, summed with the other values
+        cnt = 0u;
+    } else {
+        vals[3] = 0u;
+        cnt = c;  // wave-wide (scalar popcounts)
+    }
 }
 
 template <int U, bool PF, bool MAP, int LAYOUT>
