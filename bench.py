@@ -339,6 +339,8 @@ def main():
     # measured read-only ceiling on this GPU, outside the timed region: one
     # plain stream over the same resident bytes (median of 3)
     read_ms = float(np.median([op.read_ceiling_ms(frames) for _ in range(3)]))
+    # and with the series kernel's own access shape (tile walk, 12-B vecs)
+    walk_ms = float(np.median([op.read_ceiling_walk_ms(frames) for _ in range(3)]))
     # series-kernel time per step (one launch per step, two when the halo
     # overlap splits a per-frame batch at N > 1)
     tt = torch.tensor([elapsed, kms / args.steps], dtype=torch.float64, device=dev)
@@ -458,6 +460,12 @@ def main():
                     "frac": round(achieved / (F * fb / (read_ms / 1e3) / 1e9), 4),
                     "kernel": "read_ceiling_kernel: non-temporal 16-B loads, 4 in flight per lane, grid-stride, "
                               "over the same frames (no compute)",
+                    "series_shape": {
+                        "achieved": round(F * fb / (walk_ms / 1e3) / 1e9, 1),
+                        "frac": round(achieved / (F * fb / (walk_ms / 1e3) / 1e9), 4),
+                        "kernel": "read_walk_kernel: the series kernel's tile walk and vecs over the same frames, "
+                                  "no compute",
+                    },
                 },
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "partial_bytes_per_launch": int(pbytes) * F,

@@ -154,6 +154,7 @@ def load() -> ctypes.CDLL:
             "dips_kernel_time_reset": ([_vp], st),
             "dips_kernel_time_each": ([_vp, P(ctypes.c_double), u64, P(u64)], st),
             "dips_read_ceiling": ([_vp, _u8p, u64, P(ctypes.c_double)], st),
+            "dips_read_ceiling_walk": ([_vp, _u8p, u32, u32, u32, P(ctypes.c_double)], st),
             "dips_series_geometry": ([_vp, u32, u32, u32, P(u64), P(u64), P(u64)], st),
             "dips_alt_params_default": ([P(DipsAltParams)], st),
             "dips_alt_create": ([P(DipsAltParams), u32, u32, st, P(_vp)], st),

@@ -483,6 +483,15 @@ class DiffSeriesOperator:
                                                          ctypes.byref(ms)))
         return ms.value
 
+    def read_ceiling_walk_ms(self, frames) -> float:
+        """hipEvent time of one read-only walk over device frames [N, H, W, C]
+        in the series kernel's own access shape (RGB8 / RGBA8)."""
+        n, h, w = _frame_geometry(frames, self.fmt)
+        ms = ctypes.c_double()
+        self._dev.check(self._dev._lib.dips_read_ceiling_walk(self._dev.ptr, frames.data_ptr(), w, h, n,
+                                                              ctypes.byref(ms)))
+        return ms.value
+
     def kernel_times(self) -> List[float]:
         """Per-launch hipEvent times (ms) of the series kernel since the last reset."""
         lib, ptr = self._dev._lib, self._dev.ptr

@@ -1079,6 +1079,38 @@ dips_status dips_read_ceiling(dips_handle* h, const uint8_t* dev_bytes, uint64_t
     return DIPS_OK;
 }
 
+dips_status dips_read_ceiling_walk(dips_handle* h, const uint8_t* dev_frames, uint32_t width, uint32_t height,
+                                   uint32_t n_frames, double* ms) {
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!dev_frames || !ms) return fail(h, DIPS_ERR_INVALID, "read_ceiling_walk: null argument");
+    const int C = (int)h->p.format;
+    if (C != 3 && C != 4) return fail(h, DIPS_ERR_INVALID, "read_ceiling_walk: RGB8 / RGBA8 only");
+    FastGeom g = fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false);
+    if (!g.ok) return fail(h, DIPS_ERR_INVALID, "read_ceiling_walk: shape not eligible for the series kernel");
+    DIPS_HIP(h, h->probe_out.ensure(256));
+    dips::SeriesArgs a{};
+    a.frames = dev_frames;
+    a.items = g.items;
+    a.frame_bytes = (uint32_t)((uint64_t)width * height * (uint64_t)C);
+    a.vec_bytes = (uint32_t)g.vec_bytes;
+    a.n_frames = n_frames;
+    a.n_tiles = (uint32_t)g.n_tiles;
+    a.n_waves = (uint32_t)g.n_waves;
+    hipEvent_t e0 = take_event(h), e1 = take_event(h);
+    if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
+    DIPS_HIP(h, hipEventRecord(e0, h->stream));
+    DIPS_HIP(h, dips::launch_read_walk(a, C == 3 ? 12 : 16, (uint32_t)g.blocks, h->probe_out.as<uint32_t>(), h->stream));
+    DIPS_HIP(h, hipEventRecord(e1, h->stream));
+    DIPS_HIP(h, hipEventSynchronize(e1));
+    float t = 0.0f;
+    DIPS_HIP(h, hipEventElapsedTime(&t, e0, e1));
+    *ms = t;
+    h->ev_free.push_back(e0);
+    h->ev_free.push_back(e1);
+    return DIPS_OK;
+}
+
 dips_status dips_series_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames,
                                  uint64_t* waves, uint64_t* tiles, uint64_t* partial_bytes) {
     dips_status st = bind(h);

@@ -363,6 +363,57 @@ __global__ __launch_bounds__(256) void read_ceiling_kernel(const u32x4* __restri
     if (acc == 0x9E3779B9u) out[0] = acc;
 }
 
+// Read-only walk with the series kernels' access shape: the persistent
+// (tile, frame) item schedule of series_v2_kernel, a wave's 64 lanes x U
+// vecs of VB bytes per frame, two frames of loads in flight, no compute.
+// Its rate is the ceiling of that shape (profiles/r02_read_walk_probe.jsonl).
+template <int VB, int U>
+__global__ __launch_bounds__(256) void read_walk_kernel(SeriesArgs a, uint32_t* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    if (wave >= a.n_waves) return;
+    uint64_t i = (uint64_t)wave * a.items / a.n_waves;
+    const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
+    uint32_t acc = 0;
+    while (i < iend) {
+        const uint32_t tile = (uint32_t)(i / a.n_frames);
+        uint32_t t = (uint32_t)(i - (uint64_t)tile * a.n_frames);
+        const uint64_t rem = iend - i;
+        const uint32_t tend = (uint32_t)((uint64_t)a.n_frames < t + rem ? (uint64_t)a.n_frames : t + rem);
+        i += tend - t;
+        const uint32_t voff = (tile * (uint32_t)U * 64u + lane) * (uint32_t)VB;
+        for (; t < tend; t += 2) {
+            const uint32_t t1 = t + 1 < tend ? t + 1 : t;
+            const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.frames + (uint64_t)t * a.frame_bytes, a.vec_bytes);
+            const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.frames + (uint64_t)t1 * a.frame_bytes, a.vec_bytes);
+            uint32_t x = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if constexpr (VB == 12) {
+                    const u32x3 p0 = __builtin_amdgcn_raw_buffer_load_b96(r0, voff + u * 64 * VB, 0, kAuxNT);
+                    const u32x3 p1 = __builtin_amdgcn_raw_buffer_load_b96(r1, voff + u * 64 * VB, 0, kAuxNT);
+                    x ^= p0.x ^ p0.y ^ p0.z ^ p1.x ^ p1.y ^ p1.z;
+                } else {
+                    const u32x4 p0 = __builtin_amdgcn_raw_buffer_load_b128(r0, voff + u * 64 * VB, 0, kAuxNT);
+                    const u32x4 p1 = __builtin_amdgcn_raw_buffer_load_b128(r1, voff + u * 64 * VB, 0, kAuxNT);
+                    x ^= p0.x ^ p0.y ^ p0.z ^ p0.w ^ p1.x ^ p1.y ^ p1.z ^ p1.w;
+                }
+            }
+            acc ^= x;
+        }
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc;
+}
+
+hipError_t launch_read_walk(const SeriesArgs& a, int vec_bytes, uint32_t blocks, uint32_t* out, hipStream_t s) {
+    switch (vec_bytes) {
+        case 12: hipLaunchKernelGGL((read_walk_kernel<12, kUnrollV2>), dim3(blocks), dim3(256), 0, s, a, out); break;
+        case 16: hipLaunchKernelGGL((read_walk_kernel<16, kUnrollV2>), dim3(blocks), dim3(256), 0, s, a, out); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, hipStream_t s) {
     if (((uintptr_t)p & 15u) != 0) return hipErrorInvalidValue;
     const uint64_t n16 = bytes / 16u;

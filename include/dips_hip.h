@@ -211,6 +211,13 @@ dips_status dips_series_geometry(dips_handle *h, uint32_t width, uint32_t height
  * ("% of a measured read-only-stream ceiling"). */
 dips_status dips_read_ceiling(dips_handle *h, const uint8_t *dev_bytes, uint64_t bytes, double *ms);
 
+/* The same with the RGB8 / RGBA8 series kernel's own access shape: its
+ * persistent (tile, frame) schedule over n_frames DEVICE frames of
+ * width x height (the handle's format and mode), 12- / 16-byte vecs, two
+ * frames of loads in flight, no compute; *ms = the hipEvent duration. */
+dips_status dips_read_ceiling_walk(dips_handle *h, const uint8_t *dev_frames, uint32_t width, uint32_t height,
+                                   uint32_t n_frames, double *ms);
+
 /* Library ABI version (DIPS_ABI_VERSION). */
 int dips_abi_version(void);
 
