@@ -255,6 +255,8 @@ bool window_eligible(const dips_alt_handle* h, const uint8_t* frames, const uint
 // uploaded once, the u16 contents are refilled when the properties change.
 dips_status ensure_lut(dips_alt_handle* h, hipStream_t s) {
     const dips::AltLutIndex& ix = dips::alt_lut_index();
+    if (ix.l2_entries > (uint32_t)dips::kAltLutL2Max || ix.diffs.empty())
+        return fail(h, DIPS_ERR_INVALID, "alt epilogue table: index larger than its LDS allocation");
     {
         if (!h->lut_index_ready) {
             ALT_HIP(h, h->lut_l1.ensure(sizeof(ix.l1)));

@@ -31,7 +31,10 @@
 namespace dips {
 
 constexpr int kAltLutClusters = 1021;      // n = -510 .. 510
-constexpr int kAltLutL2Max = 6144;         // u16 entries (5,822 used)
+// u16 entries (5,822 used).  LDS per workgroup 8,168 + 11,776 = 19,944 B:
+// eight 256-thread groups per CU fit the 160 KiB with room to spare (at
+// 20,456 B the eighth group filled it to the last 192 B).
+constexpr int kAltLutL2Max = 5888;
 constexpr float kAltLutRound = 12582912.0f;  // 1.5 * 2^23
 // byte address of the level-1 entry: (bits(fma(diff, 510, 1.5 * 2^23)) << 3) - kAltLutL1Bias
 constexpr uint32_t kAltLutL1Bias = (0x4B400000u - 510u) << 3;
