@@ -269,7 +269,7 @@ dips_status ensure_lut(dips_alt_handle* h, hipStream_t s) {
             ALT_HIP(h, hipMemcpyAsync(h->lut_slots.p, ix.slots.data(), ix.slots.size() * sizeof(uint16_t),
                                       hipMemcpyHostToDevice, s));
             ALT_HIP(h, hipMemsetAsync(h->lut_l2.p, 0, (size_t)dips::kAltLutL2Max * sizeof(uint16_t), s));
-            ALT_HIP(h, hipStreamSynchronize(s));  // once per handle
+            // (the host sources are the process-lifetime index: no wait needed)
             h->lut_index_ready = true;
         }
         const uint32_t col = h->p.colorize != 0 ? 1u : 0u;
