@@ -169,6 +169,7 @@ def load() -> ctypes.CDLL:
             "dips_alt_kernel_time": ([_vp, P(ctypes.c_double), P(u64)], st),
             "dips_alt_kernel_time_reset": ([_vp], st),
             "dips_alt_lut_selfcheck": ([_vp, P(u64)], st),
+            "dips_alt_lut_index": ([_vp, u32, _vp, _vp, u32, P(u32), P(u32)], st),
         }
         del i32, f32
         for name, (args, res) in sig.items():

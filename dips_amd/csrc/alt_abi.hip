@@ -739,6 +739,23 @@ dips_status dips_alt_kernel_time_reset(dips_alt_handle* h) {
     return DIPS_OK;
 }
 
+dips_status dips_alt_lut_index(uint32_t* l1, uint32_t l1_cap, float* diffs, uint16_t* slots, uint32_t cap,
+                               uint32_t* n_diffs, uint32_t* l2_entries) {
+    const dips::AltLutIndex& ix = dips::alt_lut_index();
+    if (n_diffs) *n_diffs = (uint32_t)ix.diffs.size();
+    if (l2_entries) *l2_entries = ix.l2_entries;
+    if (l1) {
+        if (l1_cap < 2u * dips::kAltLutClusters) return DIPS_ERR_CAPACITY;
+        std::memcpy(l1, ix.l1, sizeof(ix.l1));
+    }
+    if (diffs || slots) {
+        if (cap < ix.diffs.size()) return DIPS_ERR_CAPACITY;
+        if (diffs) std::memcpy(diffs, ix.diffs.data(), ix.diffs.size() * sizeof(float));
+        if (slots) std::memcpy(slots, ix.slots.data(), ix.slots.size() * sizeof(uint16_t));
+    }
+    return DIPS_OK;
+}
+
 dips_status dips_alt_lut_selfcheck(dips_alt_handle* h, uint64_t* mismatches) {
     dips_status st = bind(h);
     if (st != DIPS_OK) return st;

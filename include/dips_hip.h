@@ -301,6 +301,13 @@ dips_status dips_alt_kernel_time_reset(dips_alt_handle *h);
  * that differ (0 expected).  Synchronous; for tests. */
 dips_status dips_alt_lut_selfcheck(dips_alt_handle *h, uint64_t *mismatches);
 
+/* The host-built index of that table (alt_lut.h), no device needed: the
+ * level-1 entries {x, sh} of the 1,021 clusters (l1_cap >= 2042 words), the
+ * distinct diff values and their level-2 slots (cap >= *n_diffs), and the
+ * level-2 size.  Any output pointer may be NULL.  For tests. */
+dips_status dips_alt_lut_index(uint32_t *l1, uint32_t l1_cap, float *diffs, uint16_t *slots, uint32_t cap,
+                               uint32_t *n_diffs, uint32_t *l2_entries);
+
 #ifdef __cplusplus
 }
 #endif

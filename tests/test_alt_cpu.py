@@ -163,3 +163,49 @@ def test_alt_null_handle_calls_are_safe():
     h = ctypes.c_void_p()
     assert lib.dips_alt_create(None, 0, 8, 0, ctypes.byref(h)) == _lib.DIPS_ERR_INVALID
     lib.dips_alt_destroy(None)
+
+
+def test_alt_lut_index_is_exact_and_injective():
+    """The host-built two-level index of the dips_alt epilogue table
+    (dips_amd/csrc/alt_lut.h, dips_alt_lut_index; no device): its value set
+    is every f32 u(S) - (u(max) + u(min)) / 2, and every value reaches its own
+    level-2 slot through the device's arithmetic -- cluster
+    rint(510 * diff) from fma(diff, 510, 1.5 * 2^23) (exact rational
+    arithmetic here), then ((bits(diff) >> sh) << 1) + x."""
+    import ctypes
+    from fractions import Fraction
+    from dips_amd import _lib
+    lib = _lib.load()
+    n, l2 = ctypes.c_uint32(), ctypes.c_uint32()
+    assert lib.dips_alt_lut_index(None, 0, None, None, 0, ctypes.byref(n), ctypes.byref(l2)) == 0
+    l1 = np.zeros(2 * 1021, dtype=np.uint32)
+    diffs = np.zeros(n.value, dtype=np.float32)
+    slots = np.zeros(n.value, dtype=np.uint16)
+    assert lib.dips_alt_lut_index(l1.ctypes.data, l1.size, diffs.ctypes.data, slots.ctypes.data, n.value,
+                                  ctypes.byref(n), ctypes.byref(l2)) == 0
+    # the value set, from the reference arithmetic
+    F32 = np.float32
+    u = (np.arange(256, dtype=np.float64) / 255.0).astype(F32)
+    mx, mn = np.meshgrid(np.arange(256), np.arange(256), indexing="ij")
+    keep = mx >= mn
+    iv = np.unique(((u[mx[keep]] + u[mn[keep]]) / F32(2)).astype(F32))
+    want = np.unique((u[:, None] - iv[None, :]).astype(F32).ravel())
+    assert len(want) == 2993
+    assert np.array_equal(np.sort(diffs.view(np.uint32)), np.sort(want.view(np.uint32)))
+    assert l2.value <= 5888  # kAltLutL2Max
+    assert len(np.unique(slots)) == len(slots) and int(slots.max()) < l2.value
+    bias = ((0x4B400000 - 510) << 3) & 0xFFFFFFFF
+    for d, slot in zip(diffs.tolist(), slots.tolist()):
+        # fma(d, 510, 1.5 * 2^23) rounded once to f32 (RNE), exactly
+        exact = Fraction(d) * 510 + 12582912
+        t = float(np.float32(float(exact)))  # the f64 of an exact rational, then f32
+        # guard the double rounding: the f32 result must be the nearest to the exact value
+        lo, hi = np.nextafter(F32(t), F32(-np.inf)), np.nextafter(F32(t), F32(np.inf))
+        assert abs(Fraction(t) - exact) <= min(abs(Fraction(float(lo)) - exact), abs(Fraction(float(hi)) - exact))
+        tb = int(np.array([t], dtype=np.float32).view(np.uint32)[0])
+        a1 = ((tb << 3) - bias) & 0xFFFFFFFF
+        assert a1 % 8 == 0 and a1 // 8 < 1021
+        x, sh = int(l1[2 * (a1 // 8)]), int(l1[2 * (a1 // 8) + 1])
+        db = int(np.array([d], dtype=np.float32).view(np.uint32)[0])
+        a2 = (((db >> sh) << 1) + x) & 0xFFFFFFFF
+        assert a2 == 2 * slot, (d, slot, a2)
