@@ -339,3 +339,27 @@ def test_gray_si_decomposition():
     frames = np.stack([b.astype(np.uint8), a.astype(np.uint8)])  # reference b, then frame a
     out4, _, _ = oracle.series(frames, mode=1, tau=0.0)
     assert int(out4[1, 3]) == int(2 * v.sum())
+
+
+@pytest.mark.parametrize("filt", [0, 1, 255])
+@pytest.mark.parametrize("colorize", [False, True])
+def test_epilogue_table_encoding(filt, colorize):
+    """The epilogue tables (compat_batch_lut_kernel, alt_lut.h) keep only
+    R | G << 8 of each texel: B = min(R, G) and A = 255 must hold for every
+    argument they are built from -- every diff u(S) - u(m) of the ComputeState
+    table and every dips_alt diff u(S) - I -- for every filter, colour mode
+    and sensitivities inside and far outside the usual range (inf / NaN
+    texels of the inverse sigmoid included).  numpy restatement of the spec
+    epilogue, exhaustive over the tables' domains."""
+    F32 = np.float32
+    u = (np.arange(256, dtype=np.float64) / 255.0).astype(F32)
+    d_compat = (u[:, None] - u[None, :]).astype(F32).ravel()
+    mx, mn = np.meshgrid(np.arange(256), np.arange(256), indexing="ij")
+    keep = mx >= mn
+    iv = np.unique(((u[mx[keep]] + u[mn[keep]]) / F32(2)).astype(F32))
+    d_alt = np.unique((u[:, None] - iv[None, :]).astype(F32).ravel())
+    for k in (5.0, 1.0, 10.0, 0.0, -3.0, 200.0, 1e-30, 1e30):
+        for d in (d_compat, d_alt):
+            out = nr.epilogue(d, filt, k, colorize)
+            assert np.all(out[:, 3] == 255)
+            assert np.array_equal(out[:, 2], np.minimum(out[:, 0], out[:, 1])), (filt, colorize, k)
