@@ -88,10 +88,18 @@ def main():
     achieved = algo / (kernel_ms / 1e3) / 1e9
     traffic, traffic_src = None, None
     if os.path.exists(args.pmc_json):
+        import hashlib
+        from dips_amd import _lib as L
+        with open(L.LIB_PATH, "rb") as f:
+            sha = hashlib.sha256(f.read()).hexdigest()
         with open(args.pmc_json) as f:
             pmc = json.load(f)
-        if (pmc.get("width"), pmc.get("height"), pmc.get("frames")) == (W, H, F):
+        # only a measurement of this very library build and workload counts
+        if (pmc.get("width"), pmc.get("height"), pmc.get("frames")) == (W, H, F) and pmc.get("lib_sha256") == sha \
+                and args.kernel == "lut":
             traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), pmc.get("source")
+        else:
+            traffic_src = "traffic null: the PMC file is of another library build, workload or kernel form"
     print(json.dumps({
         "metric": "dips_alt frames/s + achieved HBM GB/s, 4K RGBA8",
         "value": round(F * args.steps / elapsed, 2), "unit": "frames/s", "n_gpus": 1,
