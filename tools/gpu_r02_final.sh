@@ -9,6 +9,8 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 O=gpurun_out/final
 mkdir -p $O
+STAGE=${1:-a}   # a: tests, PMC, headline bench (+ rocprof); b: the rest
+if [ "$STAGE" = a ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   > $O/pytest_gpu.txt 2>&1; rc=$?
 tail -3 $O/pytest_gpu.txt; [ $rc -ne 0 ] && { tail -60 $O/pytest_gpu.txt; exit $rc; }
@@ -24,7 +26,8 @@ timeout -k 10 900 python3 bench.py > $O/bench.json 2> $O/bench.log; rc=$?
 cat $O/bench.json; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- \
   python3 bench.py --no-cpu-baseline --no-pcie --no-map > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.log
-rc=$?; echo "rocprof bench rc=$rc"; [ $rc -ne 0 ] && exit $rc
+rc=$?; echo "rocprof bench rc=$rc"; exit $rc
+fi
 timeout -k 10 600 python3 bench.py --steps 100 --warmup 3 --no-cpu-baseline --no-pcie --no-map \
   > $O/sustain_steps100.json 2> $O/sustain_steps100.log; rc=$?
 cat $O/sustain_steps100.json; [ $rc -ne 0 ] && exit $rc
