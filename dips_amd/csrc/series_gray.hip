@@ -17,7 +17,8 @@
 // gray_lut_kernel writes two byte tables for the current tau,
 //     T_d[a * 256 + b] = selected ? d : 0,   T_c[...] = selected ? corr : 0,
 // and the series kernel keeps them (128 KiB) in LDS, one 1024-thread group
-// per CU.  Layout 2 (the default): one u16 table e = d | corr << 8; per
+// per CU.  Layout 2 (the default): one u16 table e = d | corr << 8 (rows
+// swizzled against LDS bank conflicts, kGraySwizzle); per
 // pixel pair one v_perm_b32 builds the two indices a * 256 + b, two
 // ds_read_u16 fetch the entries (SDWA word-select shifts give the byte
 // addresses), one v_perm_b32 puts both in one register, and three SADs
@@ -38,6 +39,19 @@ constexpr uint32_t kGrayLutTcOffset = 65535u;  // T_c's byte offset in LDS (the 
                                                // T_d[65535] and T_c[0] share a byte: both are 0, a == b)
 constexpr uint32_t kGrayV = 8421504u;          // V = kGrayV * d + corr
 
+// Layout 2 stores the entry of (a, b) at u16 index a * 256 + (b ^ sw(a)),
+// sw(a) = (a << 2) & 0x3C.  A ds_read_u16's bank is (byte address / 4) mod
+// 32 = bits 1-5 of the stored b; unswizzled that is b alone, and where the
+// reference is smooth (b within a few levels across the 32 lanes of a half)
+// the lanes pile onto 2-4 banks: 4K gray8 with flat +-3 noise ran at 39 %
+// of 8 TB/s against 65 % on the bench's random-base frames
+// (tools/content_rate.py, profiles/r02_content_rate.jsonl).  XOR-ing the low
+// four bits of a into bank bits 2-5 spreads such boxes of (a, b) over the
+// banks (bank-conflict simulation: flat +-3 12.2 -> 3.9 LDS cycles per
+// read, random unchanged at 7.1) and costs two VALU per four pixels (the
+// reference dword is swizzled once before the index perms).
+constexpr uint32_t kGraySwizzle = 0x3Cu;
+
 // The tables for threshold tau (65,536 spec evaluations), 131,072 bytes:
 // layout 1 -- T_d at byte 0 and T_c at byte kGrayLutTcOffset;
 // layout 2 -- one u16 table, entry d | corr << 8 at byte 2 idx.
@@ -50,7 +64,8 @@ __global__ __launch_bounds__(256) void gray_lut_kernel(uint8_t* __restrict__ tab
     const uint32_t d = a > b ? a - b : b - a;
     const uint32_t corr = (uint32_t)(v - (uint64_t)kGrayV * d);  // in [0, 128] (exhaustive test)
     if (layout == 2u) {
-        reinterpret_cast<uint16_t*>(tab)[idx] = sel ? (uint16_t)(d | corr << 8) : (uint16_t)0;
+        const uint32_t pos = (a << 8) | (b ^ ((a << 2) & kGraySwizzle));
+        reinterpret_cast<uint16_t*>(tab)[pos] = sel ? (uint16_t)(d | corr << 8) : (uint16_t)0;
     } else {
         tab[idx] = sel ? (uint8_t)d : (uint8_t)0;
         if (idx != 0u) tab[kGrayLutTcOffset + idx] = sel ? (uint8_t)corr : (uint8_t)0;
@@ -90,9 +105,11 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
             const uint32_t f = cur[u][k], r = rb[u][k];
             sad = __builtin_amdgcn_sad_u8(f, r, sad);
             if constexpr (MAP) map[u][k] = absdiff_bytes(f, r);
-            // table indices f_i * 256 + r_i of pixels (0, 2) and (1, 3) as u16 pairs
-            const uint32_t i02 = __builtin_amdgcn_perm(f, r, 0x06020400u);
-            const uint32_t i13 = __builtin_amdgcn_perm(f, r, 0x07030501u);
+            // table indices f_i * 256 + r_i of pixels (0, 2) and (1, 3) as u16
+            // pairs (layout 2: r_i ^ sw(f_i), per byte of the dword at once)
+            const uint32_t rs = LAYOUT == 2 ? r ^ ((f << 2) & (kGraySwizzle * 0x01010101u)) : r;
+            const uint32_t i02 = __builtin_amdgcn_perm(f, rs, 0x06020400u);
+            const uint32_t i13 = __builtin_amdgcn_perm(f, rs, 0x07030501u);
             if constexpr (LAYOUT == 2) {
                 // one u16 entry e = d | corr << 8 per pixel (0: not selected,
                 // else d >= 1), two pixels' entries in one register.  Three

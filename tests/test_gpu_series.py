@@ -386,3 +386,29 @@ def test_gray_kernels_agree(mode, tau, monkeypatch):
                 op.close()
             _check(got, out4, si, gmap, dmap)
             _check(got_nomap, out4, si)
+
+
+@pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.1, 0.5])
+def test_gray_table_every_byte_pair(tau):
+    """Every (frame byte a, reference byte b) through the swizzled GRAY8
+    table, against the oracle: 'overall' against a reference with b = x;
+    frame t = 1..256 holds a = t - 1 everywhere (so each a value is its own
+    series entry), frame 257 holds a = y (all 65,536 pairs in one frame);
+    plus a flat low-noise clip, the content that piles LDS reads onto few
+    banks without the swizzle."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    x = np.arange(256, dtype=np.uint8)
+    frames = np.empty((258, 256, 256), dtype=np.uint8)
+    frames[0] = x[None, :]
+    frames[1:257] = x[:, None, None]
+    frames[257] = x[:, None]
+    rng = np.random.default_rng(11)
+    flat = np.clip(128 + rng.integers(-3, 4, (12, 64, 512)), 0, 255).astype(np.uint8)
+    for fr, mode in ((frames, 0), (frames, 1), (flat, 1)):
+        out4, si, _ = oracle.series(fr, mode=mode, tau=tau)
+        op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
+        try:
+            got, _ = op(fr)
+        finally:
+            op.close()
+        _check(got, out4, si)
