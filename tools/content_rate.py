@@ -60,10 +60,11 @@ def main():
     from dips_amd.api import ComputeState, DiPsFilter, ChromaFilter
     kinds = sys.argv[1].split(",") if len(sys.argv) > 1 else ["synthetic", "flat", "gradient", "moving"]
     reps = 5
+    kern = os.environ.get("CONTENT_KERNELS", "gray,compat,alt")
     # GRAY8 series (table kernel)
     n = 3000
     op = DiffSeriesOperator(PixelFormat.Gray8, Mode.PerFrame, 8.0 / 255.0, time_kernel=True)
-    for kind in kinds:
+    for kind in (kinds if "gray" in kern else []):
         fr = make(torch, kind, n, 1, lambda d: op.synth_device(d, W, H, 0xD1B5, 0))
         ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
         op.run_device(fr, ser)
@@ -80,7 +81,36 @@ def main():
         del fr, ser
         torch.cuda.empty_cache()
     op.close()
-    if os.environ.get("CONTENT_KERNELS", "gray,compat").find("compat") < 0:
+    if "alt" in kern:
+        # dips_alt run loop (RGBA8, N = 2, default colour + sigmoid: the
+        # two-level diff table)
+        from dips_amd.alt import DiPsCompute
+        n = 1000
+        syn = DiffSeriesOperator(PixelFormat.RGBA8, Mode.PerFrame, 0.0)
+        for kind in kinds:
+            fr = make(torch, kind, n, 4, lambda d: syn.synth_device(d, W, H, 0xD1B5, 0))
+            if kind != "synthetic":
+                fr[..., 3] = 255
+            out = torch.empty_like(fr)
+            flags = [t == 2 for t in range(n)]
+            c = DiPsCompute(2, H, W, time_kernel=True)
+            c.send_frames_device(fr, out, flags)
+            torch.cuda.synchronize()
+            c.kernel_time(reset=True)
+            for _ in range(reps):
+                c.send_frames_device(fr, out, flags)
+            torch.cuda.synchronize()
+            ms, cnt = c.kernel_time()
+            ms /= max(cnt, 1)
+            gbs = 2 * n * W * H * 4 / (ms / 1e3) / 1e9
+            print(json.dumps({"kernel": "alt_batch_kernel LUT (colour + sigmoid)", "content": kind, "frames": n,
+                              "kernel_ms": round(ms, 3), "launches": cnt, "GBps_read_write": round(gbs, 1),
+                              "frac_of_8TBps": round(gbs / 8000, 4)}), flush=True)
+            c.close()
+            del fr, out
+            torch.cuda.empty_cache()
+        syn.close()
+    if "compat" not in kern:
         return
     # ComputeState batch (RGBA8, colour + sigmoid: the (S, m) table kernel)
     n = 1000
