@@ -124,6 +124,7 @@ struct dips_alt_handle {
     uint32_t width = 0, height = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
+    hipEvent_t switch_ev = nullptr;  // orders a newly set stream after the previous one
     std::string err;
 
     DevBuf slots[dips::kAltMaxTextures];  // input_textures (mod.rs:279-301)
@@ -569,6 +570,7 @@ void dips_alt_destroy(dips_alt_handle* h) {
     for (auto& ev : h->meta_done)
         if (ev) (void)hipEventDestroy(ev);
     if (h->meta_free) (void)hipEventDestroy(h->meta_free);
+    if (h->switch_ev) (void)hipEventDestroy(h->switch_ev);
     if (h->meta_stream) (void)hipStreamDestroy(h->meta_stream);
     for (auto& mp : h->meta_pin) mp.release();
     for (auto& s : h->slots) s.release();
@@ -597,7 +599,16 @@ const char* dips_alt_last_error(const dips_alt_handle* h) {
 
 dips_status dips_alt_set_stream(dips_alt_handle* h, void* stream) {
     if (!h) return DIPS_ERR_INVALID;
-    h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+    hipStream_t next = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+    if (next == h->stream) return DIPS_OK;
+    // slots, snapshot and tables serve every stream: work issued on the new
+    // stream waits for all work issued on the old one
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!h->switch_ev) ALT_HIP(h, hipEventCreateWithFlags(&h->switch_ev, hipEventDisableTiming));
+    ALT_HIP(h, hipEventRecord(h->switch_ev, h->stream));
+    ALT_HIP(h, hipStreamWaitEvent(next, h->switch_ev, 0));
+    h->stream = next;
     return DIPS_OK;
 }
 

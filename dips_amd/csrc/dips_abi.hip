@@ -44,6 +44,7 @@ struct dips_handle {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;
+    hipEvent_t switch_ev = nullptr;  // orders a newly set stream after the previous one
     std::string err;
 
     // batch series workspace
@@ -445,6 +446,7 @@ void dips_destroy(dips_handle* h) {
     h->start.release();
     h->out.release();
     h->io.release();
+    if (h->switch_ev) (void)hipEventDestroy(h->switch_ev);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
     delete h;
@@ -458,7 +460,16 @@ const char* dips_last_error(const dips_handle* h) {
 
 dips_status dips_set_stream(dips_handle* h, void* stream) {
     if (!h) return DIPS_ERR_INVALID;
-    h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+    hipStream_t next = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+    if (next == h->stream) return DIPS_OK;
+    // the handle's scratch (partials, tables, staging) serves every stream:
+    // work issued on the new stream waits for all work issued on the old one
+    dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    if (!h->switch_ev) DIPS_HIP(h, hipEventCreateWithFlags(&h->switch_ev, hipEventDisableTiming));
+    DIPS_HIP(h, hipEventRecord(h->switch_ev, h->stream));
+    DIPS_HIP(h, hipStreamWaitEvent(next, h->switch_ev, 0));
+    h->stream = next;
     return DIPS_OK;
 }
 

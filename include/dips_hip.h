@@ -105,7 +105,11 @@ void dips_destroy(dips_handle *h);
 /* Last error message for `h` (or the last creation failure if h == NULL). */
 const char *dips_last_error(const dips_handle *h);
 
-/* Run subsequent work on `stream` (a hipStream_t; NULL = the handle's own). */
+/* Run subsequent work on `stream` (a hipStream_t; NULL = the handle's own).
+ * Switching streams orders the new stream after all work already issued on
+ * the previous one (the handle's device scratch serves both), so the previous
+ * stream must still exist at the switch; setting the current stream again is
+ * free. */
 dips_status dips_set_stream(dips_handle *h, void *stream);
 
 /* Block until all work issued through `h` has finished. */
@@ -261,7 +265,8 @@ void dips_alt_destroy(dips_alt_handle *h);
 /* Last error message for `h` (or the last creation failure if h == NULL). */
 const char *dips_alt_last_error(const dips_alt_handle *h);
 
-/* Run subsequent work on `stream` (a hipStream_t; NULL = the handle's own). */
+/* Run subsequent work on `stream` (a hipStream_t; NULL = the handle's own);
+ * ordered after the previous stream's work as dips_set_stream. */
 dips_status dips_alt_set_stream(dips_alt_handle *h, void *stream);
 dips_status dips_alt_synchronize(dips_alt_handle *h);
 

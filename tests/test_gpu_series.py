@@ -412,3 +412,37 @@ def test_gray_table_every_byte_pair(tau):
         finally:
             op.close()
         _check(got, out4, si)
+
+
+@pytest.mark.parametrize("c", [1, 3])
+def test_stream_switch_orders_shared_scratch(c):
+    """Back-to-back batches on two different streams through one operator,
+    no synchronisation in between: the handle's partial records and tables
+    are shared, so dips_set_stream orders the second stream after the first
+    (both series must equal the oracle's)."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    w, h, n = 640, 480, 24
+    fa = _frames(c, w, h, n, 301, "random")
+    fb = _frames(c, w, h, n, 302, "synth")
+    want = [oracle.series(f, mode=1, tau=8 / 255)[0] for f in (fa, fb)]
+    op = DiffSeriesOperator(PixelFormat(c), Mode.PerFrame, 8 / 255)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    try:
+        da, db = torch.from_numpy(fa).cuda(), torch.from_numpy(fb).cuda()
+        torch.cuda.synchronize()
+        outs = []
+        for rep in range(3):
+            sa = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+            sb = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+            with torch.cuda.stream(s1):
+                op.run_device(da, sa)
+            with torch.cuda.stream(s2):
+                op.run_device(db, sb)
+            outs.append((sa, sb))
+        torch.cuda.synchronize()
+        for sa, sb in outs:
+            assert np.array_equal(sa.cpu().numpy().view(np.uint64), want[0])
+            assert np.array_equal(sb.cpu().numpy().view(np.uint64), want[1])
+    finally:
+        op.close()
