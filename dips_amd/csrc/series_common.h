@@ -37,25 +37,25 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint3
     return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), kRsrcFlags);
 }
 
-template <int C>
+template <int C, int AUX = kAuxNT>
 __device__ __forceinline__ void load_vec(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t (&v)[Fmt<C>::NDW]) {
     if constexpr (Fmt<C>::NDW == 3) {
-        const u32x3 x = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, kAuxNT);
+        const u32x3 x = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, AUX);
         v[0] = x.x; v[1] = x.y; v[2] = x.z;
     } else {
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxNT);
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
         v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
     }
 }
 
-template <int C>
+template <int C, int AUX = kAuxNT>
 __device__ __forceinline__ void store_vec(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint32_t (&v)[Fmt<C>::NDW]) {
     if constexpr (Fmt<C>::NDW == 3) {
         u32x3 x; x.x = v[0]; x.y = v[1]; x.z = v[2];
-        __builtin_amdgcn_raw_buffer_store_b96(x, r, off, 0, kAuxNT);
+        __builtin_amdgcn_raw_buffer_store_b96(x, r, off, 0, AUX);
     } else {
         u32x4 x; x.x = v[0]; x.y = v[1]; x.z = v[2]; x.w = v[3];
-        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, kAuxNT);
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, AUX);
     }
 }
 

@@ -38,7 +38,7 @@ constexpr float kSjMul = 255.0f / 4194304.0f;
 // One frame of one tile: accumulate against the reference state `st`
 // (updated to this frame's state in per-frame mode) and the reference bytes
 // `rb`; produce the 4 per-lane values {SAD, SJ, H, L} and the wave-wide count.
-template <int C, int CH, int U, bool PF, bool MAP>
+template <int C, int CH, int U, bool PF, bool MAP, int SAUX = kAuxNT>
 __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], const uint32_t (&rb)[U][Fmt<C>::NDW],
                                          const uint32_t (&cur)[U][Fmt<C>::NDW], uint32_t voff, uint32_t t,
                                          uint32_t* vals, uint32_t& cnt) {
@@ -80,7 +80,7 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
     if constexpr (MAP) {
         const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.vec_bytes);
 #pragma unroll
-        for (int u = 0; u < U; ++u) store_vec<C>(rm, voff + (uint32_t)(u * 64 * F::VB), map[u]);
+        for (int u = 0; u < U; ++u) store_vec<C, SAUX>(rm, voff + (uint32_t)(u * 64 * F::VB), map[u]);
     }
     const uint64_t yb = __builtin_bit_cast(uint64_t, si);
     const uint32_t lo = (uint32_t)yb, hi = (uint32_t)(yb >> 32);
@@ -111,7 +111,10 @@ __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t
 template <int C, int U, bool PF, bool MAP>
 constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : 5)) : 1; }
 
-template <int C, int CH, int U, bool PF, bool MAP>
+// AUX / SAUX: cache-policy bits of the frame loads / map stores (probe
+// builds compare them in one process, tools/aux_ab.hip; the library uses the
+// defaults, nt).
+template <int C, int CH, int U, bool PF, bool MAP, int AUX = kAuxNT, int SAUX = kAuxNT>
 __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v2_kernel(SeriesArgs a) {
     using F = Fmt<C>;
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
@@ -147,7 +150,7 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v
 #endif
             const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)min(tf, tlast) * fb, vb);
 #pragma unroll
-            for (int u = 0; u < U; ++u) load_vec<C>(r, voff + (uint32_t)(u * 64 * F::VB), dst[u]);
+            for (int u = 0; u < U; ++u) load_vec<C, AUX>(r, voff + (uint32_t)(u * 64 * F::VB), dst[u]);
         };
 
         // ring: PF -- frame k of the segment in slot (k+1)&3, its reference
@@ -186,12 +189,12 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v
                     const int j = 2 * h + q;
                     const uint32_t tf = t0 + k + (uint32_t)j;
                     if constexpr (PF) {
-                        frame_v2<C, CH, U, PF, MAP>(a, st, buf[j], buf[(j + 1) & 3], voff, tf, v + 4 * q,
+                        frame_v2<C, CH, U, PF, MAP, SAUX>(a, st, buf[j], buf[(j + 1) & 3], voff, tf, v + 4 * q,
                                                     q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 3, buf[j]);
                     } else {
-                        frame_v2<C, CH, U, PF, MAP>(a, st, rb, buf[j], voff, tf, v + 4 * q, q ? c1 : c0);
+                        frame_v2<C, CH, U, PF, MAP, SAUX>(a, st, rb, buf[j], voff, tf, v + 4 * q, q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 4, buf[j]);
                     }
@@ -207,9 +210,9 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v
                 uint32_t v[4], c;
                 const uint32_t tf = t0 + k + (uint32_t)j;
                 if constexpr (PF)
-                    frame_v2<C, CH, U, PF, MAP>(a, st, buf[j], buf[j + 1], voff, tf, v, c);
+                    frame_v2<C, CH, U, PF, MAP, SAUX>(a, st, buf[j], buf[j + 1], voff, tf, v, c);
                 else
-                    frame_v2<C, CH, U, PF, MAP>(a, st, rb, buf[j], voff, tf, v, c);
+                    frame_v2<C, CH, U, PF, MAP, SAUX>(a, st, rb, buf[j], voff, tf, v, c);
                 const uint32_t y = wave_sum4_lanes(v);
                 store_one(rpart, tf, rec_off4, lane, y, c);
             }
