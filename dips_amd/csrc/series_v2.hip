@@ -111,11 +111,11 @@ __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t
 template <int C, int U, bool PF, bool MAP>
 constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : 5)) : 1; }
 
-// AUX / SAUX: cache-policy bits of the frame loads / map stores (probe
-// builds compare them in one process, tools/aux_ab.hip; the library uses the
-// defaults, nt).
-template <int C, int CH, int U, bool PF, bool MAP, int AUX = kAuxNT, int SAUX = kAuxNT>
-__global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v2_kernel(SeriesArgs a) {
+// The kernel body; AUX / SAUX are the cache-policy bits of the frame loads /
+// map stores (the library kernel below uses nt; probe builds instantiate
+// other policies to compare them in one process, tools/aux_ab.hip).
+template <int C, int CH, int U, bool PF, bool MAP, int AUX, int SAUX>
+__device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
     using F = Fmt<C>;
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;
@@ -218,6 +218,11 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v
             }
         }
     }
+}
+
+template <int C, int CH, int U, bool PF, bool MAP>
+__global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v2_kernel(SeriesArgs a) {
+    series_v2_body<C, CH, U, PF, MAP, kAuxNT, kAuxNT>(a);
 }
 
 // ---------------------------------------------------------------------------

@@ -20,6 +20,11 @@ static double now() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+template <int AUX, int SAUX, bool MAP>
+__global__ __launch_bounds__(256, (v2_min_waves<3, kUnrollV2, true, MAP>())) void probe_kernel(SeriesArgs a) {
+    series_v2_body<3, 0, kUnrollV2, true, MAP, AUX, SAUX>(a);
+}
+
 struct V {
     int aux;
     const void* k;
@@ -42,20 +47,20 @@ int main(int argc, char** argv) {
     // mode "load": the frame-load policy; mode "map": the map-store policy
     // of the MAP variant (frame loads nt)
     const bool map = argc > 4 && std::string(argv[4]) == "map";
-    const std::vector<V> vload = {{2, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, false, 2>},
-                                  {0, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, false, 0>},
-                                  {1, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, false, 1>},
-                                  {3, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, false, 3>},
-                                  {16, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, false, 16>},
-                                  {18, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, false, 18>}};
-    const std::vector<V> vmap = {{2, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, true, 2, 2>},
-                                 {0, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, true, 2, 0>},
-                                 {1, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, true, 2, 1>},
-                                 {3, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, true, 2, 3>},
-                                 {16, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, true, 2, 16>},
-                                 {17, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, true, 2, 17>},
-                                 {18, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, true, 2, 18>},
-                                 {19, (const void*)&series_v2_kernel<3, 0, kUnrollV2, true, true, 2, 19>}};
+    const std::vector<V> vload = {{2, (const void*)&probe_kernel<2, 2, false>},
+                                  {0, (const void*)&probe_kernel<0, 2, false>},
+                                  {1, (const void*)&probe_kernel<1, 2, false>},
+                                  {3, (const void*)&probe_kernel<3, 2, false>},
+                                  {16, (const void*)&probe_kernel<16, 2, false>},
+                                  {18, (const void*)&probe_kernel<18, 2, false>}};
+    const std::vector<V> vmap = {{2, (const void*)&probe_kernel<2, 2, true>},
+                                 {0, (const void*)&probe_kernel<2, 0, true>},
+                                 {1, (const void*)&probe_kernel<2, 1, true>},
+                                 {3, (const void*)&probe_kernel<2, 3, true>},
+                                 {16, (const void*)&probe_kernel<2, 16, true>},
+                                 {17, (const void*)&probe_kernel<2, 17, true>},
+                                 {18, (const void*)&probe_kernel<2, 18, true>},
+                                 {19, (const void*)&probe_kernel<2, 19, true>}};
     const std::vector<V>& vs = map ? vmap : vload;
     int occ = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vs[0].k, 256, 0) != hipSuccess) return 1;
