@@ -44,6 +44,7 @@ struct SeriesArgs {
     uint32_t n_waves;
     float thr;               // threshold in kernel units: series_threshold()
     const void* lut;         // GRAY8 table kernel: T_d / T_c bytes (series_gray.hip), 128 KiB
+    uint32_t part_frames;    // frames per part of the part-major schedule (series_v2 SCHED = 1)
 };
 
 struct GenericArgs {

@@ -114,7 +114,11 @@ constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U 
 // The kernel body; AUX / SAUX are the cache-policy bits of the frame loads /
 // map stores (the library kernel below uses nt; probe builds instantiate
 // other policies to compare them in one process, tools/aux_ab.hip).
-template <int C, int CH, int U, bool PF, bool MAP, int AUX, int SAUX>
+// SCHED: 0 -- one contiguous (tile, frame) range per wave (the library);
+// 1 -- frames cut into parts of a.part_frames, items (part, tile) taken
+// part-major with stride n_waves, so concurrent waves read the same frames of
+// adjacent tiles (probe builds, tools/sched_ab.hip).
+template <int C, int CH, int U, bool PF, bool MAP, int AUX, int SAUX, int SCHED = 0>
 __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
     using F = Fmt<C>;
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
@@ -129,13 +133,26 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
 
     uint64_t i = (uint64_t)wave * a.items / a.n_waves;
     const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
-    while (i < iend) {
-        const uint32_t tile = (uint32_t)(i / a.n_frames);
-        const uint32_t t0 = (uint32_t)(i - (uint64_t)tile * a.n_frames);
-        const uint64_t remaining = iend - i;
-        const uint32_t tend =
-            (uint32_t)((uint64_t)a.n_frames < t0 + remaining ? (uint64_t)a.n_frames : t0 + remaining);
-        i += tend - t0;
+    const uint32_t plen = SCHED == 1 ? a.part_frames : 1u;
+    const uint64_t pitems = SCHED == 1 ? (uint64_t)((a.n_frames + plen - 1) / plen) * a.n_tiles : 0u;
+    uint64_t it = wave;
+    while (true) {
+        uint32_t tile, t0, tend;
+        if constexpr (SCHED == 0) {
+            if (i >= iend) break;
+            tile = (uint32_t)(i / a.n_frames);
+            t0 = (uint32_t)(i - (uint64_t)tile * a.n_frames);
+            const uint64_t remaining = iend - i;
+            tend = (uint32_t)((uint64_t)a.n_frames < t0 + remaining ? (uint64_t)a.n_frames : t0 + remaining);
+            i += tend - t0;
+        } else {
+            if (it >= pitems) break;
+            const uint32_t part = (uint32_t)(it / a.n_tiles);
+            tile = (uint32_t)(it - (uint64_t)part * a.n_tiles);
+            t0 = part * plen;
+            tend = min(a.n_frames, t0 + plen);
+            it += a.n_waves;
+        }
         const uint32_t n = tend - t0;  // frames of this segment (>= 1)
         const uint32_t tlast = tend - 1;
         const uint32_t voff = (tile * U * 64u + lane) * (uint32_t)F::VB;
