@@ -216,6 +216,43 @@ def _config0_gpu(torch, frames_host, want):
             "note": "92 MB batch: launch-bound (a 300-frame 640x480 clip is ~0.03 ms of HBM streaming)"}
 
 
+def _start_power(torch, local):
+    """Socket power / clock / PPT throttling of this rank's GPU over the timed
+    region (tools/power_probe.py's amdsmi sampler, read-only queries); None
+    where amdsmi is unavailable."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from power_probe import Sampler
+        bus = torch.cuda.get_device_properties(local).pci_bus_id
+        smp = Sampler(period=0.01, pci_bus=bus)
+        if len(smp.handles) != 1:
+            return None
+        smp.start()
+        return smp
+    except Exception:  # report nothing rather than fail the bench
+        return None
+
+
+def _power_report(smp, t0, t1, frames):
+    if smp is None:
+        return None
+    try:
+        time.sleep(0.05)  # one more sample after the region
+        smp.stop_ev.set()
+        smp.join(timeout=2)
+        g = smp.window(t0, t1)[0]
+        if not g or not g.get("avg_power_W_energy"):
+            return None
+        fps = frames / (t1 - t0)
+        return {"avg_W": g["avg_power_W_energy"], "gfxclk_MHz_mean": g.get("gfxclk_MHz_mean"),
+                "ppt_throttle_residency": g.get("ppt_residency_frac"), "samples": g.get("samples"),
+                "mJ_per_frame": round(g["avg_power_W_energy"] / fps * 1e3, 4),
+                "source": "amdsmi energy counter, per-XCD gfx clocks and PPT residency over the timed steps "
+                          "(tools/power_probe.py); DESIGN.md 'the limiter'"}
+    except Exception:
+        return None
+
+
 def _map_variant(torch, op_cls, frames, n, W, H, mode_pf, tau):
     """The north star's bit-exact output D_t = |F_t - R| materialised: the
     MAP=true series kernel over n resident frames (read F, write D), timed by
@@ -326,14 +363,18 @@ def main():
     op.kernel_time(reset=True)
     if world > 1:
         dist.barrier()
+    smp = _start_power(torch, local) if rank == 0 else None
     torch.cuda.synchronize()
     t = time.perf_counter()
+    tm0 = time.monotonic()
     for _ in range(args.steps):
         final = step()
     torch.cuda.synchronize()
+    tm1 = time.monotonic()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t
+    power = _power_report(smp, tm0, tm1, F * args.steps)
     kms, launches = op.kernel_time()
     each = op.kernel_times()  # one launch per step at N = 1 (two at N > 1 per-frame)
     # measured read-only ceiling on this GPU, outside the timed region: one
@@ -474,6 +515,7 @@ def main():
                 "lib_sha256": lib_sha,
             },
             "cpu_baseline": cpu,
+            "power": power,
             "pcie_inclusive": pcie,
             "map_variant": mapv,
         }

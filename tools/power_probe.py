@@ -40,12 +40,23 @@ FB = W * H * C
 class Sampler(threading.Thread):
     """Polls every GPU handle amdsmi reports: (t, energy J, socket W, clocks)."""
 
-    def __init__(self, period=0.02):
+    def __init__(self, period=0.02, pci_bus=None):
         super().__init__(daemon=True)
         import amdsmi
         self.smi = amdsmi
         amdsmi.amdsmi_init()
         self.handles = amdsmi.amdsmi_get_processor_handles()
+        if pci_bus is not None:
+            # only the GPU on this PCI bus (bench.py: the rank's own device)
+            keep = []
+            for h in self.handles:
+                try:
+                    bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)
+                    if int(bdf.split(":")[1], 16) == int(pci_bus):
+                        keep.append(h)
+                except Exception:  # noqa: BLE001
+                    pass
+            self.handles = keep
         self.period = period
         self.rows = []  # (t, handle index, energy_J, socket_W, mean gfxclk MHz, hotspot C, throttle)
         self.stop_ev = threading.Event()
