@@ -217,17 +217,18 @@ def _config0_gpu(torch, frames_host, want):
 
 
 def _start_power(torch, local):
-    """Socket power / clock / PPT throttling of this rank's GPU over the timed
-    region (tools/power_probe.py's amdsmi sampler, read-only queries); None
-    where amdsmi is unavailable."""
+    """Socket energy / clock / PPT throttling of this rank's GPU over the timed
+    region (tools/power_probe.py's amdsmi reader, read-only queries): one
+    reading right before the timed steps and one right after, so nothing runs
+    beside them; None where amdsmi is unavailable."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         from power_probe import Sampler
         bus = torch.cuda.get_device_properties(local).pci_bus_id
-        smp = Sampler(period=0.01, pci_bus=bus)
+        smp = Sampler(pci_bus=bus)  # not started: explicit readings only
         if len(smp.handles) != 1:
             return None
-        smp.start()
+        smp.sample()
         return smp
     except Exception:  # report nothing rather than fail the bench
         return None
@@ -237,18 +238,17 @@ def _power_report(smp, t0, t1, frames):
     if smp is None:
         return None
     try:
-        time.sleep(0.05)  # one more sample after the region
-        smp.stop_ev.set()
-        smp.join(timeout=2)
-        g = smp.window(t0, t1)[0]
+        smp.sample()
+        g = smp.window(t0 - 1.0, t1 + 1.0)[0]
         if not g or not g.get("avg_power_W_energy"):
             return None
         fps = frames / (t1 - t0)
-        return {"avg_W": g["avg_power_W_energy"], "gfxclk_MHz_mean": g.get("gfxclk_MHz_mean"),
-                "ppt_throttle_residency": g.get("ppt_residency_frac"), "samples": g.get("samples"),
+        clocks = [r[4] for r in smp.rows if t0 - 1.0 <= r[0] <= t1 + 1.0]
+        return {"avg_W": g["avg_power_W_energy"], "gfxclk_MHz_before_after": clocks,
+                "ppt_throttle_residency": g.get("ppt_residency_frac"),
                 "mJ_per_frame": round(g["avg_power_W_energy"] / fps * 1e3, 4),
-                "source": "amdsmi energy counter, per-XCD gfx clocks and PPT residency over the timed steps "
-                          "(tools/power_probe.py); DESIGN.md 'the limiter'"}
+                "source": "amdsmi energy counter and PPT residency accumulator read right before and right after "
+                          "the timed steps, gfx clock at both readings (tools/power_probe.py); DESIGN.md 'the limiter'"}
     except Exception:
         return None
 

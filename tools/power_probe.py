@@ -158,6 +158,8 @@ def main():
     print(json.dumps({"handles": smp.info}), flush=True)
     if os.environ.get("POWER_PROBE_GRAY") == "1":
         return gray_phases(smp, secs)
+    if os.environ.get("POWER_PROBE_VISUAL") == "1":
+        return visual_phases(smp, secs)
     op = DiffSeriesOperator(PixelFormat.RGB8, Mode.PerFrame, 8.0 / 255.0, time_kernel=True)
     frames = torch.empty((F, H, W, C), dtype=torch.uint8, device="cuda")
     op.synth_device(frames, W, H, 0xD1B5, 0)
@@ -300,6 +302,63 @@ def gray_phases(smp, secs):
     rep("grid-stride read (16-B nt loads), gray frames", t0, time.monotonic(), k,
         {"kernel_ms_median": round(float(np.median(ms)), 3)})
     op.close()
+    smp.stop_ev.set()
+    smp.join(timeout=2)
+
+
+def visual_phases(smp, secs):
+    """The two visual operators over 1000 resident 4K RGBA8 frames, back to
+    back: dips ComputeState frame_callback_batch (colour + sigmoid, the (S, m)
+    table kernel) and the dips_alt run loop (default properties, the diff
+    table kernel); bytes = read + write per frame."""
+    import torch
+    from dips_amd import DiffSeriesOperator, PixelFormat
+    from dips_amd.api import ChromaFilter, ComputeState, DiPsFilter
+    from dips_amd.alt import DiPsCompute
+    n = 1000
+    fb = W * H * 4
+    frames = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+    syn = DiffSeriesOperator(PixelFormat.RGBA8)
+    syn.synth_device(frames, W, H, 0xD1B5, 0)
+    syn.close()
+    out = torch.empty_like(frames)
+    torch.cuda.synchronize()
+
+    def rep(name, t0, t1, launches):
+        dt = t1 - t0
+        fps = launches * n / dt
+        g = smp.window(t0 + 0.25 * dt, t1)[0]
+        row = {"phase": name, "seconds": round(dt, 2), "launches": launches, "frames_per_s": round(fps, 1),
+               "GBps_read_write": round(fps * 2 * fb / 1e9, 1), "frac_of_8TBps": round(fps * 2 * fb / 1e9 / 8000, 4),
+               "gpu": g}
+        if g and g.get("avg_power_W_energy"):
+            row["mJ_per_frame"] = round(g["avg_power_W_energy"] / fps * 1e3, 4)
+        print(json.dumps(row), flush=True)
+
+    cs = ComputeState(True, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+    cs.frame_callback_batch_device(frames[:7], out[:7])
+    cs.frame_callback_batch_device(frames, out)
+    torch.cuda.synchronize()
+    k, t0 = 0, time.monotonic()
+    while time.monotonic() - t0 < secs:
+        for _ in range(5):
+            cs.frame_callback_batch_device(frames, out)
+        torch.cuda.synchronize()
+        k += 5
+    rep("compat_batch_lut_kernel (ComputeState batch, colour + sigmoid)", t0, time.monotonic(), k)
+    cs.close()
+    flags = [t == 2 for t in range(n)]
+    c = DiPsCompute(2, H, W)
+    c.send_frames_device(frames, out, flags)
+    torch.cuda.synchronize()
+    k, t0 = 0, time.monotonic()
+    while time.monotonic() - t0 < secs:
+        for _ in range(5):
+            c.send_frames_device(frames, out, flags)
+        torch.cuda.synchronize()
+        k += 5
+    rep("alt_batch_kernel LUT (dips_alt run loop, default properties)", t0, time.monotonic(), k)
+    c.close()
     smp.stop_ev.set()
     smp.join(timeout=2)
 
