@@ -148,6 +148,10 @@ struct dips_alt_handle {
     int occupancy = 0;
     int occupancy_pre = 0;  // the prefiltered (W > 1) batch kernel
     int occupancy_lut = 0, occupancy_lut_pre = 0;  // the epilogue-table forms
+    const void* occ_kernel = nullptr;  // the kernel each occupancy was computed for
+    const void* occ_kernel_pre = nullptr;
+    const void* occ_kernel_lut = nullptr;
+    const void* occ_kernel_lut_pre = nullptr;
     // epilogue table (alt_lut.h): the index (uploaded once) and the u16
     // contents for the current properties
     DevBuf lut_l1, lut_diffs, lut_slots, lut_l2;
@@ -304,7 +308,9 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
                         : dips::alt_batch_kernel_ptr(chroma, (int)h->p.filter_type, h->p.colorize != 0, fast);
     if (!k) return fail(h, DIPS_ERR_INVALID, "no batch kernel for these parameters");
     int& occ = lut ? (pre ? h->occupancy_lut_pre : h->occupancy_lut) : (pre ? h->occupancy_pre : h->occupancy);
-    if (occ == 0) {
+    const void*& occ_k = lut ? (pre ? h->occ_kernel_lut_pre : h->occ_kernel_lut) : (pre ? h->occ_kernel_pre : h->occ_kernel);
+    if (occ == 0 || occ_k != k) {
+        occ_k = k;
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, 256, 0) != hipSuccess || nb < 1) nb = 1;
         occ = nb;
@@ -314,7 +320,8 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
         if (st != DIPS_OK) return st;
     }
     const uint64_t n_vec = h->n_px() / 4u;
-    const uint64_t n_tiles = (n_vec + 64u * dips::kUnrollAlt - 1) / (64u * dips::kUnrollAlt);
+    const uint64_t U = lut ? (uint64_t)dips::alt_lut_unroll() : (uint64_t)dips::kUnrollAlt;
+    const uint64_t n_tiles = (n_vec + 64u * U - 1) / (64u * U);
     const uint64_t resident = (uint64_t)occ * 4u * (uint64_t)h->cu_count;
     // chunks of >= 16 frames; enough (tile, chunk) items to fill the chip
     uint64_t n_chunks = (resident + n_tiles - 1) / n_tiles;

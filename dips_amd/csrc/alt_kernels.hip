@@ -28,6 +28,8 @@
 #include "intensity_v2.h"
 #include "window_net.h"
 
+#include <cstdlib>
+
 namespace dips {
 
 namespace {
@@ -230,7 +232,8 @@ __device__ __forceinline__ uint32_t alt_lut_texel(const uint32_t* l1, const uint
 // FAST: the branch-free epilogue of epilogue_fast.h (sigmoid with |k| <= 160,
 // or no filter); otherwise the specification's visual_epilogue.  LUT: the
 // epilogue table of alt_lut.h in LDS instead (FILT / COL / FAST unused).
-template <int CH, int FILT, int COL, bool FAST, int U, bool LUT = false>
+// U vecs per lane; D frames of loads in flight per wave (D - 1 ahead).
+template <int CH, int FILT, int COL, bool FAST, int U, bool LUT = false, int D = 2>
 __global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
     __shared__ uint32_t lut1[LUT ? 2 * kAltLutClusters : 2];
     __shared__ uint16_t lut2[LUT ? kAltLutL2Max : 2];
@@ -343,17 +346,23 @@ __global__ __launch_bounds__(256) void alt_batch_kernel(AltBatchArgs a) {
         if (snap_now) unpack_snap();
     };
 
-    // two frames in flight per wave: frame t+1 loads while t is processed
-    uint32_t buf[2][U][4];
+    // D frames in flight per wave: frames t+1 .. t+D-1 load while t is processed
+    uint32_t buf[D][U][4];
     uint32_t t = t0;
-    load_frame(t, buf[0]);
-    while (true) {
-        if (t + 1 < t1) load_frame(t + 1, buf[1]);
-        process(t, buf[0]);
-        if (++t >= t1) break;
-        if (t + 1 < t1) load_frame(t + 1, buf[0]);
-        process(t, buf[1]);
-        if (++t >= t1) break;
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j)
+        if (t0 + (uint32_t)j < t1) load_frame(t0 + (uint32_t)j, buf[j]);
+    bool more = true;
+    while (more) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            if (more) {
+                // the slot processed one step ago takes frame t + D - 1
+                if (t + D - 1 < t1) load_frame(t + D - 1, buf[(j + D - 1) % D]);
+                process(t, buf[j]);
+                more = ++t < t1;
+            }
+        }
     }
 
     if (a.last_snap >= (int32_t)t0 && a.last_snap < (int32_t)t1) {
@@ -451,13 +460,35 @@ hipError_t launch_alt_lut_check(const uint32_t* l1, const uint16_t* l2, uint32_t
     return hipGetLastError();
 }
 
-const void* alt_batch_lut_kernel_ptr(int chroma) {
+template <int U, int D>
+static const void* alt_lut_ptr(int chroma) {
     switch (chroma) {
 #define DIPS_ALT_LUT_CH(C) \
-    case C: return reinterpret_cast<const void*>(&alt_batch_kernel<C, 0, 0, true, kUnrollAlt, true>);
+    case C: return reinterpret_cast<const void*>(&alt_batch_kernel<C, 0, 0, true, U, true, D>);
         DIPS_ALT_LUT_CH(0) DIPS_ALT_LUT_CH(1) DIPS_ALT_LUT_CH(2) DIPS_ALT_LUT_CH(3) DIPS_ALT_LUT_CH(kAltPrefiltered)
 #undef DIPS_ALT_LUT_CH
         default: return nullptr;
+    }
+}
+
+int alt_lut_variant() {
+    // DIPS_ALT_LUT_VARIANT = "<U><D>" (A/B runs): 22, 23, 33, 42, 43
+    if (const char* e = std::getenv("DIPS_ALT_LUT_VARIANT")) {
+        const int v = std::atoi(e);
+        if (v == 22 || v == 23 || v == 33 || v == 42 || v == 43) return v;
+    }
+    return 10 * kUnrollAltLut + kDepthAltLut;
+}
+
+int alt_lut_unroll() { return alt_lut_variant() / 10; }
+
+const void* alt_batch_lut_kernel_ptr(int chroma) {
+    switch (alt_lut_variant()) {
+        case 23: return alt_lut_ptr<2, 3>(chroma);
+        case 33: return alt_lut_ptr<3, 3>(chroma);
+        case 42: return alt_lut_ptr<4, 2>(chroma);
+        case 43: return alt_lut_ptr<4, 3>(chroma);
+        default: return alt_lut_ptr<2, 2>(chroma);
     }
 }
 

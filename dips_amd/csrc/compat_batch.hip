@@ -19,6 +19,8 @@
 #include "epilogue_fast.h"
 #include "intensity_v2.h"
 
+#include <cstdlib>
+
 namespace dips {
 
 namespace {
@@ -152,16 +154,23 @@ __global__ __launch_bounds__(256) void compat_batch_kernel(CompatBatchArgs a) {
         }
     };
 
-    uint32_t buf[2][U][4];
+    constexpr int D = 2;  // frames of loads in flight
+    uint32_t buf[D][U][4];
     uint32_t t = t0;
-    load_frame(t, buf[0]);
-    while (true) {
-        if (t + 1 < t1) load_frame(t + 1, buf[1]);
-        process(t, buf[0]);
-        if (++t >= t1) break;
-        if (t + 1 < t1) load_frame(t + 1, buf[0]);
-        process(t, buf[1]);
-        if (++t >= t1) break;
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j)
+        if (t0 + (uint32_t)j < t1) load_frame(t0 + (uint32_t)j, buf[j]);
+    bool more = true;
+    while (more) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            if (more) {
+                // the slot processed one step ago takes frame t + D - 1
+                if (t + D - 1 < t1) load_frame(t + D - 1, buf[(j + D - 1) % D]);
+                process(t, buf[j]);
+                more = ++t < t1;
+            }
+        }
     }
 
     if (c + 1 == a.n_chunks) {
@@ -219,7 +228,9 @@ __global__ __launch_bounds__(256) void compat_lut_kernel(uint16_t* __restrict__ 
 
 constexpr int kLutWaves = (int)kCompatLutWaves;
 
-template <int CH, int U>
+// U vecs per lane, D frames of loads in flight (D - 1 ahead of the one
+// being processed)
+template <int CH, int U, int D>
 __global__ __launch_bounds__(64 * kLutWaves) void compat_batch_lut_kernel(CompatBatchArgs a) {
     __shared__ uint32_t lds[32768];  // 65536 u16 entries (128 KiB)
     {
@@ -311,16 +322,22 @@ __global__ __launch_bounds__(64 * kLutWaves) void compat_batch_lut_kernel(Compat
         }
     };
 
-    uint32_t buf[2][U][4];
+    uint32_t buf[D][U][4];
     uint32_t t = t0;
-    load_frame(t, buf[0]);
-    while (true) {
-        if (t + 1 < t1) load_frame(t + 1, buf[1]);
-        process(t, buf[0]);
-        if (++t >= t1) break;
-        if (t + 1 < t1) load_frame(t + 1, buf[0]);
-        process(t, buf[1]);
-        if (++t >= t1) break;
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j)
+        if (t0 + (uint32_t)j < t1) load_frame(t0 + (uint32_t)j, buf[j]);
+    bool more = true;
+    while (more) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            if (more) {
+                // the slot processed one step ago takes frame t + D - 1
+                if (t + D - 1 < t1) load_frame(t + D - 1, buf[(j + D - 1) % D]);
+                process(t, buf[j]);
+                more = ++t < t1;
+            }
+        }
     }
 
     if (c + 1 == a.n_chunks) {
@@ -379,13 +396,36 @@ const void* compat_batch_kernel_ptr(int chroma, int filter, bool colorize, bool 
     }
 }
 
-const void* compat_batch_lut_kernel_ptr(int chroma) {
+template <int U, int D>
+static const void* cbl_ptr(int chroma) {
     switch (chroma) {
-        case 0: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<0, kUnrollCompatLut>);
-        case 1: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<1, kUnrollCompatLut>);
-        case 2: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<2, kUnrollCompatLut>);
-        case 3: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<3, kUnrollCompatLut>);
+        case 0: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<0, U, D>);
+        case 1: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<1, U, D>);
+        case 2: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<2, U, D>);
+        case 3: return reinterpret_cast<const void*>(&compat_batch_lut_kernel<3, U, D>);
         default: return nullptr;
+    }
+}
+
+int compat_lut_variant() {
+    // DIPS_COMPAT_LUT_VARIANT = "<U><D>" (A/B runs): 22, 23, 33, 42, 43, 44
+    if (const char* e = std::getenv("DIPS_COMPAT_LUT_VARIANT")) {
+        const int v = std::atoi(e);
+        if (v == 22 || v == 23 || v == 42 || v == 43 || v == 33 || v == 44) return v;
+    }
+    return 10 * kUnrollCompatLut + kDepthCompatLut;
+}
+
+int compat_lut_unroll() { return compat_lut_variant() / 10; }
+
+const void* compat_batch_lut_kernel_ptr(int chroma) {
+    switch (compat_lut_variant()) {
+        case 23: return cbl_ptr<2, 3>(chroma);
+        case 42: return cbl_ptr<4, 2>(chroma);
+        case 43: return cbl_ptr<4, 3>(chroma);
+        case 33: return cbl_ptr<3, 3>(chroma);
+        case 44: return cbl_ptr<4, 4>(chroma);
+        default: return cbl_ptr<2, 2>(chroma);
     }
 }
 

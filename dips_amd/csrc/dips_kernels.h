@@ -104,7 +104,18 @@ struct CompatBatchArgs {
     const uint16_t* lut;     // epilogue table (compat_batch_lut_kernel): 65536 x (R | G << 8)
 };
 constexpr int kUnrollCompatBatch = 2;
-constexpr int kUnrollCompatLut = 2;  // U = 4 measured equal (profiles/r02_compat_lut_bench2.jsonl)
+// U vecs per lane and D frames of loads in flight per wave of the table
+// kernel.  In one process over one batch (tools/compat_variant_ab.py,
+// profiles/r02_compat_variant_ab.jsonl) U = 4, D = 3 ran 76.2 % of 8 TB/s
+// read + write, against 72.4 % for U = 2, D = 2 (an earlier cross-process
+// A/B had called U = 4 equal).  126 VGPRs: the 1024-thread workgroup's
+// budget is 128, and D = 4 spills.
+constexpr int kUnrollCompatLut = 4;
+constexpr int kDepthCompatLut = 3;
+// (U, D) of the table kernel this call runs: the defaults, or
+// DIPS_COMPAT_LUT_VARIANT = 22 / 23 / 42 / 43 for A/B runs
+int compat_lut_variant();
+int compat_lut_unroll();
 constexpr uint32_t kCompatLutWaves = 16;  // waves per workgroup of compat_batch_lut_kernel (one per CU)
 // the epilogue table of the current properties: lut[S * 256 + m]
 hipError_t launch_compat_lut(uint16_t* lut, uint32_t filter, float k, bool colorize, hipStream_t s);
@@ -117,6 +128,15 @@ hipError_t launch_compat_batch(const CompatBatchArgs& a, int chroma, int filter,
 // dips_alt DiPsCompute (alt_kernels.hip).
 constexpr int kAltMaxTextures = 16;  // MAX_TEMPORAL_ARRAY_SIZE (dips_alt pre_compute_shader.wgsl:12)
 constexpr int kUnrollAlt = 2;        // vecs (4 px) per lane of alt_batch_kernel
+// vecs per lane / frames of loads in flight of its epilogue-table form; A/B
+// variants by DIPS_ALT_LUT_VARIANT = 22 / 23 / 33 / 42 / 43.  In one process
+// over one batch (tools/alt_variant_ab.py, profiles/r02_alt_variant_ab.jsonl):
+// U = 4, D = 2 72.8 % of 8 TB/s read + write, U = 2, D = 2 72.1 %, the others
+// 71.2-72.3 % (8 groups of 256 threads per CU already keep enough in flight).
+constexpr int kUnrollAltLut = 4;
+constexpr int kDepthAltLut = 2;
+int alt_lut_variant();
+int alt_lut_unroll();
 
 struct AltArgs {                     // one send_frame dispatch
     const uint8_t* slots[kAltMaxTextures];  // RGBA8 contents of the N texture slots
