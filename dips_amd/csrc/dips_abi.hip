@@ -218,7 +218,7 @@ FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t nvec = npx / 16u;
     if (nvec == 0 || npx >= (1ull << 31) || n_frames == 0) return g;
-    const uint64_t U = (uint64_t)dips::kUnrollGrayLut;
+    const uint64_t U = (uint64_t)(gray_lut_layout() == 2 ? dips::gray_lut_unroll() : dips::kUnrollGrayLut);
     g.vec_bytes = nvec * 16u;
     g.tail_px0 = nvec * 16u;
     g.n_tiles = (nvec + 64 * U - 1) / (64 * U);
@@ -660,7 +660,7 @@ dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_
         resident = (uint64_t)h->cb_occupancy * 4u * (uint64_t)h->cu_count;
     }
     const uint64_t n_vec = npx / 4u;
-    const uint64_t U = lut ? (uint64_t)dips::kUnrollCompatLut : (uint64_t)dips::kUnrollCompatBatch;
+    const uint64_t U = lut ? (uint64_t)dips::compat_lut_unroll() : (uint64_t)dips::kUnrollCompatBatch;
     const uint64_t n_tiles = (n_vec + 64u * U - 1) / (64u * U);
     uint64_t n_chunks = (resident + n_tiles - 1) / n_tiles;
     n_chunks = std::min<uint64_t>(n_chunks, (m + 15u) / 16u);

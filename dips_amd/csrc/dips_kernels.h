@@ -13,11 +13,14 @@ constexpr int kUnrollRGB = 4;   // 1024 px / wave / frame for RGB8 and RGBA8
 constexpr int kUnrollGray = 2;  // 2048 px / wave / frame for GRAY8
 constexpr int kUnrollV2 = 4;    // series_v2_kernel (RGB8/RGBA8): 1024 px / wave / frame
 // series_gray_lut_kernel: 64 * 16 * U px / wave / frame (U = 4: 4K gray8
-// 61.9-62.1 % of 8 TB/s vs 60.4-60.6 % at U = 2, profiles/r02_gray_lut_unroll.jsonl)
+// 61.9-62.1 % of 8 TB/s vs 60.4-60.6 % at U = 2, profiles/r02_gray_lut_unroll.jsonl;
+// confirmed in one process with the final kernel: U = 4 65.5-65.9 %, U = 3
+// 64.9-65.7 %, U = 2 63.6-63.9 %, profiles/r02_gray_variant_ab.jsonl)
 #ifndef DIPS_UNROLL_GRAY_LUT
 #define DIPS_UNROLL_GRAY_LUT 4
 #endif
 constexpr int kUnrollGrayLut = DIPS_UNROLL_GRAY_LUT;
+int gray_lut_unroll();  // U of this call's GRAY8 table kernel (DIPS_GRAY_LUT_U for A/B runs)
 constexpr uint32_t kGrayLutWaves = 16;  // its waves per workgroup (one 1024-thread group per CU)
 constexpr size_t kGrayLutBytes = 131072;  // its T_d / T_c tables
 // Prefetch depth: frames of loads each wave keeps in flight.

@@ -33,6 +33,8 @@
 // (mode 2) forms SI_fixed = 2 (8421504 sum d + sum corr) in 64 bits.
 #include "series_common.h"
 
+#include <cstdlib>
+
 namespace dips {
 
 constexpr uint32_t kGrayLutTcOffset = 65535u;  // T_c's byte offset in LDS (the ds offset field's maximum;
@@ -268,16 +270,30 @@ __global__ __launch_bounds__(64 * kGrayWaves) void series_gray_lut_kernel(Series
 
 }  // namespace
 
-template <int L>
+template <int U, int L>
 static const void* gray_ptr(bool per_frame, bool map) {
-    return per_frame ? (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, true, true, L>)
-                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, true, false, L>))
-                     : (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, false, true, L>)
-                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, false, false, L>));
+    return per_frame ? (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<U, true, true, L>)
+                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<U, true, false, L>))
+                     : (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<U, false, true, L>)
+                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<U, false, false, L>));
+}
+
+int gray_lut_unroll() {
+    // DIPS_GRAY_LUT_U = 2 / 3 / 4 (A/B runs; layout 2 only), else the default
+    if (const char* e = std::getenv("DIPS_GRAY_LUT_U")) {
+        const int u = std::atoi(e);
+        if (u == 2 || u == 3 || u == 4) return u;
+    }
+    return kUnrollGrayLut;
 }
 
 const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout) {
-    return layout == 2 ? gray_ptr<2>(per_frame, map) : gray_ptr<1>(per_frame, map);
+    if (layout != 2) return gray_ptr<kUnrollGrayLut, 1>(per_frame, map);
+    switch (gray_lut_unroll()) {
+        case 2: return gray_ptr<2, 2>(per_frame, map);
+        case 3: return gray_ptr<3, 2>(per_frame, map);
+        default: return gray_ptr<4, 2>(per_frame, map);
+    }
 }
 
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""gray_variant_ab.py -- in-process A/B of the GRAY8 table kernel's vecs per
+lane (DIPS_GRAY_LUT_U, read per call): one batch of 4K gray8 frames,
+per-frame, tau 8/255; variants alternated over rounds, kernel time by
+hipEvents, series compared with the first variant's.
+Run on the GPU box: python tools/gray_variant_ab.py [rounds] [frames] [variants]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 6000
+    variants = (sys.argv[3] if len(sys.argv) > 3 else "4,2,3").split(",")
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    W, H = 3840, 2160
+    op = DiffSeriesOperator(PixelFormat.Gray8, Mode.PerFrame, 8.0 / 255.0, time_kernel=True)
+    frames = torch.empty((n, H, W), dtype=torch.uint8, device="cuda")
+    op.synth_device(frames, W, H, 0xD1B5, 0)
+    ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+    ref = None
+    for r in range(rounds):
+        for v in variants:
+            os.environ["DIPS_GRAY_LUT_U"] = v
+            op.run_device(frames, ser)
+            torch.cuda.synchronize()
+            op.kernel_time(reset=True)
+            for _ in range(5):
+                op.run_device(frames, ser)
+            torch.cuda.synchronize()
+            ms = float(np.median(op.kernel_times()))
+            h = ser.cpu().numpy()
+            if ref is None:
+                ref = h
+            gbs = n * W * H / (ms / 1e3) / 1e9
+            print(json.dumps({"round": r, "U": int(v), "kernel_ms": round(ms, 4), "GBps": round(gbs, 1),
+                              "frac_of_8TBps": round(gbs / 8000, 4), "series_equal_first": bool(np.array_equal(h, ref))}),
+                  flush=True)
+    op.close()
+
+
+if __name__ == "__main__":
+    main()
