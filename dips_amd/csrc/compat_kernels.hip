@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256) void compat_precompute_kernel(CompatArgs a) {
 
 // compute_main's per-pixel tail once the newest slot's filtered intensity fi
 // is known (dips_shader.wgsl:187-239).
-__device__ __forceinline__ void compat_finish(const CompatArgs& a, uint64_t p, float fi) {
+__device__ __forceinline__ uint32_t compat_texel(const CompatArgs& a, uint64_t p, float fi) {
     // in-place store of the filtered newest slot, quantised (dips_shader.wgsl:187)
     const uint32_t qi = unorm_store(fi);
     *reinterpret_cast<uint32_t*>(a.slots[a.newest] + 4 * p) = qi | (qi << 8) | (qi << 16) | (255u << 24);
@@ -147,7 +147,7 @@ __device__ __forceinline__ void compat_finish(const CompatArgs& a, uint64_t p, f
     }
     const float original = unorm_load(a.start[4 * p]);  // textureLoad(start_texture).r (:213)
     const float diff = original - upper_median4(m[0], m[1], m[2], m[3]);
-    *reinterpret_cast<uint32_t*>(a.out + 4 * p) = visual_epilogue(diff, a.filter, a.sensitivity, a.colorize != 0u);
+    return visual_epilogue(diff, a.filter, a.sensitivity, a.colorize != 0u);
 }
 
 // compute_main for one frame once `raw` holds the newest slot's filter
@@ -161,7 +161,27 @@ __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (x >= a.width || y >= yend) return;
     const uint64_t p = (uint64_t)y * a.width + x;
-    compat_finish(a, p, texel_intensity(a.raw, p, a.chroma));
+    *reinterpret_cast<uint32_t*>(a.out + 4 * p) = compat_texel(a, p, texel_intensity(a.raw, p, a.chroma));
+}
+
+// The same with the frame read from, and the output written to, pinned HOST
+// memory over PCIe (the per-frame call's zero-copy form: no DMA engine, the
+// kernel's loads and stores move both directions at once).  System-scope
+// accesses: the loads see what the host threads wrote before the launch and
+// the stores reach host memory, bypassing the non-coherent cache levels.
+// One thread per pixel over the rows' pixel range, so that a wave moves 256
+// contiguous bytes each way.  (Four pixels per thread through 16-B
+// system-coherent buffer loads / stores measured slower: 557-575 against
+// 695-701 frames/s of 4K per-frame calls, tools/callback_direct_ab.py.)
+__global__ __launch_bounds__(256) void compat_main_host_kernel(CompatArgs a) {
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    const uint64_t p = (uint64_t)a.y0 * a.width + (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= (uint64_t)yend * a.width) return;
+    const uint32_t v = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a.raw + 4 * p), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+    const float fi = intensity_rgb(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, a.chroma);
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 4 * p), compat_texel(a, p, fi), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // A ring slot as frame_callback leaves it for a W = 1 frame: the gray texel
@@ -263,6 +283,14 @@ hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s) {
     if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
     dim3 grid((a.width + kTile - 1) / kTile, (yend - a.y0 + kTile - 1) / kTile);
     hipLaunchKernelGGL(compat_main_kernel, grid, dim3(kTile, kTile), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s) {
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
+    const uint64_t n_px = (uint64_t)(yend - a.y0) * a.width;
+    hipLaunchKernelGGL(compat_main_host_kernel, dim3((uint32_t)((n_px + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 // fresh pool (the parent's workers do not exist there).
 #pragma once
 
+#include <immintrin.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -19,6 +20,7 @@
 #include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -79,6 +81,11 @@ class CopyPool {
             // child inherited and start a new one
             unsigned hw = std::thread::hardware_concurrency();
             hw = hw == 0 ? 1u : std::min(hw, 8u);
+            // DIPS_COPY_THREADS (1..32) overrides the count, read once per process
+            if (const char* e = std::getenv("DIPS_COPY_THREADS")) {
+                const long v = std::strtol(e, nullptr, 10);
+                if (v >= 1 && v <= 32) hw = (unsigned)v;
+            }
             pool = new CopyPool(hw - 1u);
             owner = getpid();
         }
@@ -121,17 +128,54 @@ class CopyPool {
     bool stop_ = false;
 };
 
+// Streaming copy for the staging buffers: every byte is written once and the
+// CPU does not read it back (the DMA engine does, or the caller much later),
+// so non-temporal 32-B stores skip the read-for-ownership of each
+// destination line and leave the caches alone.  The closing sfence makes the
+// write-combined stores globally visible before the caller enqueues a DMA
+// that reads them.
+__attribute__((target("avx2"))) inline void stream_copy_avx2(uint8_t* d, const uint8_t* s, size_t n) {
+    size_t head = (32u - ((uintptr_t)d & 31u)) & 31u;
+    if (head > n) head = n;
+    std::memcpy(d, s, head);
+    size_t i = head;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 64));
+        const __m256i e = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i + 96), e);
+    }
+    std::memcpy(d + i, s + i, n - i);
+    _mm_sfence();
+}
+
+// The staging copy: streaming stores for pieces of >= 64 KiB on CPUs with
+// AVX2, memcpy otherwise.  DIPS_NT_COPY=0 selects memcpy (read per call, so
+// one process can A/B the two: tools/callback_rate.py).
+inline void host_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    const char* e = std::getenv("DIPS_NT_COPY");
+    if (avx2 && bytes >= (64u << 10) && !(e && e[0] == '0'))
+        stream_copy_avx2(dst, src, bytes);
+    else
+        std::memcpy(dst, src, bytes);
+}
+
 // Host copy in ~4 MiB pieces over the pool.
 inline void pool_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
     const size_t kPiece = 4u << 20;
     if (bytes < 2 * kPiece) {
-        std::memcpy(dst, src, bytes);
+        host_copy(dst, src, bytes);
         return;
     }
     const size_t n = (bytes + kPiece - 1) / kPiece;
     CopyPool::global().run(n, [&](size_t i) {
         const size_t o = i * kPiece;
-        std::memcpy(dst + o, src + o, std::min(kPiece, bytes - o));
+        host_copy(dst + o, src + o, std::min(kPiece, bytes - o));
     });
 }
 

@@ -777,6 +777,29 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
     a.filter = h->p.filter_type;
     a.sensitivity = h->p.sensitivity;
     a.colorize = h->p.colorize ? 1u : 0u;
+    // zero-copy form (default; DIPS_CALLBACK_DIRECT=0 selects the DMA form
+    // above): the main kernel reads the staged stripe from pinned host memory
+    // and writes its output there, the pool copies stripes in and out
+    const char* direct_env = std::getenv("DIPS_CALLBACK_DIRECT");
+    if (!direct_env || direct_env[0] != '0') {
+        void *din = nullptr, *dout = nullptr;
+        DIPS_HIP(h, hipHostGetDevicePointer(&din, h->io.p, 0));
+        DIPS_HIP(h, hipHostGetDevicePointer(&dout, h->io_out.p, 0));
+        a.raw = static_cast<const uint8_t*>(din);
+        a.out = static_cast<uint8_t*>(dout);
+        // odd stripes on copy_stream (idle here, synchronised above); every
+        // stripe's kernel has finished when the call returns
+        const char* one_env = std::getenv("DIPS_DIRECT_STREAMS");  // "1": every stripe on the compute stream (A/B)
+        const hipStream_t cs[2] = {h->stream, (one_env && one_env[0] == '1') ? h->stream : h->copy_stream};
+        DIPS_HIP(h, dips_host::run_striped_frame_direct(frame, out, H, row, h->io.bytes(), h->io_out.bytes(), cs,
+                                                        h->device, h->pieces,
+                                                        [&](uint32_t y0, uint32_t y1, hipStream_t s) {
+                                                            a.y0 = y0;
+                                                            a.y1 = y1;
+                                                            return dips::launch_compat_main_host(a, s);
+                                                        }));
+        return 1;
+    }
     DIPS_HIP(h, dips_host::run_striped_frame(frame, out, H, row, h->io.bytes(), h->io_out.bytes(), slot,
                                              h->out.as<uint8_t>(), h->copy_stream, h->stream, h->up_pieces,
                                              h->pieces, [&](uint32_t y0, uint32_t y1) {

@@ -231,6 +231,8 @@ hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, 
 hipError_t launch_read_walk(const SeriesArgs& a, int vec_bytes, uint32_t blocks, uint32_t* out, hipStream_t s);
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s);
+// compat_main with raw / out in pinned host memory (zero-copy per-frame call)
+hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, uint32_t chroma, hipStream_t s);
 // W > 1 steady state: the ring texel compute_main stores for each of n frames
 // (gray q(spatial_median_filter(frame)), dips_shader.wgsl:120-170, 187), so

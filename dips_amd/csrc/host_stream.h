@@ -14,6 +14,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -48,7 +50,7 @@ inline hipError_t upload_via(void* dev, const uint8_t* host, size_t bytes, uint8
     std::atomic<int> err{(int)hipSuccess};
     CopyPool::global().run(n, [&](size_t i) {
         const size_t o = i * kPieceBytes, len = std::min(kPieceBytes, bytes - o);
-        std::memcpy(pin + o, host + o, len);
+        host_copy(pin + o, host + o, len);
         const hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(dev) + o, pin + o, len, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) err.store((int)e);
     });
@@ -98,7 +100,7 @@ inline hipError_t download_via(uint8_t* host, const void* dev, size_t bytes, uin
             return;
         }
         const size_t o = i * kPieceBytes;
-        std::memcpy(host + o, pin + o, std::min(kPieceBytes, bytes - o));
+        host_copy(host + o, pin + o, std::min(kPieceBytes, bytes - o));
     });
     return (hipError_t)err.load();
 }
@@ -120,13 +122,23 @@ hipError_t run_striped_frame(const uint8_t* frame, uint8_t* out, uint32_t height
     hipError_t e = up_ev.ensure(n_s);
     if (e == hipSuccess) e = down_ev.ensure(n_s);
     if (e != hipSuccess) return e;
+    // DIPS_STRIPE_TRACE: per call, the host time (us from entry) at which each
+    // stripe was staged / its DMA enqueued, the kernels enqueued, each
+    // readback landed and was copied out (tools/nt_copy_ab.py --trace)
+    static const bool trace = std::getenv("DIPS_STRIPE_TRACE") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto tbeg = clk::now();
+    std::vector<double> ts(trace ? 4 * n_s : 0);
+    auto since = [&]() { return std::chrono::duration<double, std::micro>(clk::now() - tbeg).count(); };
     std::atomic<int> err{(int)hipSuccess};
     CopyPool::global().run(n_s, [&](size_t si) {
         const size_t o = si * rows * row, len = std::min<size_t>((size_t)rows * row, fb - o);
-        std::memcpy(pin_in + o, frame + o, len);
+        host_copy(pin_in + o, frame + o, len);
+        if (trace) ts[4 * si] = since();
         hipError_t r = hipMemcpyAsync(dev_in + o, pin_in + o, len, hipMemcpyHostToDevice, up);
         if (r == hipSuccess) r = hipEventRecord(up_ev.ev[si], up);
         if (r != hipSuccess) err.store((int)r);
+        if (trace) ts[4 * si + 1] = since();
     });
     if ((e = (hipError_t)err.load()) != hipSuccess) return e;
     for (uint32_t si = 0; si < n_s; ++si) {
@@ -138,15 +150,96 @@ hipError_t run_striped_frame(const uint8_t* frame, uint8_t* out, uint32_t height
             return e;
         if ((e = hipEventRecord(down_ev.ev[si], compute)) != hipSuccess) return e;
     }
+    const double t_enq = trace ? since() : 0.0;
     CopyPool::global().run(n_s, [&](size_t si) {
         const hipError_t r = hipEventSynchronize(down_ev.ev[si]);
         if (r != hipSuccess) {
             err.store((int)r);
             return;
         }
+        if (trace) ts[4 * si + 2] = since();
         const size_t o = si * rows * row;
-        std::memcpy(out + o, pin_out + o, std::min<size_t>((size_t)rows * row, fb - o));
+        host_copy(out + o, pin_out + o, std::min<size_t>((size_t)rows * row, fb - o));
+        if (trace) ts[4 * si + 3] = since();
     });
+    if (trace) {
+        std::fprintf(stderr, "stripes %u enqueued %.0f us:", n_s, t_enq);
+        for (uint32_t si = 0; si < n_s; ++si)
+            std::fprintf(stderr, " [%.0f %.0f %.0f %.0f]", ts[4 * si], ts[4 * si + 1], ts[4 * si + 2], ts[4 * si + 3]);
+        std::fprintf(stderr, " end %.0f\n", since());
+    }
+    return (hipError_t)err.load();
+}
+
+// One frame through a per-pixel kernel that reads its input from, and writes
+// its output to, the pinned buffers themselves (zero-copy over PCIe, no DMA
+// engine): the pool stages stripe s into `pin_in` and at once launches
+// launch(y0, y1, stream) for it (stripes in any order -- rows are
+// independent), then copies stripe s of `pin_out` to `out` as soon as its
+// kernel has finished.  Even stripes go to compute[0], odd ones to
+// compute[1], so that one stripe's PCIe reads run beside the previous one's
+// writes.  Tasks 0..n-1 stage + launch, n..2n-1 copy out; a
+// copy-out task waits for its stripe's launch, so one worker or many run the
+// same schedule.  The caller makes sure no earlier kernel still reads
+// `pin_in` or writes `pin_out`.
+template <typename Launch>
+hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t height, size_t row,
+                                    uint8_t* pin_in, const uint8_t* pin_out, const hipStream_t (&compute)[2],
+                                    int device, PieceEvents& ev, Launch&& launch) {
+    const size_t fb = row * height;
+    const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
+    const uint32_t n_s = (height + rows - 1) / rows;
+    hipError_t e = ev.ensure(n_s);
+    if (e != hipSuccess) return e;
+    std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[n_s]);
+    for (uint32_t i = 0; i < n_s; ++i) ready[i].store(0, std::memory_order_relaxed);
+    std::mutex launch_mu;
+    std::atomic<int> err{(int)hipSuccess};
+    static const bool trace = std::getenv("DIPS_STRIPE_TRACE") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto tbeg = clk::now();
+    std::vector<double> ts(trace ? 4 * n_s : 0);
+    auto since = [&]() { return std::chrono::duration<double, std::micro>(clk::now() - tbeg).count(); };
+    CopyPool::global().run(2 * (size_t)n_s, [&](size_t i) {
+        const size_t si = i < n_s ? i : i - n_s;
+        const uint32_t y0 = (uint32_t)si * rows, y1 = std::min(height, y0 + rows);
+        const size_t o = (size_t)y0 * row, len = (size_t)(y1 - y0) * row;
+        if (i < n_s) {
+            host_copy(pin_in + o, frame + o, len);
+            if (trace) ts[4 * si] = since();
+            hipError_t r;
+            {
+                // the kernel and its event back to back on the stream
+                std::lock_guard<std::mutex> lk(launch_mu);
+                hipStream_t cs = compute[si & 1u];
+                r = hipSetDevice(device);
+                if (r == hipSuccess) r = launch(y0, y1, cs);
+                if (r == hipSuccess) r = hipEventRecord(ev.ev[si], cs);
+            }
+            if (r != hipSuccess) err.store((int)r);
+            if (trace) ts[4 * si + 1] = since();
+            ready[si].store(r == hipSuccess ? 1 : -1, std::memory_order_release);
+            return;
+        }
+        int st;
+        while ((st = ready[si].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        if (st < 0) return;
+        const hipError_t r = hipEventSynchronize(ev.ev[si]);
+        if (r != hipSuccess) {
+            err.store((int)r);
+            return;
+        }
+        if (trace) ts[4 * si + 2] = since();
+        host_copy(out + o, pin_out + o, len);
+        if (trace) ts[4 * si + 3] = since();
+    });
+    if (trace) {
+        std::fprintf(stderr, "direct stripes %u:", n_s);
+        for (uint32_t si = 0; si < n_s; ++si)
+            std::fprintf(stderr, " [%.0f %.0f %.0f %.0f]", ts[4 * si], ts[4 * si + 1], ts[4 * si + 2], ts[4 * si + 3]);
+        std::fprintf(stderr, " end %.0f\n", since());
+    }
+    (void)fb;
     return (hipError_t)err.load();
 }
 

@@ -54,3 +54,53 @@ def test_frame_geometry_checks():
 def test_modes_and_formats():
     assert int(Mode.Overall) == 0 and int(Mode.PerFrame) == 1
     assert [int(f) for f in PixelFormat] == [1, 3, 4]
+
+
+_COPY_CHECK = r"""
+#include "copy_pool.h"
+#include <cstdio>
+#include <random>
+int main() {
+    std::mt19937_64 rng(7);
+    std::vector<uint8_t> src(9u << 20), dst((9u << 20) + 64), want;
+    for (auto& b : src) b = (uint8_t)rng();
+    const size_t sizes[] = {0, 1, 31, 32, 127, 128, 129, 65535, 65536, 65537, 1u << 20, (4u << 20) + 77, 9u << 20};
+    int bad = 0;
+    for (int nt = 0; nt < 2; ++nt) {
+        setenv("DIPS_NT_COPY", nt ? "1" : "0", 1);
+        for (size_t n : sizes)
+            for (size_t so = 0; so < 4; ++so)
+                for (size_t dof = 0; dof < 40; dof += 13) {
+                    if (so + n > src.size() || dof + n + 8 > dst.size()) continue;
+                    std::fill(dst.begin(), dst.end(), 0xA5);
+                    dips_host::host_copy(dst.data() + dof, src.data() + so, n);
+                    for (size_t i = 0; i < dof; ++i) bad += dst[i] != 0xA5;
+                    bad += std::memcmp(dst.data() + dof, src.data() + so, n) != 0;
+                    for (size_t i = dof + n; i < dof + n + 8; ++i) bad += dst[i] != 0xA5;
+                }
+        std::fill(dst.begin(), dst.end(), 0);
+        dips_host::pool_copy(dst.data() + 3, src.data() + 1, (9u << 20) - 1);
+        bad += std::memcmp(dst.data() + 3, src.data() + 1, (9u << 20) - 1) != 0;
+    }
+    std::printf("bad=%d\n", bad);
+    return bad != 0;
+}
+"""
+
+
+def test_host_staging_copy_matches_memcpy(tmp_path):
+    """copy_pool.h: the streaming staging copy (AVX2 non-temporal stores) and
+    the pooled piecewise copy equal memcpy for every size class and source /
+    destination alignment, and write nothing outside the destination range."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dips_amd", "csrc")
+    src = tmp_path / "copy_check.cpp"
+    src.write_text(_COPY_CHECK)
+    exe = tmp_path / "copy_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", f"-I{csrc}", str(src), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout + r.stderr
