@@ -668,6 +668,28 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     // the compute stream while stripes s+1.. still go up
     ALT_HIP(h, h->io_out.ensure(fb));
     ALT_HIP(h, hipStreamSynchronize(h->meta_stream));  // no upload of an earlier call still reads `io`
+    // zero-copy form (default; DIPS_CALLBACK_DIRECT=0 selects the DMA form
+    // below): the kernel reads the staged stripe from pinned host memory,
+    // stores it into the slot and writes its output to pinned host memory;
+    // odd stripes on meta_stream (idle here, synchronised above)
+    const char* direct_env = std::getenv("DIPS_CALLBACK_DIRECT");
+    if (!direct_env || direct_env[0] != '0') {
+        void *din = nullptr, *dout = nullptr;
+        ALT_HIP(h, hipHostGetDevicePointer(&din, h->io.p, 0));
+        ALT_HIP(h, hipHostGetDevicePointer(&dout, h->io_out.p, 0));
+        a.out = static_cast<uint8_t*>(dout);
+        const uint32_t newest = (uint32_t)((h->sent - 1) % N);
+        const char* one_env = std::getenv("DIPS_DIRECT_STREAMS");  // "1": every stripe on the compute stream
+        const hipStream_t cs[2] = {h->stream, (one_env && one_env[0] == '1') ? h->stream : h->meta_stream};
+        ALT_HIP(h, dips_host::run_striped_frame_direct(
+                       frame, out, h->height, (size_t)h->width * 4u, h->io.bytes(), h->io_out.bytes(), cs, h->device,
+                       h->pieces, [&](uint32_t y0, uint32_t y1, hipStream_t s) {
+                           a.y0 = y0;
+                           a.y1 = y1;
+                           return dips::launch_alt_frame_host(a, static_cast<const uint8_t*>(din), slot, newest, s);
+                       }));
+        return DIPS_OK;
+    }
     ALT_HIP(h, dips_host::run_striped_frame(frame, out, h->height, (size_t)h->width * 4u, h->io.bytes(),
                                             h->io_out.bytes(), slot, h->out1.as<uint8_t>(), h->meta_stream,
                                             h->stream, h->up_pieces, h->pieces, [&](uint32_t y0, uint32_t y1) {

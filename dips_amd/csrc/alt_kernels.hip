@@ -113,7 +113,7 @@ __device__ __forceinline__ uint32_t gray_rgba(uint32_t s) { return s | (s << 8) 
 // send_frame's per-pixel tail once the N slot intensities are known
 // (:228-261).
 template <int N>
-__device__ __forceinline__ void alt_finish(const AltArgs& a, uint64_t p, const float (&v)[N]) {
+__device__ __forceinline__ uint32_t alt_texel(const AltArgs& a, uint64_t p, const float (&v)[N]) {
     const float med = alt_temporal<N>(v);
     uint32_t o;
     if (a.snapshot) {
@@ -127,7 +127,12 @@ __device__ __forceinline__ void alt_finish(const AltArgs& a, uint64_t p, const f
         // DIFF_SCALE / colour (:237-261)
         o = visual_epilogue(unorm_load(a.snap[p]) - med, a.filter, a.scalar, a.colorize != 0u);
     }
-    *reinterpret_cast<uint32_t*>(a.out + 4 * p) = o;
+    return o;
+}
+
+template <int N>
+__device__ __forceinline__ void alt_finish(const AltArgs& a, uint64_t p, const float (&v)[N]) {
+    *reinterpret_cast<uint32_t*>(a.out + 4 * p) = alt_texel<N>(a, p, v);
 }
 
 // SIDE = 2 * (window / 2): 0 for W = 1 (one pixel per thread, 16x16
@@ -172,6 +177,30 @@ __global__ __launch_bounds__(256) void alt_frame_kernel(AltArgs a) {
         const uint32_t y = yb + r;
         if (x < a.width && y < yend) alt_finish<N>(a, (uint64_t)y * a.width + x, v[r]);
     }
+}
+
+// send_frame for W = 1 in the per-frame call's zero-copy form: the new frame
+// is read from pinned HOST memory (`in`) over PCIe, written into its ring
+// slot (queue.write_texture, dips_alt/src/dips_compute/mod.rs:498-646) and
+// used as that slot's texel; the output goes straight to pinned host memory
+// (a.out).  System-scope accesses (see compat_main_host_kernel).  One thread
+// per pixel over the rows' pixel range.
+template <int N>
+__global__ __launch_bounds__(256) void alt_frame_host_kernel(AltArgs a, const uint8_t* in, uint8_t* newest_slot,
+                                                             uint32_t newest) {
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    const uint64_t p = (uint64_t)a.y0 * a.width + (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= (uint64_t)yend * a.width) return;
+    const uint32_t raw =
+        __hip_atomic_load(reinterpret_cast<const uint32_t*>(in + 4 * p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    *reinterpret_cast<uint32_t*>(newest_slot + 4 * p) = raw;
+    float v[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        v[k] = (uint32_t)k == newest ? intensity_rgb(raw & 0xFFu, (raw >> 8) & 0xFFu, (raw >> 16) & 0xFFu, a.chroma)
+                                     : alt_texel_intensity(a.slots[k], p, a.chroma);
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 4 * p), alt_texel<N>(a, p, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -506,6 +535,30 @@ hipError_t launch_alt_lut_fill(uint16_t* lut_l2, const float* diffs, const uint1
     hipLaunchKernelGGL(alt_lut_fill_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, lut_l2, diffs, slots, n, filter,
                        k, colorize ? 1u : 0u);
     return hipGetLastError();
+}
+
+template <int N>
+hipError_t launch_frame_host_n(const AltArgs& a, const uint8_t* in, uint8_t* newest_slot, uint32_t newest,
+                               hipStream_t s) {
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    if (a.y0 >= yend || yend > a.height || a.window > 1 || newest >= (uint32_t)N) return hipErrorInvalidValue;
+    const uint64_t n_px = (uint64_t)(yend - a.y0) * a.width;
+    hipLaunchKernelGGL((alt_frame_host_kernel<N>), dim3((uint32_t)((n_px + 255) / 256)), dim3(256), 0, s, a, in,
+                       newest_slot, newest);
+    return hipGetLastError();
+}
+
+hipError_t launch_alt_frame_host(const AltArgs& a, const uint8_t* in, uint8_t* newest_slot, uint32_t newest,
+                                 hipStream_t s) {
+    switch (a.n_tex) {
+#define DIPS_ALT_N(NV) \
+    case NV: return launch_frame_host_n<NV>(a, in, newest_slot, newest, s);
+        DIPS_ALT_N(1) DIPS_ALT_N(2) DIPS_ALT_N(3) DIPS_ALT_N(4) DIPS_ALT_N(5) DIPS_ALT_N(6) DIPS_ALT_N(7)
+        DIPS_ALT_N(8) DIPS_ALT_N(9) DIPS_ALT_N(10) DIPS_ALT_N(11) DIPS_ALT_N(12) DIPS_ALT_N(13)
+        DIPS_ALT_N(14) DIPS_ALT_N(15) DIPS_ALT_N(16)
+#undef DIPS_ALT_N
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_alt_frame(const AltArgs& a, hipStream_t s) {

@@ -174,6 +174,11 @@ struct AltBatchArgs {                // a run of frames, N = 2, W = 1
 };
 
 hipError_t launch_alt_frame(const AltArgs& a, hipStream_t s);
+// send_frame (W = 1) reading the new frame from pinned host memory `in`,
+// storing it into `newest_slot` (= a.slots[newest]) and writing a.out (pinned
+// host memory): the per-frame call's zero-copy form
+hipError_t launch_alt_frame_host(const AltArgs& a, const uint8_t* in, uint8_t* newest_slot, uint32_t newest,
+                                 hipStream_t s);
 
 struct CopyFramesArgs {
     const uint8_t* src[2];

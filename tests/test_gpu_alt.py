@@ -269,23 +269,29 @@ def test_run_host_feed_chunks(monkeypatch, chunk_frames):
     assert np.array_equal(got, want), np.argwhere(got != want)[:4]
 
 
-@pytest.mark.parametrize("n_tex,filt,colorize", [(2, 0, True), (3, 255, False), (1, 1, True)])
+@pytest.mark.parametrize("n_tex,filt,colorize", [(2, 0, True), (3, 255, False), (1, 1, True), (16, 0, False)])
 @pytest.mark.parametrize("piece", ["rows3", "odd"])
-def test_send_frame_striped_matches_oracle(monkeypatch, n_tex, filt, colorize, piece):
-    """send_frame with W = 1 goes through the striped upload / kernel /
-    readback; with stripes of a few rows (ragged last stripe) and snapshots
-    on some frames (read back by the frames after them), every output
-    equals the oracle's."""
+@pytest.mark.parametrize("form", ["direct", "direct-1stream", "dma"])
+def test_send_frame_striped_matches_oracle(monkeypatch, n_tex, filt, colorize, piece, form):
+    """send_frame with W = 1 goes through the striped path -- the zero-copy
+    form (the kernel reads the frame from pinned host memory, stores it into
+    its slot and writes the output to pinned host memory; stripes on two
+    streams or one) or the DMA form (upload / kernel / readback); with
+    stripes of a few rows (ragged last stripe), more frames than slots and
+    snapshots on some frames (read back by the frames after them), every
+    output equals the oracle's."""
     from dips_amd.alt import DiPsCompute
     w, h = 40, 27
     row = w * 4
     monkeypatch.setenv("DIPS_PIECE_BYTES", str({"rows3": 3 * row, "odd": 5 * row + 9}[piece]))
-    frames = _frames(w, h, 12, 60 + n_tex)
-    snaps = [False, True, False, False, True, False, False, False, False, True, False, False]
+    monkeypatch.setenv("DIPS_CALLBACK_DIRECT", "0" if form == "dma" else "1")
+    monkeypatch.setenv("DIPS_DIRECT_STREAMS", "1" if form == "direct-1stream" else "2")
+    frames = _frames(w, h, 20, 60 + n_tex)
+    snaps = [False, True, False, False, True, False, False, False, False, True, False, False] + [False] * 8
     c = DiPsCompute(n_tex, h, w, _props(colorize, 1, 5.0, filt, 0))
     ref = oracle.AltCompute(n_tex, w, h, colorize, 1, 5.0, filt, 0)
     try:
-        for t in range(12):
+        for t in range(20):
             got = c.send_frame(frames[t], True if snaps[t] else None)
             want = ref.send_frame(frames[t], snaps[t])
             assert np.array_equal(got, want), (t, np.argwhere(got != want)[:4])

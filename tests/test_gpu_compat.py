@@ -273,15 +273,20 @@ def test_frame_callback_batch_host_feed_chunks(monkeypatch, chunk_frames):
 
 @pytest.mark.parametrize("colorize,sens,filt,chroma", [(False, 5.0, 255, 0), (True, 5.0, 0, 0), (True, 0.7, 1, 2)])
 @pytest.mark.parametrize("piece", ["rows3", "odd", "whole"])
-def test_frame_callback_striped_matches_oracle(monkeypatch, colorize, sens, filt, chroma, piece):
-    """Steady-state frame_callback goes through the striped path (upload,
-    per-stripe kernel and readback overlapped); with stripes of a few rows, a
-    ragged last stripe or one stripe, every output and the ring state equal
-    the oracle's add_texture + dispatch."""
+@pytest.mark.parametrize("form", ["direct", "direct-1stream", "dma"])
+def test_frame_callback_striped_matches_oracle(monkeypatch, colorize, sens, filt, chroma, piece, form):
+    """Steady-state frame_callback goes through the striped path -- the
+    zero-copy form (the kernel reads and writes pinned host memory, stripes
+    on two streams or one) or the DMA form (upload, per-stripe kernel and
+    readback overlapped); with stripes of a few rows, a ragged last stripe or
+    one stripe, every output and the ring state equal the oracle's
+    add_texture + dispatch."""
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
     w, h = 40, 29
     row = w * 4
     monkeypatch.setenv("DIPS_PIECE_BYTES", str({"rows3": 3 * row, "odd": 7 * row + 5, "whole": 1 << 22}[piece]))
+    monkeypatch.setenv("DIPS_CALLBACK_DIRECT", "0" if form == "dma" else "1")
+    monkeypatch.setenv("DIPS_DIRECT_STREAMS", "1" if form == "direct-1stream" else "2")
     frames = _frames(w, h, 16, 90 + filt)
     cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter(chroma))
     ref = oracle.ComputeState(colorize, 1, sens, filt, chroma)

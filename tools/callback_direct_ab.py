@@ -80,10 +80,36 @@ def main():
                               "outputs_equal_plain": ok}), flush=True)
     for k in ("DIPS_CALLBACK_DIRECT", "DIPS_PIECE_BYTES", "DIPS_DIRECT_STREAMS"):
         os.environ.pop(k, None)
+    cs.close()
+    # dips_alt send_frame, one frame per call, both forms (default N = 2)
+    from dips_amd.alt import DiPsCompute
+    c = DiPsCompute(2, H, W)
+    ha = c._host
+    for t in range(F):
+        ha.check(ha._lib.dips_alt_send_frame(ha.ptr, host[t].ctypes.data, host[t].nbytes, 0, out.ctypes.data, out.nbytes))
+    last = {}
+    for rnd in range(rounds):
+        for name, direct in (("alt dma", "0"), ("alt direct", "1")) if rnd % 2 == 0 else (("alt direct", "1"), ("alt dma", "0")):
+            os.environ["DIPS_CALLBACK_DIRECT"] = direct
+            os.environ["DIPS_PIECE_BYTES"] = str(4 << 20)
+            t0 = time.perf_counter()
+            for t in range(8, F):
+                ha.check(ha._lib.dips_alt_send_frame(ha.ptr, host[t].ctypes.data, host[t].nbytes, 0,
+                                                     out.ctypes.data, out.nbytes))
+            dt = time.perf_counter() - t0
+            last.setdefault(name, out.copy())
+            res.setdefault(name + " 4 MiB", []).append((F - 8) / dt)
+            print(json.dumps({"variant": name + " 4 MiB", "round": rnd, "frames_per_s": round((F - 8) / dt, 1),
+                              "ms_per_frame": round(dt / (F - 8) * 1e3, 3),
+                              "pcie_GBps_each_way": round((F - 8) * W * H * 4 / dt / 1e9, 2),
+                              "outputs_equal_other_form": bool(len(last) < 2 or np.array_equal(*last.values()))}),
+                  flush=True)
+    c.close()
+    for k in ("DIPS_CALLBACK_DIRECT", "DIPS_PIECE_BYTES"):
+        os.environ.pop(k, None)
     for k, v in res.items():
         print(json.dumps({"variant": k, "summary": True, "median_frames_per_s": round(float(np.median(v)), 1)}),
               flush=True)
-    cs.close()
 
 
 if __name__ == "__main__":
