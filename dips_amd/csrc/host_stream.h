@@ -173,43 +173,77 @@ hipError_t run_striped_frame(const uint8_t* frame, uint8_t* out, uint32_t height
 
 // One frame through a per-pixel kernel that reads its input from, and writes
 // its output to, the pinned buffers themselves (zero-copy over PCIe, no DMA
-// engine): the pool stages stripe s into `pin_in` and at once launches
-// launch(y0, y1, stream) for it (stripes in any order -- rows are
-// independent), then copies stripe s of `pin_out` to `out` as soon as its
-// kernel has finished.  Even stripes go to compute[0], odd ones to
-// compute[1], so that one stripe's PCIe reads run beside the previous one's
-// writes.  Tasks 0..n-1 stage + launch, n..2n-1 copy out; a
-// copy-out task waits for its stripe's launch, so one worker or many run the
-// same schedule.  The caller makes sure no earlier kernel still reads
-// `pin_in` or writes `pin_out`.
+// engine).  The frame is cut into row stripes of ~piece_bytes() (the first
+// one a quarter of that) and each stripe into `split` byte pieces for the
+// copy pool: the pool stages the
+// pieces into `pin_in` in stripe order, the thread that stages a stripe's
+// last piece launches launch(y0, y1, stream) for it (stripes in any order --
+// rows are independent; even stripes on compute[0], odd ones on compute[1],
+// so one stripe's PCIe reads run beside the previous one's writes), and the
+// pieces of stripe s are copied from `pin_out` to `out` as soon as its
+// kernel has finished.  Small pieces let several threads stage the first
+// stripe and copy out the last one, the two exposed ends of the call.  The
+// copy-out tasks come after every staging task and wait for their stripe's
+// launch, so one worker or many run the same schedule.  The caller makes
+// sure no earlier kernel still reads `pin_in` or writes `pin_out`.
+inline uint32_t direct_split() {
+    if (const char* e = std::getenv("DIPS_DIRECT_SPLIT")) {
+        const long v = std::strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 64) return (uint32_t)v;
+    }
+    return 8u;
+}
+
+// Rows of the first stripe: a quarter stripe, so that the first kernel (whose
+// PCIe reads and writes do not overlap another kernel's) starts and lands
+// early; DIPS_DIRECT_FIRST=0 makes it a full stripe.
+inline uint32_t direct_first_rows(uint32_t rows) {
+    const char* e = std::getenv("DIPS_DIRECT_FIRST");
+    if (e && e[0] == '0') return rows;
+    return std::max(1u, rows / 4u);
+}
+
 template <typename Launch>
 hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t height, size_t row,
                                     uint8_t* pin_in, const uint8_t* pin_out, const hipStream_t (&compute)[2],
                                     int device, PieceEvents& ev, Launch&& launch) {
-    const size_t fb = row * height;
     const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
-    const uint32_t n_s = (height + rows - 1) / rows;
+    const uint32_t first = std::min(height, direct_first_rows(rows));
+    const uint32_t n_s = 1u + (height - first + rows - 1) / rows;
+    auto stripe_y0 = [&](uint32_t si) { return si == 0 ? 0u : std::min(height, first + (si - 1) * rows); };
+    const uint32_t k = direct_split();
+    const size_t n_t = (size_t)n_s * k;  // pieces per direction
     hipError_t e = ev.ensure(n_s);
     if (e != hipSuccess) return e;
     std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[n_s]);
-    for (uint32_t i = 0; i < n_s; ++i) ready[i].store(0, std::memory_order_relaxed);
+    std::unique_ptr<std::atomic<uint32_t>[]> staged(new std::atomic<uint32_t>[n_s]);
+    for (uint32_t i = 0; i < n_s; ++i) {
+        ready[i].store(0, std::memory_order_relaxed);
+        staged[i].store(0, std::memory_order_relaxed);
+    }
     std::mutex launch_mu;
     std::atomic<int> err{(int)hipSuccess};
     static const bool trace = std::getenv("DIPS_STRIPE_TRACE") != nullptr;
     using clk = std::chrono::steady_clock;
     const auto tbeg = clk::now();
-    std::vector<double> ts(trace ? 4 * n_s : 0);
+    std::vector<double> ts(trace ? 2 * n_s + n_t : 0);
     auto since = [&]() { return std::chrono::duration<double, std::micro>(clk::now() - tbeg).count(); };
-    CopyPool::global().run(2 * (size_t)n_s, [&](size_t i) {
-        const size_t si = i < n_s ? i : i - n_s;
-        const uint32_t y0 = (uint32_t)si * rows, y1 = std::min(height, y0 + rows);
-        const size_t o = (size_t)y0 * row, len = (size_t)(y1 - y0) * row;
-        if (i < n_s) {
-            host_copy(pin_in + o, frame + o, len);
-            if (trace) ts[4 * si] = since();
+    CopyPool::global().run(2 * n_t, [&](size_t i) {
+        const size_t pi = i < n_t ? i : i - n_t;
+        const uint32_t si = (uint32_t)(pi / k), j = (uint32_t)(pi % k);
+        const uint32_t y0 = stripe_y0(si), y1 = si + 1 == n_s ? height : stripe_y0(si + 1);
+        const size_t so = (size_t)y0 * row, slen = (size_t)(y1 - y0) * row;
+        // piece j of the stripe: 64-B aligned cut points
+        const size_t p0 = std::min(slen, (slen * j / k) & ~(size_t)63);
+        const size_t p1 = j + 1 == k ? slen : std::min(slen, (slen * (j + 1) / k) & ~(size_t)63);
+        const size_t o = so + p0, len = p1 - p0;
+        if (i < n_t) {
+            if (len) host_copy(pin_in + o, frame + o, len);
+            if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != k) return;
+            // the stripe's last piece: its kernel and event back to back on the stream
+            if (trace) ts[2 * si] = since();
             hipError_t r;
             {
-                // the kernel and its event back to back on the stream
                 std::lock_guard<std::mutex> lk(launch_mu);
                 hipStream_t cs = compute[si & 1u];
                 r = hipSetDevice(device);
@@ -217,7 +251,7 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
                 if (r == hipSuccess) r = hipEventRecord(ev.ev[si], cs);
             }
             if (r != hipSuccess) err.store((int)r);
-            if (trace) ts[4 * si + 1] = since();
+            if (trace) ts[2 * si + 1] = since();
             ready[si].store(r == hipSuccess ? 1 : -1, std::memory_order_release);
             return;
         }
@@ -229,17 +263,18 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
             err.store((int)r);
             return;
         }
-        if (trace) ts[4 * si + 2] = since();
-        host_copy(out + o, pin_out + o, len);
-        if (trace) ts[4 * si + 3] = since();
+        if (len) host_copy(out + o, pin_out + o, len);
+        if (trace) ts[2 * n_s + pi] = since();
     });
     if (trace) {
-        std::fprintf(stderr, "direct stripes %u:", n_s);
-        for (uint32_t si = 0; si < n_s; ++si)
-            std::fprintf(stderr, " [%.0f %.0f %.0f %.0f]", ts[4 * si], ts[4 * si + 1], ts[4 * si + 2], ts[4 * si + 3]);
+        std::fprintf(stderr, "direct stripes %u x %u pieces: [staged launched copied-out]", n_s, k);
+        for (uint32_t si = 0; si < n_s; ++si) {
+            double done = 0.0;
+            for (uint32_t j = 0; j < k; ++j) done = std::max(done, ts[2 * n_s + (size_t)si * k + j]);
+            std::fprintf(stderr, " [%.0f %.0f %.0f]", ts[2 * si], ts[2 * si + 1], done);
+        }
         std::fprintf(stderr, " end %.0f\n", since());
     }
-    (void)fb;
     return (hipError_t)err.load();
 }
 

@@ -286,6 +286,7 @@ def test_send_frame_striped_matches_oracle(monkeypatch, n_tex, filt, colorize, p
     monkeypatch.setenv("DIPS_PIECE_BYTES", str({"rows3": 3 * row, "odd": 5 * row + 9}[piece]))
     monkeypatch.setenv("DIPS_CALLBACK_DIRECT", "0" if form == "dma" else "1")
     monkeypatch.setenv("DIPS_DIRECT_STREAMS", "1" if form == "direct-1stream" else "2")
+    monkeypatch.setenv("DIPS_DIRECT_SPLIT", "3" if form == "direct-1stream" else "4")  # copy-pool pieces per stripe
     frames = _frames(w, h, 20, 60 + n_tex)
     snaps = [False, True, False, False, True, False, False, False, False, True, False, False] + [False] * 8
     c = DiPsCompute(n_tex, h, w, _props(colorize, 1, 5.0, filt, 0))

@@ -287,6 +287,7 @@ def test_frame_callback_striped_matches_oracle(monkeypatch, colorize, sens, filt
     monkeypatch.setenv("DIPS_PIECE_BYTES", str({"rows3": 3 * row, "odd": 7 * row + 5, "whole": 1 << 22}[piece]))
     monkeypatch.setenv("DIPS_CALLBACK_DIRECT", "0" if form == "dma" else "1")
     monkeypatch.setenv("DIPS_DIRECT_STREAMS", "1" if form == "direct-1stream" else "2")
+    monkeypatch.setenv("DIPS_DIRECT_SPLIT", "3" if form == "direct-1stream" else "4")  # copy-pool pieces per stripe
     frames = _frames(w, h, 16, 90 + filt)
     cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter(chroma))
     ref = oracle.ComputeState(colorize, 1, sens, filt, chroma)

@@ -50,35 +50,40 @@ def main():
     lib, hd = cs._hd._lib, cs._hd
     for t in range(F):  # the same stream prefix as the reference pass: every timed pass follows frames F-3..F-1
         hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes, out.ctypes.data, out.nbytes))
-    # (name, DIPS_CALLBACK_DIRECT, stripe bytes, extra env): the direct form's
-    # default puts odd stripes on a second stream; DIPS_DIRECT_STREAMS=1 puts
-    # every stripe on the compute stream
-    variants = [("dma", "0", 4 << 20, {}), ("direct", "1", 2 << 20, {}), ("direct", "1", 4 << 20, {}),
-                ("direct 1-stream", "1", 2 << 20, {"DIPS_DIRECT_STREAMS": "1"}),
-                ("direct 1-stream", "1", 4 << 20, {"DIPS_DIRECT_STREAMS": "1"})]
+    # (name, DIPS_CALLBACK_DIRECT, stripe bytes, extra env): the direct form
+    # puts odd stripes on a second stream (DIPS_DIRECT_STREAMS=1: all on one)
+    # and cuts each stripe into DIPS_DIRECT_SPLIT copy-pool pieces
+    variants = [("dma", "0", 4 << 20, {}),
+                ("direct split1 full-first", "1", 4 << 20, {"DIPS_DIRECT_SPLIT": "1", "DIPS_DIRECT_FIRST": "0"}),
+                ("direct split8 full-first", "1", 4 << 20, {"DIPS_DIRECT_SPLIT": "8", "DIPS_DIRECT_FIRST": "0"}),
+                ("direct split8", "1", 4 << 20, {"DIPS_DIRECT_SPLIT": "8"}),
+                ("direct split16", "1", 4 << 20, {"DIPS_DIRECT_SPLIT": "16"}),
+                ("direct split8", "1", 8 << 20, {"DIPS_DIRECT_SPLIT": "8"})]
     res = {}
     for rnd in range(rounds):
         for name, direct, piece, extra in (variants if rnd % 2 == 0 else variants[::-1]):
             os.environ["DIPS_CALLBACK_DIRECT"] = direct
             os.environ["DIPS_PIECE_BYTES"] = str(piece)
-            for k in ("DIPS_DIRECT_STREAMS",):
+            for k in ("DIPS_DIRECT_STREAMS", "DIPS_DIRECT_SPLIT", "DIPS_DIRECT_FIRST"):
                 os.environ.pop(k, None)
             os.environ.update(extra)
             ok = True
-            t0 = time.perf_counter()
+            dt = 0.0
             for t in range(8, F):
+                t0 = time.perf_counter()
                 hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
                                                  out.ctypes.data, out.nbytes))
-                if t in (8, F // 2, F - 1):  # spot checks inside the timed loop (cheap: 3 frames)
+                dt += time.perf_counter() - t0
+                if t in (8, F // 2, F - 1):  # spot checks (outside the timed calls)
                     ok = ok and bool(np.array_equal(out, want[t]))
-            dt = time.perf_counter() - t0
             key = f"{name} {piece >> 20} MiB"
             res.setdefault(key, []).append((F - 8) / dt)
             print(json.dumps({"variant": key, "round": rnd, "frames_per_s": round((F - 8) / dt, 1),
                               "ms_per_frame": round(dt / (F - 8) * 1e3, 3),
                               "pcie_GBps_each_way": round((F - 8) * W * H * 4 / dt / 1e9, 2),
                               "outputs_equal_plain": ok}), flush=True)
-    for k in ("DIPS_CALLBACK_DIRECT", "DIPS_PIECE_BYTES", "DIPS_DIRECT_STREAMS"):
+    for k in ("DIPS_CALLBACK_DIRECT", "DIPS_PIECE_BYTES", "DIPS_DIRECT_STREAMS", "DIPS_DIRECT_SPLIT",
+              "DIPS_DIRECT_FIRST"):
         os.environ.pop(k, None)
     cs.close()
     # dips_alt send_frame, one frame per call, both forms (default N = 2)

@@ -33,7 +33,7 @@ def main():
     lib, hd = cs._hd._lib, cs._hd
     for t in range(8):
         hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes, out.ctypes.data, out.nbytes))
-    for direct, piece in (("0", 4 << 20), ("1", 2 << 20), ("1", 4 << 20)):
+    for direct, piece in (("0", 4 << 20), ("1", 4 << 20)):
         os.environ["DIPS_CALLBACK_DIRECT"] = direct
         os.environ["DIPS_PIECE_BYTES"] = str(piece)
         print(f"== direct {direct} piece {piece >> 20} MiB", file=sys.stderr, flush=True)
