@@ -135,10 +135,15 @@ __global__ __launch_bounds__(256) void compat_precompute_kernel(CompatArgs a) {
 
 // compute_main's per-pixel tail once the newest slot's filtered intensity fi
 // is known (dips_shader.wgsl:187-239).
-__device__ __forceinline__ uint32_t compat_texel(const CompatArgs& a, uint64_t p, float fi) {
+// raw_slot: the newest slot receives the frame's raw texel instead of the
+// quantised one (the speculative dispatch of a deferred add_texture; the
+// dispatch that claims it quantises the slot, compat_gray_kernel in place).
+__device__ __forceinline__ uint32_t compat_texel(const CompatArgs& a, uint64_t p, float fi, bool raw_slot = false,
+                                                 uint32_t raw = 0u) {
     // in-place store of the filtered newest slot, quantised (dips_shader.wgsl:187)
     const uint32_t qi = unorm_store(fi);
-    *reinterpret_cast<uint32_t*>(a.slots[a.newest] + 4 * p) = qi | (qi << 8) | (qi << 16) | (255u << 24);
+    *reinterpret_cast<uint32_t*>(a.slots[a.newest] + 4 * p) =
+        raw_slot ? raw : (qi | (qi << 8) | (qi << 16) | (255u << 24));
     float m[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -173,6 +178,7 @@ __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
 // contiguous bytes each way.  (Four pixels per thread through 16-B
 // system-coherent buffer loads / stores measured slower: 557-575 against
 // 695-701 frames/s of 4K per-frame calls, tools/callback_direct_ab.py.)
+template <bool RAW_SLOT>
 __global__ __launch_bounds__(256) void compat_main_host_kernel(CompatArgs a) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     const uint64_t p = (uint64_t)a.y0 * a.width + (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -180,8 +186,8 @@ __global__ __launch_bounds__(256) void compat_main_host_kernel(CompatArgs a) {
     const uint32_t v = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a.raw + 4 * p), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_SYSTEM);
     const float fi = intensity_rgb(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, a.chroma);
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 4 * p), compat_texel(a, p, fi), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 4 * p), compat_texel(a, p, fi, RAW_SLOT, v),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // A ring slot as frame_callback leaves it for a W = 1 frame: the gray texel
@@ -193,6 +199,22 @@ __global__ __launch_bounds__(256) void compat_gray_kernel(const uint8_t* __restr
     if (p >= n_px) return;
     const uint32_t q = unorm_store(texel_intensity(src, p, chroma));
     *reinterpret_cast<uint32_t*>(dst + 4 * p) = q | (q << 8) | (q << 16) | (255u << 24);
+}
+
+// The same in place: a ring slot holding a raw frame becomes the gray texel
+// compute_main stores (the dispatch that claims a speculative one).
+__global__ __launch_bounds__(256) void compat_quantise_slot_kernel(uint8_t* slot, uint64_t n_px, uint32_t chroma) {
+    const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (p >= n_px) return;
+    const uint32_t q = unorm_store(texel_intensity(slot, p, chroma));
+    *reinterpret_cast<uint32_t*>(slot + 4 * p) = q | (q << 8) | (q << 16) | (255u << 24);
+}
+
+hipError_t launch_compat_quantise_slot(uint8_t* slot, uint64_t n_px, uint32_t chroma, hipStream_t s) {
+    if (n_px == 0) return hipSuccess;
+    hipLaunchKernelGGL(compat_quantise_slot_kernel, dim3((uint32_t)((n_px + 255) / 256)), dim3(256), 0, s, slot, n_px,
+                       chroma);
+    return hipGetLastError();
 }
 
 hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, uint32_t chroma, hipStream_t s) {
@@ -286,11 +308,34 @@ hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s) {
+// A frame staged in pinned host memory into a ring slot (the deferred
+// add_texture's upload when no dispatch consumed it): system-scope loads, one
+// dword per thread.
+__global__ __launch_bounds__(256) void copy_from_host_kernel(const uint32_t* src, uint32_t* __restrict__ dst,
+                                                            uint64_t n_words) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= n_words) return;
+    dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_copy_from_host(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s) {
+    if (bytes % 4u != 0) return hipErrorInvalidValue;
+    const uint64_t n = bytes / 4u;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(copy_from_host_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
+                       reinterpret_cast<const uint32_t*>(src), reinterpret_cast<uint32_t*>(dst), n);
+    return hipGetLastError();
+}
+
+hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, bool raw_slot) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
     const uint64_t n_px = (uint64_t)(yend - a.y0) * a.width;
-    hipLaunchKernelGGL(compat_main_host_kernel, dim3((uint32_t)((n_px + 255) / 256)), dim3(256), 0, s, a);
+    const dim3 grid((uint32_t)((n_px + 255) / 256));
+    if (raw_slot)
+        hipLaunchKernelGGL(compat_main_host_kernel<true>, grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(compat_main_host_kernel<false>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -81,6 +81,20 @@ struct dips_handle {
     dips_host::PieceEvents pieces;  // per-piece completion of the per-frame readback
     dips_host::PieceEvents up_pieces;  // per-stripe upload completion (striped frame_callback)
     HostPinned io_out;                 // readback staging of the striped frame_callback
+    // deferred add_texture (steady state, W = 1, host frame): add_texture
+    // stages the frame into `io` and launches, stripe by stripe, the
+    // compute_main of the dispatch that normally follows (zero-copy, output
+    // into `io_out`, the raw frame into its slot); that dispatch only collects
+    // the stripes and quantises the slot; any other call first lets the
+    // speculative kernels finish (flush_pending) and leaves the slot raw, as
+    // an add_texture without a dispatch does in the reference
+    bool pending = false;
+    uint32_t pending_slot = 0;
+    dips_host::DirectGeom pend_geom;  // stripes of the speculative dispatch
+    // slots holding a raw frame (added, not yet quantised by a dispatch): the
+    // reference reads their unquantised intensity, which the
+    // batch kernel's gray-texel ring cannot express
+    bool slot_raw[4] = {false, false, false, false};
     int cb_occupancy = 0;
     DevBuf gray_lut;          // T_d / T_c tables of series_gray_lut_kernel (128 KiB) for gray_lut_tau
     bool gray_lut_valid = false;
@@ -98,6 +112,8 @@ dips_status fail(dips_handle* h, dips_status st, const std::string& msg) {
     if (h) h->err = msg;
     return st;
 }
+
+dips_status flush_pending(dips_handle* h);  // below, with add_texture
 
 dips_status hip_fail(dips_handle* h, hipError_t e, const char* what) {
     std::string m = std::string(what) + ": " + hipGetErrorString(e);
@@ -466,6 +482,8 @@ dips_status dips_set_stream(dips_handle* h, void* stream) {
     // work issued on the new stream waits for all work issued on the old one
     dips_status st = bind(h);
     if (st != DIPS_OK) return st;
+    st = flush_pending(h);  // on the old stream, ordered before the switch
+    if (st != DIPS_OK) return st;
     if (!h->switch_ev) DIPS_HIP(h, hipEventCreateWithFlags(&h->switch_ev, hipEventDisableTiming));
     DIPS_HIP(h, hipEventRecord(h->switch_ev, h->stream));
     DIPS_HIP(h, hipStreamWaitEvent(next, h->switch_ev, 0));
@@ -475,6 +493,8 @@ dips_status dips_set_stream(dips_handle* h, void* stream) {
 
 dips_status dips_synchronize(dips_handle* h) {
     dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    st = flush_pending(h);  // a deferred frame into its slot first
     if (st != DIPS_OK) return st;
     DIPS_HIP(h, hipStreamSynchronize(h->stream));
     return DIPS_OK;
@@ -488,8 +508,30 @@ dips_status dips_synchronize(dips_handle* h) {
 
 namespace {
 
+// A deferred frame (see dips_handle::pending) abandoned by its dispatch: the
+// speculative kernels have stored the raw frame into its slot (what the
+// reference's add_texture leaves there); the odd stripes ran on copy_stream,
+// so wait for them -- later work on the stream is ordered after the even
+// ones.  Every entry point except dispatch calls this first.
+dips_status flush_pending(dips_handle* h) {
+    if (!h->pending) return DIPS_OK;
+    h->pending = false;
+    DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
+    return DIPS_OK;
+}
+
+// Deferral of host frames in steady state (DIPS_DEFER_UPLOAD=0 turns it off).
+bool defer_upload(const dips_handle* h) {
+    if (!h->main_init || h->p.spatial_window_size != 1 || (h->p.flags & DIPS_FLAG_DEVICE_PTRS)) return false;
+    const char* e = std::getenv("DIPS_DEFER_UPLOAD");
+    return !(e && e[0] == '0');
+}
+
 // ComputeState::add_texture (dips/src/gpu/mod.rs:170-216) from a host frame
-// (through the pinned staging buffer) or a device frame (D2D).
+// (through the pinned staging buffer) or a device frame (D2D).  In steady
+// state with W = 1 a host frame is only staged into the pinned buffer and the
+// next dispatch reads it from there (zero-copy, both PCIe directions at once,
+// as in frame_callback_striped); the ring bookkeeping is the same.
 dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frame, size_t len,
                              bool device_src) {
     if (!frame || width == 0 || height == 0) return fail(h, DIPS_ERR_INVALID, "add_texture: empty frame");
@@ -497,6 +539,48 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
     if (len != fb) return fail(h, DIPS_ERR_INVALID, "add_texture: len != width*height*4 (RGBA8, stride width*4)");
     if (h->n_queued > 0 && (width != h->width || height != h->height))
         return fail(h, DIPS_ERR_INVALID, "add_texture: frame size changed after the first frame");
+    dips_status fst = flush_pending(h);
+    if (fst != DIPS_OK) return fst;
+    if (!device_src && defer_upload(h)) {
+        DIPS_HIP(h, h->io_out.ensure(fb));
+        // io / io_out are free once both streams have drained
+        DIPS_HIP(h, hipStreamSynchronize(h->stream));
+        DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
+        // update_temporal_texture (bind_groups.rs:407-427)
+        const uint32_t slot = h->ring_idx;
+        h->slot_raw[slot] = true;
+        h->uniform_idx = slot;
+        h->ring_idx = (slot + 1u) % 4u;
+        h->added += 1;
+        // the speculative compute_main, stripe by stripe as the pool stages them
+        void *din = nullptr, *dout = nullptr;
+        DIPS_HIP(h, hipHostGetDevicePointer(&din, h->io.p, 0));
+        DIPS_HIP(h, hipHostGetDevicePointer(&dout, h->io_out.p, 0));
+        dips::CompatArgs a{};
+        for (int k = 0; k < 4; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
+        a.start = h->start.as<uint8_t>();
+        a.raw = static_cast<const uint8_t*>(din);
+        a.out = static_cast<uint8_t*>(dout);
+        a.width = width;
+        a.height = height;
+        a.newest = slot;
+        a.window = 1;
+        a.chroma = h->p.chroma_filter;
+        a.filter = h->p.filter_type;
+        a.sensitivity = h->p.sensitivity;
+        a.colorize = h->p.colorize ? 1u : 0u;
+        h->pend_geom.init(height, (size_t)width * 4u);
+        const hipStream_t cs[2] = {h->stream, h->copy_stream};
+        DIPS_HIP(h, dips_host::direct_stage_launch(frame, h->io.bytes(), cs, h->device, h->pieces, h->pend_geom,
+                                                   [&](uint32_t y0, uint32_t y1, hipStream_t st) {
+                                                       a.y0 = y0;
+                                                       a.y1 = y1;
+                                                       return dips::launch_compat_main_host(a, st, true);
+                                                   }));
+        h->pending = true;
+        h->pending_slot = slot;
+        return DIPS_OK;
+    }
     if (h->n_queued == 0) {
         for (auto& s : h->slots) DIPS_HIP(h, s.ensure(fb));
         DIPS_HIP(h, h->raw.ensure(fb));
@@ -516,6 +600,7 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
     if (!h->main_init) {
         // VecDeque phase (dips/src/gpu/mod.rs:171-177): frames 0..3 fill slots 0..3
         DIPS_HIP(h, put(h->slots[h->n_queued].p));
+        h->slot_raw[h->n_queued] = true;
         h->n_queued += 1;
         if (h->n_queued == 4) {
             // PreComputeBindGroups::initialize + run_precompute_pipeline (:178-188)
@@ -535,6 +620,7 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
     } else {
         // update_temporal_texture (bind_groups.rs:407-427)
         DIPS_HIP(h, put(h->slots[h->ring_idx].p));
+        h->slot_raw[h->ring_idx] = true;
         h->uniform_idx = h->ring_idx;
         h->ring_idx = (h->ring_idx + 1u) % 4u;
     }
@@ -550,6 +636,19 @@ int dispatch_impl(dips_handle* h, uint8_t* out, size_t cap, bool device_dst) {
     const size_t fb = (size_t)h->width * h->height * 4u;
     if (!out) return fail(h, DIPS_ERR_INVALID, "dispatch: null output");
     if (cap < fb) return fail(h, DIPS_ERR_CAPACITY, "dispatch: output buffer smaller than width*height*4");
+    if (h->pending && !device_dst) {
+        // the speculative compute_main of the deferred add_texture: collect
+        // its stripes, then store the quantised texel into the newest slot
+        // (every stripe's kernel has finished once collected)
+        h->pending = false;
+        DIPS_HIP(h, dips_host::direct_collect(out, h->io_out.bytes(), h->pieces, h->pend_geom));
+        DIPS_HIP(h, dips::launch_compat_quantise_slot(h->slots[h->pending_slot].as<uint8_t>(),
+                                                      (uint64_t)h->width * h->height, h->p.chroma_filter, h->stream));
+        h->slot_raw[h->pending_slot] = false;
+        return 1;
+    }
+    dips_status fst = flush_pending(h);
+    if (fst != DIPS_OK) return fst;
     dips::CompatArgs a{};
     for (int k = 0; k < 4; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
     a.start = h->start.as<uint8_t>();
@@ -572,6 +671,7 @@ int dispatch_impl(dips_handle* h, uint8_t* out, size_t cap, bool device_dst) {
         a.raw = h->raw.as<uint8_t>();
     }
     DIPS_HIP(h, dips::launch_compat_main(a, h->stream));
+    h->slot_raw[a.newest] = false;  // compute_main stored the quantised texel
     if (device_dst) return 1;
     // readback (copy_texture_to_buffer + map, gpu/mod.rs:342-393) in pieces,
     // each copied out as soon as its DMA lands
@@ -590,7 +690,13 @@ dips_status frame_callback_device(dips_handle* h, uint32_t width, uint32_t heigh
                                   uint8_t* out) {
     const size_t fb = (size_t)width * height * 4u;
     uint32_t t = 0;
-    for (; t < n && h->added < 7; ++t) {
+    // one by one while the batch kernel cannot take the state: the stream's
+    // first frames, or a raw frame among the three slots it reads as the ring
+    auto ring_raw = [&]() {
+        return h->slot_raw[(h->ring_idx + 1u) % 4u] || h->slot_raw[(h->ring_idx + 2u) % 4u] ||
+               h->slot_raw[(h->ring_idx + 3u) % 4u];
+    };
+    for (; t < n && (h->added < 7 || ring_raw()); ++t) {
         dips_status st = add_texture_impl(h, width, height, frames + (size_t)t * fb, fb, true);
         if (st != DIPS_OK) return st;
         const int r = dispatch_impl(h, out + (size_t)t * fb, fb, true);
@@ -617,7 +723,12 @@ dips_status frame_callback_device(dips_handle* h, uint32_t width, uint32_t heigh
         return DIPS_OK;
     }
     const int32_t window = h->p.spatial_window_size;
-    if (window == 1) return batch_steady(h, bf, bo, m, nullptr);
+    if (window == 1) {
+        const dips_status st = batch_steady(h, bf, bo, m, nullptr);
+        if (st == DIPS_OK)
+            for (auto& r : h->slot_raw) r = false;  // the batch leaves gray ring texels
+        return st;
+    }
     // filtered ring texels of up to g frames at a time (~1 GiB of scratch)
     uint64_t g = std::max<uint64_t>(16u, (1ull << 30) / fb);
     if (const char* e = std::getenv("DIPS_WINDOW_BATCH_FRAMES")) g = std::max(1ul, std::strtoul(e, nullptr, 10));
@@ -628,6 +739,7 @@ dips_status frame_callback_device(dips_handle* h, uint32_t width, uint32_t heigh
         dips_status st = batch_steady(h, h->filtered.as<uint8_t>(), bo + (size_t)s0 * fb, gn, bf + (size_t)s0 * fb);
         if (st != DIPS_OK) return st;
     }
+    for (auto& r : h->slot_raw) r = false;  // the batch leaves gray ring texels
     return DIPS_OK;
 }
 
@@ -750,6 +862,8 @@ dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_
 // stripe s comes back while stripes s+1.. still go up (both PCIe directions
 // at once).  Same outputs and ring state as add_texture + dispatch.
 int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
+    dips_status st = flush_pending(h);  // a deferred frame into its slot first
+    if (st != DIPS_OK) return st;
     const uint32_t W = h->width, H = h->height;
     const size_t row = (size_t)W * 4u, fb = row * H;
     DIPS_HIP(h, h->io_out.ensure(fb));
@@ -761,6 +875,7 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
     DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
     // update_temporal_texture (bind_groups.rs:407-427)
     uint8_t* slot = h->slots[h->ring_idx].as<uint8_t>();
+    h->slot_raw[h->ring_idx] = false;  // compute_main stores the quantised texel
     h->uniform_idx = h->ring_idx;
     h->ring_idx = (h->ring_idx + 1u) % 4u;
     h->added += 1;
@@ -852,6 +967,7 @@ dips_status dips_compat_resume(dips_handle* h, uint32_t width, uint32_t height, 
     if (!start_rgba || !halo || width == 0 || height == 0)
         return fail(h, DIPS_ERR_INVALID, "compat_resume: null or empty argument");
     if (t0 < 7) return fail(h, DIPS_ERR_INVALID, "compat_resume: t0 must be >= 7 (steady state of the ring)");
+    h->pending = false;  // a deferred frame's slot is rewritten below like every other
     const size_t fb = (size_t)width * height * 4u;
     const bool dev = (h->p.flags & DIPS_FLAG_DEVICE_PTRS) != 0;
     for (auto& sl : h->slots) DIPS_HIP(h, sl.ensure(fb));
@@ -883,6 +999,7 @@ dips_status dips_compat_resume(dips_handle* h, uint32_t width, uint32_t height, 
     h->height = height;
     h->n_queued = 4;
     h->main_init = true;
+    for (auto& r : h->slot_raw) r = false;  // gray texels, as the ring of a continuous run
     h->ring_idx = (uint32_t)(t0 % 4u);
     h->uniform_idx = (uint32_t)((t0 - 1) % 4u);
     h->added = t0;
@@ -892,6 +1009,8 @@ dips_status dips_compat_resume(dips_handle* h, uint32_t width, uint32_t height, 
 dips_status dips_frame_callback_batch(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
                                       uint32_t n_frames, uint8_t* out) {
     dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    st = flush_pending(h);  // a deferred frame into its slot first
     if (st != DIPS_OK) return st;
     if (n_frames == 0) return DIPS_OK;
     if (!frames || !out || width == 0 || height == 0)
@@ -914,6 +1033,8 @@ dips_status dips_frame_callback_batch(dips_handle* h, uint32_t width, uint32_t h
 
 int dips_start_texture(dips_handle* h, uint8_t* out, size_t cap) {
     dips_status st = bind(h);
+    if (st != DIPS_OK) return st;
+    st = flush_pending(h);  // a deferred frame into its slot first
     if (st != DIPS_OK) return st;
     if (!h->main_init) return 0;
     const size_t fb = (size_t)h->width * h->height * 4u;

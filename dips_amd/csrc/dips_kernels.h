@@ -237,7 +237,13 @@ hipError_t launch_read_walk(const SeriesArgs& a, int vec_bytes, uint32_t blocks,
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s);
 // compat_main with raw / out in pinned host memory (zero-copy per-frame call)
-hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s);
+// raw_slot: store the raw frame texel into the newest slot instead of its
+// quantised gray texel (the speculative dispatch of a deferred add_texture)
+hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, bool raw_slot = false);
+// a raw ring slot into its gray texel q(get_intensity) in place
+hipError_t launch_compat_quantise_slot(uint8_t* slot, uint64_t n_px, uint32_t chroma, hipStream_t s);
+// bytes (a multiple of 4) from pinned host memory (device-visible pointer) into HBM
+hipError_t launch_copy_from_host(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s);
 hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, uint32_t chroma, hipStream_t s);
 // W > 1 steady state: the ring texel compute_main stores for each of n frames
 // (gray q(spatial_median_filter(frame)), dips_shader.wgsl:120-170, 187), so

@@ -238,7 +238,7 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
         const size_t p1 = j + 1 == k ? slen : std::min(slen, (slen * (j + 1) / k) & ~(size_t)63);
         const size_t o = so + p0, len = p1 - p0;
         if (i < n_t) {
-            if (len) host_copy(pin_in + o, frame + o, len);
+            if (len && frame) host_copy(pin_in + o, frame + o, len);  // frame == nullptr: already staged
             if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != k) return;
             // the stripe's last piece: its kernel and event back to back on the stream
             if (trace) ts[2 * si] = since();
@@ -275,6 +275,80 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
         }
         std::fprintf(stderr, " end %.0f\n", since());
     }
+    return (hipError_t)err.load();
+}
+
+// Stripe / piece geometry of the zero-copy frame pipeline (as in
+// run_striped_frame_direct), fixed at staging time so that a later collect
+// uses the same cut.
+struct DirectGeom {
+    uint32_t height = 0, rows = 1, first = 1, n_s = 0, k = 1;
+    size_t row = 0;
+    void init(uint32_t h, size_t row_bytes) {
+        height = h;
+        row = row_bytes;
+        rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
+        first = std::min(height, direct_first_rows(rows));
+        n_s = 1u + (height - first + rows - 1) / rows;
+        k = direct_split();
+    }
+    uint32_t y0(uint32_t si) const { return si == 0 ? 0u : std::min(height, first + (si - 1) * rows); }
+    uint32_t y1(uint32_t si) const { return si + 1 == n_s ? height : y0(si + 1); }
+    // byte range [o, o + len) of piece j of stripe si (64-B aligned cuts)
+    void piece(uint32_t si, uint32_t j, size_t& o, size_t& len) const {
+        const size_t so = (size_t)y0(si) * row, slen = (size_t)(y1(si) - y0(si)) * row;
+        const size_t p0 = std::min(slen, (slen * j / k) & ~(size_t)63);
+        const size_t p1 = j + 1 == k ? slen : std::min(slen, (slen * (j + 1) / k) & ~(size_t)63);
+        o = so + p0;
+        len = p1 - p0;
+    }
+};
+
+// First half of the zero-copy pipeline: the pool stages the frame's pieces
+// into `pin_in` and the thread that stages a stripe's last piece launches
+// launch(y0, y1, stream) for it and records the stripe's event (stripes
+// alternating over compute[0] / compute[1]).  Returns when every stripe is
+// staged and launched; the kernels may still run (and read `pin_in`).
+template <typename Launch>
+hipError_t direct_stage_launch(const uint8_t* frame, uint8_t* pin_in, const hipStream_t (&compute)[2], int device,
+                               PieceEvents& ev, const DirectGeom& g, Launch&& launch) {
+    hipError_t e = ev.ensure(g.n_s);
+    if (e != hipSuccess) return e;
+    std::unique_ptr<std::atomic<uint32_t>[]> staged(new std::atomic<uint32_t>[g.n_s]);
+    for (uint32_t i = 0; i < g.n_s; ++i) staged[i].store(0, std::memory_order_relaxed);
+    std::mutex launch_mu;
+    std::atomic<int> err{(int)hipSuccess};
+    CopyPool::global().run((size_t)g.n_s * g.k, [&](size_t i) {
+        const uint32_t si = (uint32_t)(i / g.k), j = (uint32_t)(i % g.k);
+        size_t o, len;
+        g.piece(si, j, o, len);
+        if (len) host_copy(pin_in + o, frame + o, len);
+        if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != g.k) return;
+        std::lock_guard<std::mutex> lk(launch_mu);
+        hipStream_t cs = compute[si & 1u];
+        hipError_t r = hipSetDevice(device);
+        if (r == hipSuccess) r = launch(g.y0(si), g.y1(si), cs);
+        if (r == hipSuccess) r = hipEventRecord(ev.ev[si], cs);
+        if (r != hipSuccess) err.store((int)r);
+    });
+    return (hipError_t)err.load();
+}
+
+// Second half: the pool copies each stripe's pieces from `pin_out` to `out`
+// as soon as the stripe's event (recorded by direct_stage_launch) has fired.
+inline hipError_t direct_collect(uint8_t* out, const uint8_t* pin_out, PieceEvents& ev, const DirectGeom& g) {
+    std::atomic<int> err{(int)hipSuccess};
+    CopyPool::global().run((size_t)g.n_s * g.k, [&](size_t i) {
+        const uint32_t si = (uint32_t)(i / g.k), j = (uint32_t)(i % g.k);
+        const hipError_t r = hipEventSynchronize(ev.ev[si]);
+        if (r != hipSuccess) {
+            err.store((int)r);
+            return;
+        }
+        size_t o, len;
+        g.piece(si, j, o, len);
+        if (len) host_copy(out + o, pin_out + o, len);
+    });
     return (hipError_t)err.load();
 }
 

@@ -459,3 +459,73 @@ def test_batch_epilogue_table_equals_arithmetic_and_oracle(colorize, filt, sens,
             cs.close()
     assert np.array_equal(outs["1"], outs["0"]), np.argwhere(outs["1"] != outs["0"])[:4]
     assert np.array_equal(outs["1"], want), np.argwhere(outs["1"] != want)[:4]
+
+
+@pytest.mark.parametrize("defer", ["1", "0"])
+@pytest.mark.parametrize("colorize,sens,filt,chroma", [(False, 5.0, 255, 0), (True, 0.7, 0, 3)])
+def test_deferred_add_texture_sequences_match_oracle(monkeypatch, defer, colorize, sens, filt, chroma):
+    """add_texture in steady state (W = 1, host frame) only stages the frame;
+    the next dispatch reads it from pinned memory (zero-copy), and every other
+    call first copies it into its slot.  Mixed call sequences -- add + dispatch,
+    two adds without a dispatch, dispatch twice, add then start_texture, add
+    then a striped frame_callback, add then a host batch -- give the oracle's
+    outputs and ring state, with the deferral on and off."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
+    monkeypatch.setenv("DIPS_DEFER_UPLOAD", defer)
+    monkeypatch.setenv("DIPS_PIECE_BYTES", str(5 * 44 * 4 + 12))  # several ragged stripes
+    w, h = 44, 31
+    frames = _frames(w, h, 40, 140 + filt)
+    cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter(chroma))
+    ref = oracle.ComputeState(colorize, 1, sens, filt, chroma)
+    t = 0
+
+    def add():
+        nonlocal t
+        cs.add_texture(w, h, frames[t])
+        ref.add_texture(w, h, frames[t])
+        t += 1
+
+    def disp(tag):
+        got, want = cs.dispatch(), ref.dispatch()
+        assert (got is None) == (want is None), tag
+        if want is not None:
+            assert np.array_equal(got, want), (tag, t, np.argwhere(got != want)[:4])
+
+    try:
+        for _ in range(6):  # warm-up phase and first steady frames
+            add()
+            disp("warm")
+        for _ in range(3):
+            add()
+            disp("add+dispatch")
+        add()
+        add()  # two adds: the first deferred frame is flushed into its slot
+        disp("add,add,dispatch")
+        add()
+        disp("dispatch 1")
+        disp("dispatch twice")
+        add()
+        assert np.array_equal(cs.start_texture(), ref.start_texture())
+        disp("after start_texture")
+        add()
+        got = frame_callback(w, h, frames[t], cs)  # striped call right after a deferred add
+        want = oracle.frame_callback(w, h, frames[t], ref)
+        t += 1
+        assert np.array_equal(got, want), ("frame_callback after add", t)
+        disp("dispatch after callback")
+        add()
+        got = cs.frame_callback_batch(w, h, frames[t:t + 5])
+        want = np.stack([oracle.frame_callback(w, h, frames[t + k], ref) for k in range(5)])
+        t += 5
+        assert np.array_equal(got, want), ("batch after add", np.argwhere(got != want)[:4])
+        add()
+        add()  # two raw slots in the ring the batch reads: its first frames go one by one
+        got = cs.frame_callback_batch(w, h, frames[t:t + 6])
+        want = np.stack([oracle.frame_callback(w, h, frames[t + k], ref) for k in range(6)])
+        t += 6
+        assert np.array_equal(got, want), ("batch after two adds", np.argwhere(got != want)[:4])
+        for _ in range(4):
+            add()
+            disp("tail")
+    finally:
+        cs.close()

@@ -38,12 +38,14 @@ def main():
     ref = ComputeState(False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
     rl, rh = ref._hd._lib, ref._hd
     os.environ["DIPS_CALLBACK_STRIPED"] = "0"
+    os.environ["DIPS_DEFER_UPLOAD"] = "0"  # the reference pass: DMA upload + DMA readback
     want = {}
     for t in list(range(F)) + list(range(8, F)):
         rh.check(rl.dips_frame_callback(rh.ptr, W, H, host[t].ctypes.data, host[t].nbytes, out.ctypes.data, out.nbytes))
         if t >= 8:
             want[t] = out.copy()
     os.environ.pop("DIPS_CALLBACK_STRIPED")
+    os.environ.pop("DIPS_DEFER_UPLOAD")
     ref.close()
 
     cs = ComputeState(False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
@@ -58,13 +60,19 @@ def main():
                 ("direct split8 full-first", "1", 4 << 20, {"DIPS_DIRECT_SPLIT": "8", "DIPS_DIRECT_FIRST": "0"}),
                 ("direct split8", "1", 4 << 20, {"DIPS_DIRECT_SPLIT": "8"}),
                 ("direct split16", "1", 4 << 20, {"DIPS_DIRECT_SPLIT": "16"}),
-                ("direct split8", "1", 8 << 20, {"DIPS_DIRECT_SPLIT": "8"})]
+                ("direct split8", "1", 8 << 20, {"DIPS_DIRECT_SPLIT": "8"}),
+                # the reference's own sequence, add_texture + dispatch (the
+                # unstriped frame_callback): staged frame read by the dispatch
+                # (deferred upload) or DMA up + DMA down
+                ("add_texture+dispatch deferred", "1", 4 << 20, {"DIPS_CALLBACK_STRIPED": "0", "DIPS_DEFER_UPLOAD": "1"}),
+                ("add_texture+dispatch dma", "1", 4 << 20, {"DIPS_CALLBACK_STRIPED": "0", "DIPS_DEFER_UPLOAD": "0"})]
     res = {}
     for rnd in range(rounds):
         for name, direct, piece, extra in (variants if rnd % 2 == 0 else variants[::-1]):
             os.environ["DIPS_CALLBACK_DIRECT"] = direct
             os.environ["DIPS_PIECE_BYTES"] = str(piece)
-            for k in ("DIPS_DIRECT_STREAMS", "DIPS_DIRECT_SPLIT", "DIPS_DIRECT_FIRST"):
+            for k in ("DIPS_DIRECT_STREAMS", "DIPS_DIRECT_SPLIT", "DIPS_DIRECT_FIRST", "DIPS_CALLBACK_STRIPED",
+                      "DIPS_DEFER_UPLOAD"):
                 os.environ.pop(k, None)
             os.environ.update(extra)
             ok = True
@@ -83,7 +91,7 @@ def main():
                               "pcie_GBps_each_way": round((F - 8) * W * H * 4 / dt / 1e9, 2),
                               "outputs_equal_plain": ok}), flush=True)
     for k in ("DIPS_CALLBACK_DIRECT", "DIPS_PIECE_BYTES", "DIPS_DIRECT_STREAMS", "DIPS_DIRECT_SPLIT",
-              "DIPS_DIRECT_FIRST"):
+              "DIPS_DIRECT_FIRST", "DIPS_CALLBACK_STRIPED", "DIPS_DEFER_UPLOAD"):
         os.environ.pop(k, None)
     cs.close()
     # dips_alt send_frame, one frame per call, both forms (default N = 2)
