@@ -308,23 +308,52 @@ hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// A frame staged in pinned host memory into a ring slot (the deferred
-// add_texture's upload when no dispatch consumed it): system-scope loads, one
-// dword per thread.
-__global__ __launch_bounds__(256) void copy_from_host_kernel(const uint32_t* src, uint32_t* __restrict__ dst,
-                                                            uint64_t n_words) {
+// Copies between pinned host memory (device-visible pointer) and HBM by a
+// kernel instead of a DMA engine (the host-fed pipelines, host_stream.h):
+// system-scope accesses on the host side, one word per thread.
+template <typename T>
+__global__ __launch_bounds__(256) void copy_from_host_kernel(const T* src, T* __restrict__ dst, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-    if (i >= n_words) return;
+    if (i >= n) return;
     dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_copy_from_host(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s) {
-    if (bytes % 4u != 0) return hipErrorInvalidValue;
-    const uint64_t n = bytes / 4u;
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(copy_from_host_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s,
-                       reinterpret_cast<const uint32_t*>(src), reinterpret_cast<uint32_t*>(dst), n);
+template <typename T>
+__global__ __launch_bounds__(256) void copy_to_host_kernel(const T* __restrict__ src, T* dst, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool TO_HOST>
+static hipError_t launch_host_copy(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    const bool w8 = bytes % 8u == 0 && ((uintptr_t)src & 7u) == 0 && ((uintptr_t)dst & 7u) == 0;
+    if (!w8 && (bytes % 4u != 0 || ((uintptr_t)src & 3u) != 0 || ((uintptr_t)dst & 3u) != 0))
+        return hipErrorInvalidValue;
+    const uint64_t n = w8 ? bytes / 8u : bytes / 4u;
+    if ((n + 255) / 256 >= (1ull << 31)) return hipErrorInvalidValue;
+    const dim3 grid((uint32_t)((n + 255) / 256));
+    if (w8) {
+        auto* a = reinterpret_cast<const uint64_t*>(src);
+        auto* b = reinterpret_cast<uint64_t*>(dst);
+        if (TO_HOST) hipLaunchKernelGGL(copy_to_host_kernel<uint64_t>, grid, dim3(256), 0, s, a, b, n);
+        else hipLaunchKernelGGL(copy_from_host_kernel<uint64_t>, grid, dim3(256), 0, s, a, b, n);
+    } else {
+        auto* a = reinterpret_cast<const uint32_t*>(src);
+        auto* b = reinterpret_cast<uint32_t*>(dst);
+        if (TO_HOST) hipLaunchKernelGGL(copy_to_host_kernel<uint32_t>, grid, dim3(256), 0, s, a, b, n);
+        else hipLaunchKernelGGL(copy_from_host_kernel<uint32_t>, grid, dim3(256), 0, s, a, b, n);
+    }
     return hipGetLastError();
+}
+
+hipError_t launch_copy_from_host(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s) {
+    return launch_host_copy<false>(src, dst, bytes, s);
+}
+
+hipError_t launch_copy_to_host(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s) {
+    return launch_host_copy<true>(src, dst, bytes, s);
 }
 
 hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, bool raw_slot) {

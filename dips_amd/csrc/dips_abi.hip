@@ -1133,7 +1133,7 @@ dips_status dips_diff_series_streamed(dips_handle* h, uint32_t width, uint32_t h
         staged_copy(static_cast<uint8_t*>(h->pinned[hb].p), host_frames + (size_t)f0 * fb, (size_t)nk * fb);
         // ring[b] was read by kernel k-3 (frames) and kernel k-2 (per-frame ref)
         if (k >= 2) DIPS_HIP(h, hipStreamWaitEvent(h->copy_stream, h->kernel_done[(k - 2) % 3u], 0));
-        DIPS_HIP(h, hipMemcpyAsync(h->ring[b].p, h->pinned[hb].p, (size_t)nk * fb, hipMemcpyHostToDevice, h->copy_stream));
+        DIPS_HIP(h, dips_host::pipe_h2d(h->ring[b].p, h->pinned[hb].p, (size_t)nk * fb, h->copy_stream, true));
         DIPS_HIP(h, hipEventRecord(h->copy_done[b], h->copy_stream));
         DIPS_HIP(h, hipStreamWaitEvent(h->stream, h->copy_done[b], 0));
         const uint8_t* frames_dev = h->ring[b].as<uint8_t>();

@@ -242,8 +242,10 @@ hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, bool raw_slot = false);
 // a raw ring slot into its gray texel q(get_intensity) in place
 hipError_t launch_compat_quantise_slot(uint8_t* slot, uint64_t n_px, uint32_t chroma, hipStream_t s);
-// bytes (a multiple of 4) from pinned host memory (device-visible pointer) into HBM
+// bytes (a multiple of 4, 4-B aligned) between pinned host memory (its
+// device-visible pointer) and HBM, by a kernel instead of a DMA engine
 hipError_t launch_copy_from_host(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s);
+hipError_t launch_copy_to_host(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s);
 hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, uint32_t chroma, hipStream_t s);
 // W > 1 steady state: the ring texel compute_main stores for each of n frames
 // (gray q(spatial_median_filter(frame)), dips_shader.wgsl:120-170, 187), so

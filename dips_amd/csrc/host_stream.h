@@ -22,7 +22,45 @@
 #include "copy_pool.h"
 #include "host_buffers.h"
 
+namespace dips {  // compat_kernels.hip (also declared in dips_kernels.h)
+hipError_t launch_copy_from_host(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s);
+hipError_t launch_copy_to_host(const uint8_t* src, uint8_t* dst, uint64_t bytes, hipStream_t s);
+}  // namespace dips
+
 namespace dips_host {
+
+// Chunk copies of the host-fed pipelines between a pinned buffer and HBM: a
+// copy kernel (system-scope accesses to the pinned side) or hipMemcpyAsync
+// (a DMA engine).  Measured in one process (tools/nt_copy_ab.py --var
+// DIPS_PIPE_KERNEL_COPY): the streamed series' uploads by kernel ran 1.00-1.15x
+// the DMA rate (the kernel default there), the visual operators' two-way
+// pipe 0.81-0.82x with a kernel upload (DMA kept).  DIPS_PIPE_KERNEL_COPY
+// overrides every call site: "1" kernels both ways, "0" DMA both ways, "h" /
+// "d" a kernel for host->device / device->host only.  Read per call.
+inline bool pipe_kernel_copy(bool to_host, bool dflt) {
+    const char* e = std::getenv("DIPS_PIPE_KERNEL_COPY");
+    if (!e || !e[0]) return dflt;
+    const char c = e[0];
+    return c == '1' || (c == 'h' && !to_host) || (c == 'd' && to_host);
+}
+inline hipError_t pipe_h2d(void* dev, const void* pin, size_t bytes, hipStream_t s, bool kernel_default = false) {
+    if (pipe_kernel_copy(false, kernel_default) && bytes % 4u == 0) {
+        void* pd = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&pd, const_cast<void*>(pin), 0);
+        if (e != hipSuccess) return e;
+        return dips::launch_copy_from_host(static_cast<const uint8_t*>(pd), static_cast<uint8_t*>(dev), bytes, s);
+    }
+    return hipMemcpyAsync(dev, pin, bytes, hipMemcpyHostToDevice, s);
+}
+inline hipError_t pipe_d2h(void* pin, const void* dev, size_t bytes, hipStream_t s, bool kernel_default = false) {
+    if (pipe_kernel_copy(true, kernel_default) && bytes % 4u == 0) {
+        void* pd = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&pd, pin, 0);
+        if (e != hipSuccess) return e;
+        return dips::launch_copy_to_host(static_cast<const uint8_t*>(dev), static_cast<uint8_t*>(pd), bytes, s);
+    }
+    return hipMemcpyAsync(pin, dev, bytes, hipMemcpyDeviceToHost, s);
+}
 
 // Host copy over the persistent pool (copy_pool.h).
 inline void staged_copy(uint8_t* dst, const uint8_t* src, size_t bytes) { pool_copy(dst, src, bytes); }
@@ -442,7 +480,7 @@ hipError_t run_stream_pipe(StreamPipe& p, hipStream_t compute, uint64_t n, size_
             staged_copy(p.pin_in[b].bytes(), in + k * chunk * ib, m * ib);
             const auto t2 = clk::now();
             if (k >= 2 && (e = hipStreamWaitEvent(p.up, p.computed[b], 0)) != hipSuccess) return e;
-            if ((e = hipMemcpyAsync(p.dev_in[b].p, p.pin_in[b].p, m * ib, hipMemcpyHostToDevice, p.up)) != hipSuccess)
+            if ((e = pipe_h2d(p.dev_in[b].p, p.pin_in[b].p, m * ib, p.up)) != hipSuccess)
                 return e;
             if ((e = hipEventRecord(p.uploaded[b], p.up)) != hipSuccess) return e;
             // dev_out[b] was last read by chunk k-2's download
@@ -458,7 +496,7 @@ hipError_t run_stream_pipe(StreamPipe& p, hipStream_t compute, uint64_t n, size_
             }
             if ((e = hipEventRecord(p.computed[b], compute)) != hipSuccess) return e;
             if ((e = hipStreamWaitEvent(p.down, p.computed[b], 0)) != hipSuccess) return e;
-            if ((e = hipMemcpyAsync(p.pin_out[b].p, p.dev_out[b].p, m * ob, hipMemcpyDeviceToHost, p.down)) != hipSuccess)
+            if ((e = pipe_d2h(p.pin_out[b].p, p.dev_out[b].p, m * ob, p.down)) != hipSuccess)
                 return e;
             if ((e = hipEventRecord(p.downloaded[b], p.down)) != hipSuccess) return e;
             if (trace)

@@ -251,12 +251,14 @@ def test_rejects_bad_input():
 
 
 @pytest.mark.parametrize("chunk_frames", [1, 4, 9])
-def test_run_host_feed_chunks(monkeypatch, chunk_frames):
+@pytest.mark.parametrize("copies", ["", "1"])  # default (DMA) / copy kernels both ways
+def test_run_host_feed_chunks(monkeypatch, chunk_frames, copies):
     """Host frames go through the pipelined feed in chunks; with a few frames
     per chunk (ragged last chunk, refresh markers and snapshots falling on
     chunk edges) the loop's outputs equal the oracle's."""
     from dips_amd.alt import DiPsRunner
     w, h = 32, 24
+    monkeypatch.setenv("DIPS_PIPE_KERNEL_COPY", copies)
     monkeypatch.setenv("DIPS_FEED_CHUNK_BYTES", str(chunk_frames * w * h * 4))
     frames = _frames(w, h, 50, 40 + chunk_frames)
     markers = [4, 9, 10, 27, 36]

@@ -253,12 +253,14 @@ def test_frame_callback_batch_device_4k():
 
 
 @pytest.mark.parametrize("chunk_frames", [1, 3, 7])
-def test_frame_callback_batch_host_feed_chunks(monkeypatch, chunk_frames):
+@pytest.mark.parametrize("copies", ["", "1"])  # default (DMA) / copy kernels both ways
+def test_frame_callback_batch_host_feed_chunks(monkeypatch, chunk_frames, copies):
     """The host-pointer batch is fed through the pipelined upload / kernel /
     download in chunks (two in flight); forced down to a few frames per chunk
     with a ragged last chunk, the outputs stay those of the oracle."""
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter
     w, h = 64, 48
+    monkeypatch.setenv("DIPS_PIPE_KERNEL_COPY", copies)
     monkeypatch.setenv("DIPS_FEED_CHUNK_BYTES", str(chunk_frames * w * h * 4))
     frames = _frames(w, h, 61, 5 + chunk_frames)
     params = (True, 1, 5.0, 0, 0)

@@ -130,8 +130,10 @@ def test_identical_frames_zero():
         assert not m.any()
 
 
-def test_streamed_equals_batch():
+@pytest.mark.parametrize("copies", ["", "0"])  # default (copy kernel uploads) / DMA
+def test_streamed_equals_batch(monkeypatch, copies):
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    monkeypatch.setenv("DIPS_PIPE_KERNEL_COPY", copies)
     frames = _frames(3, 64, 48, 23, 7, "synth")
     ref = _frames(3, 64, 48, 1, 8, "random")[0]
     for mode in (Mode.Overall, Mode.PerFrame):

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""nt_copy_ab.py -- A/B of the host staging copy (copy_pool.h host_copy:
-streaming AVX2 stores vs memcpy, DIPS_NT_COPY=1/0) in ONE process,
-alternated over rounds, on every host-memory path of the library:
+"""nt_copy_ab.py -- in-process A/B of a host-path switch, alternated over
+rounds, on every host-memory path of the library.  Default: the staging copy
+(copy_pool.h host_copy: streaming AVX2 stores vs memcpy, DIPS_NT_COPY=1/0);
+--var DIPS_PIPE_KERNEL_COPY: the host-fed pipelines' chunk copies by kernel
+vs DMA engine (host_stream.h pipe_h2d / pipe_d2h).  Paths:
   * dips frame_callback, one 4K RGBA8 frame per call (the reference's own
     pattern, dips/src/lib.rs:233-246), striped;
   * dips_alt send_frame, one frame per call;
@@ -27,9 +29,16 @@ def main():
     from dips_amd import ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, Mode, PixelFormat
     from dips_amd.alt import DiPsCompute
 
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("frames", type=int, nargs="?", default=48)
+    ap.add_argument("rounds", type=int, nargs="?", default=3)
+    ap.add_argument("--var", default="DIPS_NT_COPY")
+    ap.add_argument("--values", default="1,0", help="values of --var, alternated (first two summarised as on/off)")
+    args = ap.parse_args()
+    values = args.values.split(",")
     W, H = 3840, 2160
-    F = int(sys.argv[1]) if len(sys.argv) > 1 else 48
-    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    F, rounds, var = args.frames, args.rounds, args.var
     dev = torch.empty((F, H, W, 4), dtype=torch.uint8, device="cuda")
     op = DiffSeriesOperator(PixelFormat.RGBA8)
     op.synth_device(dev, W, H, 0xD1B5, 0)
@@ -86,25 +95,24 @@ def main():
              ("dips_alt send_frame per frame, 4K RGBA8", send_frame, 2 * fb),
              ("frame_callback_batch from host, 4K RGBA8", batch, 2 * fb),
              ("series streamed from host, 4K RGB8", streamed, W * H * 3)]
-    summary = {p[0]: {"1": [], "0": [], "check": {}} for p in paths}
+    summary = {p[0]: {**{v: [] for v in values}, "check": {}} for p in paths}
     for rnd in range(rounds):
-        for nt in ("1", "0") if rnd % 2 == 0 else ("0", "1"):
-            os.environ["DIPS_NT_COPY"] = nt
+        for nt in (values if rnd % 2 == 0 else values[::-1]):
+            os.environ[var] = nt
             for name, fn, bpf in paths:
                 n, dt, chk = fn()
                 fps = n / dt
                 summary[name][nt].append(fps)
                 if rnd >= 1:  # round 0's batch follows the warm-up frames, later ones the same tail
                     summary[name]["check"].setdefault(nt, chk)
-                print(json.dumps({"path": name, "nt_copy": nt == "1", "round": rnd, "frames": n,
+                print(json.dumps({"path": name, var: nt, "round": rnd, "frames": n,
                                   "frames_per_s": round(fps, 1), "ms_per_frame": round(dt / n * 1e3, 3),
                                   "pcie_GBps": round(n * bpf / dt / 1e9, 2), "check": chk}), flush=True)
-    os.environ.pop("DIPS_NT_COPY", None)
+    os.environ.pop(var, None)
     for name, s in summary.items():
-        print(json.dumps({"path": name, "summary": True,
-                          "nt_fps_median": round(float(np.median(s["1"])), 1),
-                          "memcpy_fps_median": round(float(np.median(s["0"])), 1),
-                          "ratio": round(float(np.median(s["1"]) / np.median(s["0"])), 4),
+        print(json.dumps({"path": name, "summary": True, "var": var,
+                          "fps_median": {v: round(float(np.median(s[v])), 1) for v in values},
+                          "ratio_first_second": round(float(np.median(s[values[0]]) / np.median(s[values[1]])), 4),
                           "outputs_equal": len(set(s["check"].values())) == 1}), flush=True)
     for o in (cs, csb, alt):
         o.close()
