@@ -669,7 +669,7 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     ALT_HIP(h, h->io_out.ensure(fb));
     ALT_HIP(h, hipStreamSynchronize(h->meta_stream));  // no upload of an earlier call still reads `io`
     // zero-copy form (default; DIPS_CALLBACK_DIRECT=0 selects the DMA form
-    // below): the kernel reads the staged stripe from pinned host memory,
+    // after this block): the kernel reads the staged stripe from pinned host memory,
     // stores it into the slot and writes its output to pinned host memory;
     // odd stripes on meta_stream (idle here, synchronised above)
     const char* direct_env = std::getenv("DIPS_CALLBACK_DIRECT");

@@ -529,9 +529,11 @@ bool defer_upload(const dips_handle* h) {
 
 // ComputeState::add_texture (dips/src/gpu/mod.rs:170-216) from a host frame
 // (through the pinned staging buffer) or a device frame (D2D).  In steady
-// state with W = 1 a host frame is only staged into the pinned buffer and the
-// next dispatch reads it from there (zero-copy, both PCIe directions at once,
-// as in frame_callback_striped); the ring bookkeeping is the same.
+// state with W = 1 a host frame is staged into the pinned buffer and the
+// compute of the dispatch that normally follows is launched on it, stripe by
+// stripe (zero-copy, both PCIe directions at once, as in
+// frame_callback_striped; see dips_handle::pending); the ring bookkeeping is
+// the same.
 dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frame, size_t len,
                              bool device_src) {
     if (!frame || width == 0 || height == 0) return fail(h, DIPS_ERR_INVALID, "add_texture: empty frame");
@@ -893,8 +895,9 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
     a.sensitivity = h->p.sensitivity;
     a.colorize = h->p.colorize ? 1u : 0u;
     // zero-copy form (default; DIPS_CALLBACK_DIRECT=0 selects the DMA form
-    // above): the main kernel reads the staged stripe from pinned host memory
-    // and writes its output there, the pool copies stripes in and out
+    // after this block): the main kernel reads the staged stripe from pinned
+    // host memory and writes its output there, the pool copies stripes in and
+    // out
     const char* direct_env = std::getenv("DIPS_CALLBACK_DIRECT");
     if (!direct_env || direct_env[0] != '0') {
         void *din = nullptr, *dout = nullptr;
