@@ -118,7 +118,12 @@ dips_status dips_synchronize(dips_handle *h);
 /* Replaces ComputeState::add_texture (dips/src/gpu/mod.rs:170-216): queue an
  * RGBA8 host frame (len = width*height*4, stride = width*4 as at
  * bind_groups.rs:264); the 4th frame builds the start texture and the
- * temporal ring, later frames replace the ring slot. */
+ * temporal ring, later frames replace the ring slot.  The frame is read
+ * before the call returns (borrowed, as in the reference).  In steady state
+ * (window 1, host pointers) the call also starts the compute of the
+ * dispatch that normally follows on the staged frame; that dispatch then
+ * only collects it, and any other call first lets it finish, keeping the
+ * reference's state (DIPS_DEFER_UPLOAD=0 turns this off). */
 dips_status dips_add_texture(dips_handle *h, uint32_t width, uint32_t height,
                              const uint8_t *frame_rgba, size_t len);
 
