@@ -135,15 +135,20 @@ __global__ __launch_bounds__(256) void compat_precompute_kernel(CompatArgs a) {
 
 // compute_main's per-pixel tail once the newest slot's filtered intensity fi
 // is known (dips_shader.wgsl:187-239).
-// raw_slot: the newest slot receives the frame's raw texel instead of the
-// quantised one (the speculative dispatch of a deferred add_texture; the
-// dispatch that claims it quantises the slot, compat_gray_kernel in place).
-__device__ __forceinline__ uint32_t compat_texel(const CompatArgs& a, uint64_t p, float fi, bool raw_slot = false,
+// Slot store of compat_texel: kSlotQ stores the quantised filtered texel
+// (compute_main, dips_shader.wgsl:187); the speculative dispatch of a deferred
+// add_texture stores the frame's raw texel (kSlotRaw, W = 1) or nothing
+// (kSlotNone, W > 1: the upload already put the raw frame there); the
+// dispatch that claims it stores the gray texel afterwards.
+constexpr int kSlotQ = 0, kSlotRaw = 1, kSlotNone = 2;
+
+__device__ __forceinline__ uint32_t compat_texel(const CompatArgs& a, uint64_t p, float fi, int slot_mode = kSlotQ,
                                                  uint32_t raw = 0u) {
     // in-place store of the filtered newest slot, quantised (dips_shader.wgsl:187)
     const uint32_t qi = unorm_store(fi);
-    *reinterpret_cast<uint32_t*>(a.slots[a.newest] + 4 * p) =
-        raw_slot ? raw : (qi | (qi << 8) | (qi << 16) | (255u << 24));
+    if (slot_mode != kSlotNone)
+        *reinterpret_cast<uint32_t*>(a.slots[a.newest] + 4 * p) =
+            slot_mode == kSlotRaw ? raw : (qi | (qi << 8) | (qi << 16) | (255u << 24));
     float m[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -178,7 +183,7 @@ __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
 // contiguous bytes each way.  (Four pixels per thread through 16-B
 // system-coherent buffer loads / stores measured slower: 557-575 against
 // 695-701 frames/s of 4K per-frame calls, tools/callback_direct_ab.py.)
-template <bool RAW_SLOT>
+template <int SLOT_MODE>
 __global__ __launch_bounds__(256) void compat_main_host_kernel(CompatArgs a) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     const uint64_t p = (uint64_t)a.y0 * a.width + (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(256) void compat_main_host_kernel(CompatArgs a) {
     const uint32_t v = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a.raw + 4 * p), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_SYSTEM);
     const float fi = intensity_rgb(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, a.chroma);
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 4 * p), compat_texel(a, p, fi, RAW_SLOT, v),
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 4 * p), compat_texel(a, p, fi, SLOT_MODE, v),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -356,15 +361,17 @@ hipError_t launch_copy_to_host(const uint8_t* src, uint8_t* dst, uint64_t bytes,
     return launch_host_copy<true>(src, dst, bytes, s);
 }
 
-hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, bool raw_slot) {
+hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, int slot_mode) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
     const uint64_t n_px = (uint64_t)(yend - a.y0) * a.width;
     const dim3 grid((uint32_t)((n_px + 255) / 256));
-    if (raw_slot)
-        hipLaunchKernelGGL(compat_main_host_kernel<true>, grid, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(compat_main_host_kernel<false>, grid, dim3(256), 0, s, a);
+    switch (slot_mode) {
+        case kSlotQ: hipLaunchKernelGGL(compat_main_host_kernel<kSlotQ>, grid, dim3(256), 0, s, a); break;
+        case kSlotRaw: hipLaunchKernelGGL(compat_main_host_kernel<kSlotRaw>, grid, dim3(256), 0, s, a); break;
+        case kSlotNone: hipLaunchKernelGGL(compat_main_host_kernel<kSlotNone>, grid, dim3(256), 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

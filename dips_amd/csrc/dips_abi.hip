@@ -45,6 +45,7 @@ struct dips_handle {
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;
     hipEvent_t switch_ev = nullptr;  // orders a newly set stream after the previous one
+    hipEvent_t join_ev = nullptr;    // orders the stream after copy_stream (deferred W > 1 upload)
     std::string err;
 
     // batch series workspace
@@ -463,6 +464,7 @@ void dips_destroy(dips_handle* h) {
     h->out.release();
     h->io.release();
     if (h->switch_ev) (void)hipEventDestroy(h->switch_ev);
+    if (h->join_ev) (void)hipEventDestroy(h->join_ev);
     if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     if (h->copy_stream) (void)hipStreamDestroy(h->copy_stream);
     delete h;
@@ -522,7 +524,7 @@ dips_status flush_pending(dips_handle* h) {
 
 // Deferral of host frames in steady state (DIPS_DEFER_UPLOAD=0 turns it off).
 bool defer_upload(const dips_handle* h) {
-    if (!h->main_init || h->p.spatial_window_size != 1 || (h->p.flags & DIPS_FLAG_DEVICE_PTRS)) return false;
+    if (!h->main_init || (h->p.flags & DIPS_FLAG_DEVICE_PTRS)) return false;
     const char* e = std::getenv("DIPS_DEFER_UPLOAD");
     return !(e && e[0] == '0');
 }
@@ -571,14 +573,45 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
         a.filter = h->p.filter_type;
         a.sensitivity = h->p.sensitivity;
         a.colorize = h->p.colorize ? 1u : 0u;
-        h->pend_geom.init(height, (size_t)width * 4u);
+        const size_t row = (size_t)width * 4u;
+        h->pend_geom.init(height, row);
         const hipStream_t cs[2] = {h->stream, h->copy_stream};
-        DIPS_HIP(h, dips_host::direct_stage_launch(frame, h->io.bytes(), cs, h->device, h->pieces, h->pend_geom,
-                                                   [&](uint32_t y0, uint32_t y1, hipStream_t st) {
-                                                       a.y0 = y0;
-                                                       a.y1 = y1;
-                                                       return dips::launch_compat_main_host(a, st, true);
-                                                   }));
+        const int32_t win = h->p.spatial_window_size;
+        if (win == 1) {
+            DIPS_HIP(h, dips_host::direct_stage_launch(frame, h->io.bytes(), cs, h->device, h->pieces, h->pend_geom,
+                                                       [&](uint32_t y0, uint32_t y1, hipStream_t st) {
+                                                           a.y0 = y0;
+                                                           a.y1 = y1;
+                                                           return dips::launch_compat_main_host(a, st, 1);
+                                                       }));
+        } else {
+            // W > 1: the filter needs the whole frame, so the stripes first go
+            // into the slot (copy kernels from the pinned buffer, launched as
+            // the pool stages them), then the spatial filter of the newest
+            // slot into `raw` (dips_shader.wgsl:120-170, as dispatch_impl),
+            // then compute_main per stripe with its output into io_out
+            uint8_t* dslot = h->slots[slot].as<uint8_t>();
+            const uint8_t* dsrc = static_cast<const uint8_t*>(din);
+            DIPS_HIP(h, dips_host::direct_stage_launch(frame, h->io.bytes(), cs, h->device, h->up_pieces,
+                                                       h->pend_geom, [&](uint32_t y0, uint32_t y1, hipStream_t st) {
+                                                           return dips::launch_copy_from_host(
+                                                               dsrc + (size_t)y0 * row, dslot + (size_t)y0 * row,
+                                                               (uint64_t)(y1 - y0) * row, st);
+                                                       }));
+            if (!h->join_ev) DIPS_HIP(h, hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+            DIPS_HIP(h, hipEventRecord(h->join_ev, h->copy_stream));
+            DIPS_HIP(h, hipStreamWaitEvent(h->stream, h->join_ev, 0));
+            DIPS_HIP(h, dips::launch_compat_filter_frames(dslot, h->raw.as<uint8_t>(), width, height, 1, win,
+                                                          h->p.chroma_filter, h->stream));
+            a.raw = h->raw.as<uint8_t>();
+            DIPS_HIP(h, h->pieces.ensure(h->pend_geom.n_s));
+            for (uint32_t si = 0; si < h->pend_geom.n_s; ++si) {
+                a.y0 = h->pend_geom.y0(si);
+                a.y1 = h->pend_geom.y1(si);
+                DIPS_HIP(h, dips::launch_compat_main_host(a, h->stream, 2));
+                DIPS_HIP(h, hipEventRecord(h->pieces.ev[si], h->stream));
+            }
+        }
         h->pending = true;
         h->pending_slot = slot;
         return DIPS_OK;
@@ -640,12 +673,17 @@ int dispatch_impl(dips_handle* h, uint8_t* out, size_t cap, bool device_dst) {
     if (cap < fb) return fail(h, DIPS_ERR_CAPACITY, "dispatch: output buffer smaller than width*height*4");
     if (h->pending && !device_dst) {
         // the speculative compute_main of the deferred add_texture: collect
-        // its stripes, then store the quantised texel into the newest slot
-        // (every stripe's kernel has finished once collected)
+        // its stripes, then store the gray texel into the newest slot (every
+        // stripe's kernel has finished once collected): W = 1 quantises the
+        // raw frame in place, W > 1 copies the filtered texel from `raw`
         h->pending = false;
         DIPS_HIP(h, dips_host::direct_collect(out, h->io_out.bytes(), h->pieces, h->pend_geom));
-        DIPS_HIP(h, dips::launch_compat_quantise_slot(h->slots[h->pending_slot].as<uint8_t>(),
-                                                      (uint64_t)h->width * h->height, h->p.chroma_filter, h->stream));
+        uint8_t* dslot = h->slots[h->pending_slot].as<uint8_t>();
+        if (h->p.spatial_window_size == 1)
+            DIPS_HIP(h, dips::launch_compat_quantise_slot(dslot, (uint64_t)h->width * h->height, h->p.chroma_filter,
+                                                          h->stream));
+        else
+            DIPS_HIP(h, dips::launch_copy_from_host(h->raw.as<uint8_t>(), dslot, fb, h->stream));
         h->slot_raw[h->pending_slot] = false;
         return 1;
     }

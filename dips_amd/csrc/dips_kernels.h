@@ -237,9 +237,10 @@ hipError_t launch_read_walk(const SeriesArgs& a, int vec_bytes, uint32_t blocks,
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s);
 // compat_main with raw / out in pinned host memory (zero-copy per-frame call)
-// raw_slot: store the raw frame texel into the newest slot instead of its
-// quantised gray texel (the speculative dispatch of a deferred add_texture)
-hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, bool raw_slot = false);
+// slot_mode 0: store the quantised gray texel into the newest slot
+// (compute_main); 1: store the raw frame texel, 2: store nothing (the
+// speculative dispatch of a deferred add_texture, W = 1 / W > 1)
+hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, int slot_mode = 0);
 // a raw ring slot into its gray texel q(get_intensity) in place
 hipError_t launch_compat_quantise_slot(uint8_t* slot, uint64_t n_px, uint32_t chroma, hipStream_t s);
 // bytes (a multiple of 4, 4-B aligned) between pinned host memory (its

@@ -464,11 +464,13 @@ def test_batch_epilogue_table_equals_arithmetic_and_oracle(colorize, filt, sens,
 
 
 @pytest.mark.parametrize("defer", ["1", "0"])
-@pytest.mark.parametrize("colorize,sens,filt,chroma", [(False, 5.0, 255, 0), (True, 0.7, 0, 3)])
-def test_deferred_add_texture_sequences_match_oracle(monkeypatch, defer, colorize, sens, filt, chroma):
-    """add_texture in steady state (W = 1, host frame) only stages the frame;
-    the next dispatch reads it from pinned memory (zero-copy), and every other
-    call first copies it into its slot.  Mixed call sequences -- add + dispatch,
+@pytest.mark.parametrize("colorize,sens,filt,chroma,window", [(False, 5.0, 255, 0, 1), (True, 0.7, 0, 3, 1),
+                                                             (False, 5.0, 255, 0, 4), (True, 5.0, 1, 2, 7)])
+def test_deferred_add_texture_sequences_match_oracle(monkeypatch, defer, colorize, sens, filt, chroma, window):
+    """add_texture in steady state (host frame) stages the frame and starts
+    the dispatch that normally follows on it (zero-copy; W > 1: upload,
+    spatial filter, then the main kernel); that dispatch collects it, every
+    other call first lets it finish and keeps the slot raw.  Mixed call sequences -- add + dispatch,
     two adds without a dispatch, dispatch twice, add then start_texture, add
     then a striped frame_callback, add then a host batch -- give the oracle's
     outputs and ring state, with the deferral on and off."""
@@ -477,8 +479,8 @@ def test_deferred_add_texture_sequences_match_oracle(monkeypatch, defer, coloriz
     monkeypatch.setenv("DIPS_PIECE_BYTES", str(5 * 44 * 4 + 12))  # several ragged stripes
     w, h = 44, 31
     frames = _frames(w, h, 40, 140 + filt)
-    cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter(chroma))
-    ref = oracle.ComputeState(colorize, 1, sens, filt, chroma)
+    cs = ComputeState(colorize, window, sens, DiPsFilter(filt), ChromaFilter(chroma))
+    ref = oracle.ComputeState(colorize, window, sens, filt, chroma)
     t = 0
 
     def add():
