@@ -125,6 +125,7 @@ struct dips_alt_handle {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     hipEvent_t switch_ev = nullptr;  // orders a newly set stream after the previous one
+    hipEvent_t join_ev = nullptr;    // orders the stream after meta_stream (zero-copy W > 1 upload)
     std::string err;
 
     DevBuf slots[dips::kAltMaxTextures];  // input_textures (mod.rs:279-301)
@@ -578,6 +579,7 @@ void dips_alt_destroy(dips_alt_handle* h) {
         if (ev) (void)hipEventDestroy(ev);
     if (h->meta_free) (void)hipEventDestroy(h->meta_free);
     if (h->switch_ev) (void)hipEventDestroy(h->switch_ev);
+    if (h->join_ev) (void)hipEventDestroy(h->join_ev);
     if (h->meta_stream) (void)hipStreamDestroy(h->meta_stream);
     for (auto& mp : h->meta_pin) mp.release();
     for (auto& s : h->slots) s.release();
@@ -642,7 +644,14 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     uint8_t* slot = h->slots[h->sent % N].as<uint8_t>();
     const char* striped_env = std::getenv("DIPS_CALLBACK_STRIPED");  // "0": whole-frame transfers
     const bool striped = h->p.window_size == 1 && (!striped_env || striped_env[0] != '0');
-    if (!striped) ALT_HIP(h, dips_host::upload_via(slot, frame, fb, h->io.bytes(), h->stream));
+    const char* direct_env = std::getenv("DIPS_CALLBACK_DIRECT");
+    const bool direct = !direct_env || direct_env[0] != '0';
+    // W > 1, zero-copy form (default): the stripes go into the slot by copy
+    // kernels as the pool stages them, the frame kernel runs on the whole
+    // frame, and its output comes back by copy kernels into pinned memory,
+    // stripe by stripe, copied out as each lands
+    const bool window_direct = h->p.window_size > 1 && direct && fb % 4u == 0;
+    if (!striped && !window_direct) ALT_HIP(h, dips_host::upload_via(slot, frame, fb, h->io.bytes(), h->stream));
     h->sent += 1;
     dips::AltArgs a{};
     for (uint32_t k = 0; k < N; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
@@ -657,6 +666,38 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     a.scalar = h->p.sigmoid_horizontal_scalar;
     a.colorize = h->p.colorize ? 1u : 0u;
     a.snapshot = snapshot ? 1u : 0u;
+    if (window_direct) {
+        ALT_HIP(h, h->io_out.ensure(fb));
+        ALT_HIP(h, hipStreamSynchronize(h->meta_stream));
+        void *din = nullptr, *dout = nullptr;
+        ALT_HIP(h, hipHostGetDevicePointer(&din, h->io.p, 0));
+        ALT_HIP(h, hipHostGetDevicePointer(&dout, h->io_out.p, 0));
+        const size_t row = (size_t)h->width * 4u;
+        dips_host::DirectGeom g;
+        g.init(h->height, row);
+        const hipStream_t cs[2] = {h->stream, h->meta_stream};
+        const uint8_t* src = static_cast<const uint8_t*>(din);
+        ALT_HIP(h, dips_host::direct_stage_launch(frame, h->io.bytes(), cs, h->device, h->up_pieces, g,
+                                                  [&](uint32_t y0, uint32_t y1, hipStream_t st) {
+                                                      return dips::launch_copy_from_host(src + (size_t)y0 * row,
+                                                                                         slot + (size_t)y0 * row,
+                                                                                         (uint64_t)(y1 - y0) * row, st);
+                                                  }));
+        if (!h->join_ev) ALT_HIP(h, hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+        ALT_HIP(h, hipEventRecord(h->join_ev, h->meta_stream));
+        ALT_HIP(h, hipStreamWaitEvent(h->stream, h->join_ev, 0));
+        ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
+        ALT_HIP(h, h->pieces.ensure(g.n_s));
+        const uint8_t* o1 = h->out1.as<uint8_t>();
+        uint8_t* dst = static_cast<uint8_t*>(dout);
+        for (uint32_t si = 0; si < g.n_s; ++si) {
+            const size_t o = (size_t)g.y0(si) * row, len = (size_t)(g.y1(si) - g.y0(si)) * row;
+            ALT_HIP(h, dips::launch_copy_to_host(o1 + o, dst + o, len, h->stream));
+            ALT_HIP(h, hipEventRecord(h->pieces.ev[si], h->stream));
+        }
+        ALT_HIP(h, dips_host::direct_collect(out, h->io_out.bytes(), h->pieces, g));
+        return DIPS_OK;
+    }
     if (!striped) {
         ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
         // copy_texture_to_buffer + map_async + de-pad (mod.rs:597-643)
@@ -672,8 +713,7 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
     // after this block): the kernel reads the staged stripe from pinned host memory,
     // stores it into the slot and writes its output to pinned host memory;
     // odd stripes on meta_stream (idle here, synchronised above)
-    const char* direct_env = std::getenv("DIPS_CALLBACK_DIRECT");
-    if (!direct_env || direct_env[0] != '0') {
+    if (direct) {
         void *din = nullptr, *dout = nullptr;
         ALT_HIP(h, hipHostGetDevicePointer(&din, h->io.p, 0));
         ALT_HIP(h, hipHostGetDevicePointer(&dout, h->io_out.p, 0));

@@ -382,3 +382,30 @@ def test_batch_lut_equals_arithmetic_and_oracle(filt, colorize, window, chroma, 
     assert np.array_equal(outs["1"], outs["0"]), np.argwhere(outs["1"] != outs["0"])[:4]
     want = oracle.AltCompute(2, w, h, colorize, window, 4.0, filt, chroma).run(frames, markers)
     assert np.array_equal(outs["1"], want), np.argwhere(outs["1"] != want)[:4]
+
+
+@pytest.mark.parametrize("window", [3, 6])
+@pytest.mark.parametrize("form", ["direct", "dma"])
+@pytest.mark.parametrize("piece", ["rows3", "odd"])
+def test_send_frame_window_stripes_match_oracle(monkeypatch, window, form, piece):
+    """send_frame with W > 1: the zero-copy form uploads the stripes into the
+    slot by copy kernels, runs the frame kernel on the whole frame and brings
+    the output back by copy kernels, stripe by stripe (several ragged stripes
+    here); the DMA form moves whole frames.  Every output equals the
+    oracle's, snapshots included."""
+    from dips_amd.alt import DiPsCompute
+    w, h = 41, 23
+    row = w * 4
+    monkeypatch.setenv("DIPS_PIECE_BYTES", str({"rows3": 3 * row, "odd": 5 * row + 9}[piece]))
+    monkeypatch.setenv("DIPS_CALLBACK_DIRECT", "0" if form == "dma" else "1")
+    frames = _frames(w, h, 10, 300 + window)
+    gpu = DiPsCompute(3, h, w, _props(True, window, 3.0, 0, 0))
+    ref = oracle.AltCompute(3, w, h, True, window, 3.0, 0, 0)
+    try:
+        for t in range(10):
+            snap = t in (1, 5)
+            a = gpu.send_frame(frames[t], () if snap else None)
+            b = ref.send_frame(frames[t], snap)
+            assert np.array_equal(a, b), (t, np.argwhere(a != b)[:4])
+    finally:
+        gpu.close()

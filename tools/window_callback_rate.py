@@ -54,6 +54,30 @@ def main():
                           "outputs_equal": bool(np.array_equal(last["1"], last["0"]))}), flush=True)
     for k in ("DIPS_CALLBACK_STRIPED", "DIPS_DEFER_UPLOAD"):
         os.environ.pop(k, None)
+    # dips_alt send_frame with a window: zero-copy (default) vs DMA
+    from dips_amd.alt import DiPsCompute, DiPsProperties
+    for win in (3, 5, 11):
+        res, last = {}, {}
+        for rnd in range(2):
+            for direct in (("1", "0") if rnd == 0 else ("0", "1")):
+                os.environ["DIPS_CALLBACK_DIRECT"] = direct
+                c = DiPsCompute(2, H, W, DiPsProperties(window_size=win))
+                ha = c._host
+                for t in range(4):
+                    ha.check(ha._lib.dips_alt_send_frame(ha.ptr, host[t].ctypes.data, host[t].nbytes, 0,
+                                                         out.ctypes.data, out.nbytes))
+                t0 = time.perf_counter()
+                for t in range(4, F):
+                    ha.check(ha._lib.dips_alt_send_frame(ha.ptr, host[t].ctypes.data, host[t].nbytes, 0,
+                                                         out.ctypes.data, out.nbytes))
+                dt = time.perf_counter() - t0
+                c.close()
+                res.setdefault(direct, []).append((F - 4) / dt)
+                last[direct] = out.copy()
+        print(json.dumps({"alt_window": win, "zero_copy_fps": [round(v, 1) for v in res["1"]],
+                          "dma_fps": [round(v, 1) for v in res["0"]],
+                          "outputs_equal": bool(np.array_equal(last["1"], last["0"]))}), flush=True)
+    os.environ.pop("DIPS_CALLBACK_DIRECT", None)
 
 
 if __name__ == "__main__":
