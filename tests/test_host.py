@@ -104,3 +104,71 @@ def test_host_staging_copy_matches_memcpy(tmp_path):
     subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", f"-I{csrc}", str(src), "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout + r.stderr
+
+
+_GEOM_CHECK = r"""
+#include "host_stream.h"
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+int main() {
+    int bad = 0, cases = 0;
+    const size_t pieces[] = {64, 1000, 4096, 1u << 20, 4u << 20, 8u << 20};
+    const uint32_t heights[] = {1, 2, 3, 7, 29, 1080, 2160};
+    const size_t rows[] = {4, 160, 164, 7680, 15360};
+    const char* splits[] = {"1", "3", "8", "64"};
+    const char* firsts[] = {"0", "1"};
+    for (size_t pb : pieces) for (uint32_t hgt : heights) for (size_t row : rows) for (const char* sp : splits)
+    for (const char* fr : firsts) {
+        setenv("DIPS_PIECE_BYTES", std::to_string(pb).c_str(), 1);
+        setenv("DIPS_DIRECT_SPLIT", sp, 1);
+        setenv("DIPS_DIRECT_FIRST", fr, 1);
+        dips_host::DirectGeom g;
+        g.init(hgt, row);
+        ++cases;
+        // stripes cover [0, height) in order, each non-empty
+        uint32_t y = 0;
+        for (uint32_t si = 0; si < g.n_s; ++si) {
+            if (g.y0(si) != y || g.y1(si) <= g.y0(si)) { ++bad; break; }
+            y = g.y1(si);
+        }
+        if (y != hgt) ++bad;
+        // pieces cover each stripe's bytes exactly, cuts 64-B aligned inside the stripe
+        for (uint32_t si = 0; si < g.n_s; ++si) {
+            size_t at = (size_t)g.y0(si) * row;
+            for (uint32_t j = 0; j < g.k; ++j) {
+                size_t o, len;
+                g.piece(si, j, o, len);
+                if (o != at) { ++bad; break; }
+                if (j + 1 < g.k && ((o + len - (size_t)g.y0(si) * row) % 64) != 0 && len) ++bad;
+                at = o + len;
+            }
+            if (at != (size_t)g.y1(si) * row) ++bad;
+        }
+    }
+    std::printf("cases=%d bad=%d\n", cases, bad);
+    return bad != 0;
+}
+"""
+
+
+def test_zero_copy_stripe_geometry(tmp_path):
+    """host_stream.h DirectGeom (the zero-copy per-frame pipeline): for every
+    stripe size, frame height, row size, copy-pool split and first-stripe
+    setting, the stripes cover the frame's rows in order with none empty, and
+    each stripe's pieces cover its bytes exactly with cuts 64-B aligned
+    inside the stripe."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None or not os.path.exists("/opt/rocm/include/hip/hip_runtime.h"):
+        pytest.skip("no g++ or HIP headers")
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dips_amd", "csrc")
+    src = tmp_path / "geom_check.cpp"
+    src.write_text(_GEOM_CHECK)
+    exe = tmp_path / "geom_check"
+    subprocess.run(["g++", "-O1", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    f"-I{csrc}", str(src), "-o", str(exe), "-L/opt/rocm/lib", "-lamdhip64"], check=True)
+    env = dict(os.environ, LD_LIBRARY_PATH="/opt/rocm/lib:" + os.environ.get("LD_LIBRARY_PATH", ""))
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout + r.stderr
