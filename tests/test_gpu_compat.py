@@ -533,3 +533,36 @@ def test_deferred_add_texture_sequences_match_oracle(monkeypatch, defer, coloriz
             disp("tail")
     finally:
         cs.close()
+
+
+@pytest.mark.parametrize("window", [1, 3])
+def test_deferred_add_texture_across_stream_switches(window):
+    """dips_set_stream between calls: before an add_texture (the speculative
+    dispatch runs on the new stream) and between an add_texture and its
+    dispatch (the switch first lets the speculative kernels finish; the
+    dispatch then computes from the raw slot) -- outputs equal the oracle's."""
+    import ctypes
+    import torch
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+    w, h = 52, 37
+    frames = _frames(w, h, 18, 400 + window)
+    cs = ComputeState(True, window, 2.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+    ref = oracle.ComputeState(True, window, 2.0, 0, 0)
+    lib, hd = cs._hd._lib, cs._hd
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    try:
+        for t in range(18):
+            if t == 9:
+                hd.check(lib.dips_set_stream(hd.ptr, ctypes.c_void_p(int(s1.cuda_stream))))
+            cs.add_texture(w, h, frames[t])
+            ref.add_texture(w, h, frames[t])
+            if t == 12:
+                hd.check(lib.dips_set_stream(hd.ptr, ctypes.c_void_p(int(s2.cuda_stream))))
+            if t == 15:
+                hd.check(lib.dips_set_stream(hd.ptr, None))  # back to the handle's own stream
+            got, want = cs.dispatch(), ref.dispatch()
+            assert (got is None) == (want is None), t
+            if want is not None:
+                assert np.array_equal(got, want), (t, np.argwhere(got != want)[:4])
+    finally:
+        cs.close()
