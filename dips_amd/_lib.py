@@ -194,3 +194,24 @@ def check_alt(status: int, handle=None) -> int:
         msg = lib.dips_alt_last_error(handle)
         raise DipsError(status, msg.decode() if msg else "")
     return status
+
+
+class on_stream:
+    """Bind a handle to the caller's HIP stream for one call, then back to
+    the handle's own stream (``setter(ptr, NULL)``): the switch records an
+    event on the stream the handle was bound to, so a handle must never stay
+    bound to an external stream that may be destroyed before its next call.
+    ``setter`` is dips_set_stream or dips_alt_set_stream."""
+
+    def __init__(self, setter, ptr, check_fn, stream):
+        self.setter, self.ptr, self.check_fn, self.stream = setter, ptr, check_fn, stream
+
+    def __enter__(self):
+        self.check_fn(self.setter(self.ptr, ctypes.c_void_p(int(self.stream))))
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        st = self.setter(self.ptr, None)
+        if exc_type is None:
+            self.check_fn(st)
+        return False

@@ -206,13 +206,14 @@ class DiPsCompute:
         if stream is None:
             import torch
             stream = torch.cuda.current_stream(frames.device).cuda_stream
-        hd.check(hd._lib.dips_alt_set_stream(hd.ptr, ctypes.c_void_p(int(stream))))
         flags = None
         if snapshots is not None:
             flags = np.ascontiguousarray(np.asarray(snapshots, dtype=bool).astype(np.uint8))
-        hd.check(hd._lib.dips_alt_send_frames(hd.ptr, frames.data_ptr(), n,
-                                              flags.ctypes.data if flags is not None else None,
-                                              out.data_ptr()))
+        # bound to the caller's stream for this call only (_lib.on_stream)
+        with _lib.on_stream(hd._lib.dips_alt_set_stream, hd.ptr, hd.check, stream):
+            hd.check(hd._lib.dips_alt_send_frames(hd.ptr, frames.data_ptr(), n,
+                                                  flags.ctypes.data if flags is not None else None,
+                                                  out.data_ptr()))
 
     def kernel_time(self, reset: bool = False):
         hd = self._device_handle()

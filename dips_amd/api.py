@@ -168,6 +168,15 @@ class _Handle:
         return check(st, self._h)
 
 
+def _stream_of(hd: "_Handle", tensor, stream=None) -> "_lib.on_stream":
+    """`hd` bound to `stream` (default: the tensor's current stream) for one
+    call, then back to its own stream (see _lib.on_stream)."""
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream(tensor.device).cuda_stream
+    return _lib.on_stream(hd._lib.dips_set_stream, hd.ptr, hd.check, stream)
+
+
 def _as_u8(frame) -> np.ndarray:
     a = np.ascontiguousarray(frame)
     if a.dtype != np.uint8:
@@ -227,21 +236,17 @@ class ComputeState:
         for t in (frames, out):
             if not t.is_cuda or not t.is_contiguous():
                 raise ValueError("device path needs contiguous HIP tensors")
-        dv = self._device_handle(frames, stream)
-        dv.check(dv._lib.dips_frame_callback_batch(dv.ptr, w, h, frames.data_ptr(), n, out.data_ptr()))
+        dv = self._device_handle()
+        with _stream_of(dv, frames, stream):
+            dv.check(dv._lib.dips_frame_callback_batch(dv.ptr, w, h, frames.data_ptr(), n, out.data_ptr()))
 
-    def _device_handle(self, tensor, stream=None) -> "_Handle":
-        """The device-pointer twin handle (own ComputeState), bound to
-        `stream` (default: the tensor's current stream)."""
+    def _device_handle(self) -> "_Handle":
+        """The device-pointer twin handle (own ComputeState)."""
         if self._dev is None:
             p = DipsParams()
             ctypes.memmove(ctypes.byref(p), ctypes.byref(self._hd.params), ctypes.sizeof(p))
             p.flags |= _lib.FLAG_DEVICE_PTRS
             self._dev = _Handle(p, self._hd.device)
-        if stream is None:
-            import torch
-            stream = torch.cuda.current_stream(tensor.device).cuda_stream
-        self._dev.check(self._dev._lib.dips_set_stream(self._dev.ptr, ctypes.c_void_p(int(stream))))
         return self._dev
 
     # -- frame-range sharding (SURVEY.md s8e: 3-frame halo + start texture) --
@@ -265,14 +270,16 @@ class ComputeState:
         for t in (start, halo):
             if not t.is_cuda or not t.is_contiguous():
                 raise ValueError("device path needs contiguous HIP tensors")
-        dv = self._device_handle(start, stream)
-        dv.check(dv._lib.dips_compat_resume(dv.ptr, w, h, start.data_ptr(), halo.data_ptr(), int(t0)))
+        dv = self._device_handle()
+        with _stream_of(dv, start, stream):
+            dv.check(dv._lib.dips_compat_resume(dv.ptr, w, h, start.data_ptr(), halo.data_ptr(), int(t0)))
 
     def start_texture_device(self, out, stream=None) -> bool:
         """The device handle's start texture into a uint8 HIP tensor [H, W, 4]
         (asynchronous); False while it is not built yet."""
-        dv = self._device_handle(out, stream)
-        return dv.check(dv._lib.dips_start_texture(dv.ptr, out.data_ptr(), out.numel())) == 1
+        dv = self._device_handle()
+        with _stream_of(dv, out, stream):
+            return dv.check(dv._lib.dips_start_texture(dv.ptr, out.data_ptr(), out.numel())) == 1
 
     def kernel_time(self, reset: bool = False) -> Tuple[float, int]:
         """hipEvent time of the batch kernel on the device handle (time_kernel=True)."""
@@ -455,25 +462,19 @@ class DiffSeriesOperator:
         if map_out is not None and tuple(map_out.shape) != tuple(frames.shape):
             raise ValueError("map_out must have the shape of frames")
         lib = self._dev._lib
-        if stream is None:
-            import torch
-            stream = torch.cuda.current_stream(frames.device).cuda_stream
-        self._dev.check(lib.dips_set_stream(self._dev.ptr, ctypes.c_void_p(int(stream))))
-        self._dev.check(lib.dips_diff_series(
-            self._dev.ptr, w, h, frames.data_ptr(), n,
-            ref.data_ptr() if ref is not None else None, series_out.data_ptr(),
-            map_out.data_ptr() if map_out is not None else None))
+        with _stream_of(self._dev, frames, stream):
+            self._dev.check(lib.dips_diff_series(
+                self._dev.ptr, w, h, frames.data_ptr(), n,
+                ref.data_ptr() if ref is not None else None, series_out.data_ptr(),
+                map_out.data_ptr() if map_out is not None else None))
 
     def synth_device(self, dst, width: int, height: int, seed: int, t0: int, stream=None) -> None:
         """Fill a uint8 device tensor [N, H, W(, C)] with synthetic frames t0..t0+N-1."""
         n = dst.shape[0]
         lib = self._dev._lib
-        if stream is None:
-            import torch
-            stream = torch.cuda.current_stream(dst.device).cuda_stream
-        self._dev.check(lib.dips_set_stream(self._dev.ptr, ctypes.c_void_p(int(stream))))
-        self._dev.check(lib.dips_synth_frames(self._dev.ptr, width, height, int(seed), int(t0), n,
-                                              dst.data_ptr()))
+        with _stream_of(self._dev, dst, stream):
+            self._dev.check(lib.dips_synth_frames(self._dev.ptr, width, height, int(seed), int(t0), n,
+                                                  dst.data_ptr()))
 
     def read_ceiling_ms(self, tensor) -> float:
         """hipEvent time of one read-only stream over a device tensor's bytes."""

@@ -153,13 +153,21 @@ __attribute__((target("avx2"))) inline void stream_copy_avx2(uint8_t* d, const u
     _mm_sfence();
 }
 
-// The staging copy: streaming stores for pieces of >= 64 KiB on CPUs with
-// AVX2, memcpy otherwise.  DIPS_NT_COPY=0 selects memcpy (read per call, so
-// one process can A/B the two: tools/callback_rate.py).
-inline void host_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
-    static const bool avx2 = __builtin_cpu_supports("avx2");
+// Whether the staging copies use streaming stores: DIPS_NT_COPY=0 selects
+// memcpy.  Read on the CALLING thread once per operation (so one process can
+// A/B the two, tools/callback_rate.py) and handed to the pool's workers as a
+// value -- the workers never touch the environment, which another thread may
+// be changing (setenv is not safe beside a concurrent getenv).
+inline bool nt_copy() {
     const char* e = std::getenv("DIPS_NT_COPY");
-    if (avx2 && bytes >= (64u << 10) && !(e && e[0] == '0'))
+    return !(e && e[0] == '0');
+}
+
+// The staging copy: streaming stores for pieces of >= 64 KiB on CPUs with
+// AVX2 when `nt`, memcpy otherwise.
+inline void host_copy(uint8_t* dst, const uint8_t* src, size_t bytes, bool nt) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2 && nt && bytes >= (64u << 10))
         stream_copy_avx2(dst, src, bytes);
     else
         std::memcpy(dst, src, bytes);
@@ -168,14 +176,15 @@ inline void host_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
 // Host copy in ~4 MiB pieces over the pool.
 inline void pool_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
     const size_t kPiece = 4u << 20;
+    const bool nt = nt_copy();
     if (bytes < 2 * kPiece) {
-        host_copy(dst, src, bytes);
+        host_copy(dst, src, bytes, nt);
         return;
     }
     const size_t n = (bytes + kPiece - 1) / kPiece;
     CopyPool::global().run(n, [&](size_t i) {
         const size_t o = i * kPiece;
-        host_copy(dst + o, src + o, std::min(kPiece, bytes - o));
+        host_copy(dst + o, src + o, std::min(kPiece, bytes - o), nt);
     });
 }
 

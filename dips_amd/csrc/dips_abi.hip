@@ -1008,7 +1008,10 @@ dips_status dips_compat_resume(dips_handle* h, uint32_t width, uint32_t height, 
     if (!start_rgba || !halo || width == 0 || height == 0)
         return fail(h, DIPS_ERR_INVALID, "compat_resume: null or empty argument");
     if (t0 < 7) return fail(h, DIPS_ERR_INVALID, "compat_resume: t0 must be >= 7 (steady state of the ring)");
-    h->pending = false;  // a deferred frame's slot is rewritten below like every other
+    // a deferred frame's speculative kernels (odd stripes on copy_stream) must
+    // land before the slots are rewritten below on h->stream
+    st = flush_pending(h);
+    if (st != DIPS_OK) return st;
     const size_t fb = (size_t)width * height * 4u;
     const bool dev = (h->p.flags & DIPS_FLAG_DEVICE_PTRS) != 0;
     for (auto& sl : h->slots) DIPS_HIP(h, sl.ensure(fb));

@@ -83,12 +83,13 @@ inline size_t piece_bytes() {
 // soon as it is staged, so the host copy and the PCIe transfer overlap.
 // The caller makes sure no earlier transfer still reads `pin`.
 inline hipError_t upload_via(void* dev, const uint8_t* host, size_t bytes, uint8_t* pin, hipStream_t s) {
+    const bool nt = nt_copy();  // on the calling thread, never in the workers
     const size_t kPieceBytes = piece_bytes();
     const size_t n = (bytes + kPieceBytes - 1) / kPieceBytes;
     std::atomic<int> err{(int)hipSuccess};
     CopyPool::global().run(n, [&](size_t i) {
         const size_t o = i * kPieceBytes, len = std::min(kPieceBytes, bytes - o);
-        host_copy(pin + o, host + o, len);
+        host_copy(pin + o, host + o, len, nt);
         const hipError_t e = hipMemcpyAsync(static_cast<uint8_t*>(dev) + o, pin + o, len, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) err.store((int)e);
     });
@@ -119,6 +120,7 @@ struct PieceEvents {
 // the whole frame.
 inline hipError_t download_via(uint8_t* host, const void* dev, size_t bytes, uint8_t* pin, hipStream_t s,
                                PieceEvents& pe) {
+    const bool nt = nt_copy();  // on the calling thread, never in the workers
     const size_t kPieceBytes = piece_bytes();
     const size_t n = (bytes + kPieceBytes - 1) / kPieceBytes;
     hipError_t e = pe.ensure(n);
@@ -138,7 +140,7 @@ inline hipError_t download_via(uint8_t* host, const void* dev, size_t bytes, uin
             return;
         }
         const size_t o = i * kPieceBytes;
-        host_copy(host + o, pin + o, std::min(kPieceBytes, bytes - o));
+        host_copy(host + o, pin + o, std::min(kPieceBytes, bytes - o), nt);
     });
     return (hipError_t)err.load();
 }
@@ -154,6 +156,7 @@ template <typename Launch>
 hipError_t run_striped_frame(const uint8_t* frame, uint8_t* out, uint32_t height, size_t row, uint8_t* pin_in,
                              uint8_t* pin_out, uint8_t* dev_in, const uint8_t* dev_out, hipStream_t up,
                              hipStream_t compute, PieceEvents& up_ev, PieceEvents& down_ev, Launch&& launch) {
+    const bool nt = nt_copy();  // on the calling thread, never in the workers
     const size_t fb = row * height;
     const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
     const uint32_t n_s = (height + rows - 1) / rows;
@@ -171,7 +174,7 @@ hipError_t run_striped_frame(const uint8_t* frame, uint8_t* out, uint32_t height
     std::atomic<int> err{(int)hipSuccess};
     CopyPool::global().run(n_s, [&](size_t si) {
         const size_t o = si * rows * row, len = std::min<size_t>((size_t)rows * row, fb - o);
-        host_copy(pin_in + o, frame + o, len);
+        host_copy(pin_in + o, frame + o, len, nt);
         if (trace) ts[4 * si] = since();
         hipError_t r = hipMemcpyAsync(dev_in + o, pin_in + o, len, hipMemcpyHostToDevice, up);
         if (r == hipSuccess) r = hipEventRecord(up_ev.ev[si], up);
@@ -197,7 +200,7 @@ hipError_t run_striped_frame(const uint8_t* frame, uint8_t* out, uint32_t height
         }
         if (trace) ts[4 * si + 2] = since();
         const size_t o = si * rows * row;
-        host_copy(out + o, pin_out + o, std::min<size_t>((size_t)rows * row, fb - o));
+        host_copy(out + o, pin_out + o, std::min<size_t>((size_t)rows * row, fb - o), nt);
         if (trace) ts[4 * si + 3] = since();
     });
     if (trace) {
@@ -245,6 +248,7 @@ template <typename Launch>
 hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t height, size_t row,
                                     uint8_t* pin_in, const uint8_t* pin_out, const hipStream_t (&compute)[2],
                                     int device, PieceEvents& ev, Launch&& launch) {
+    const bool nt = nt_copy();  // on the calling thread, never in the workers
     const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
     const uint32_t first = std::min(height, direct_first_rows(rows));
     const uint32_t n_s = 1u + (height - first + rows - 1) / rows;
@@ -276,7 +280,7 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
         const size_t p1 = j + 1 == k ? slen : std::min(slen, (slen * (j + 1) / k) & ~(size_t)63);
         const size_t o = so + p0, len = p1 - p0;
         if (i < n_t) {
-            if (len && frame) host_copy(pin_in + o, frame + o, len);  // frame == nullptr: already staged
+            if (len && frame) host_copy(pin_in + o, frame + o, len, nt);  // frame == nullptr: already staged
             if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != k) return;
             // the stripe's last piece: its kernel and event back to back on the stream
             if (trace) ts[2 * si] = since();
@@ -301,7 +305,7 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
             err.store((int)r);
             return;
         }
-        if (len) host_copy(out + o, pin_out + o, len);
+        if (len) host_copy(out + o, pin_out + o, len, nt);
         if (trace) ts[2 * n_s + pi] = since();
     });
     if (trace) {
@@ -350,6 +354,7 @@ struct DirectGeom {
 template <typename Launch>
 hipError_t direct_stage_launch(const uint8_t* frame, uint8_t* pin_in, const hipStream_t (&compute)[2], int device,
                                PieceEvents& ev, const DirectGeom& g, Launch&& launch) {
+    const bool nt = nt_copy();  // on the calling thread, never in the workers
     hipError_t e = ev.ensure(g.n_s);
     if (e != hipSuccess) return e;
     std::unique_ptr<std::atomic<uint32_t>[]> staged(new std::atomic<uint32_t>[g.n_s]);
@@ -360,7 +365,7 @@ hipError_t direct_stage_launch(const uint8_t* frame, uint8_t* pin_in, const hipS
         const uint32_t si = (uint32_t)(i / g.k), j = (uint32_t)(i % g.k);
         size_t o, len;
         g.piece(si, j, o, len);
-        if (len) host_copy(pin_in + o, frame + o, len);
+        if (len) host_copy(pin_in + o, frame + o, len, nt);
         if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != g.k) return;
         std::lock_guard<std::mutex> lk(launch_mu);
         hipStream_t cs = compute[si & 1u];
@@ -375,6 +380,7 @@ hipError_t direct_stage_launch(const uint8_t* frame, uint8_t* pin_in, const hipS
 // Second half: the pool copies each stripe's pieces from `pin_out` to `out`
 // as soon as the stripe's event (recorded by direct_stage_launch) has fired.
 inline hipError_t direct_collect(uint8_t* out, const uint8_t* pin_out, PieceEvents& ev, const DirectGeom& g) {
+    const bool nt = nt_copy();  // on the calling thread, never in the workers
     std::atomic<int> err{(int)hipSuccess};
     CopyPool::global().run((size_t)g.n_s * g.k, [&](size_t i) {
         const uint32_t si = (uint32_t)(i / g.k), j = (uint32_t)(i % g.k);
@@ -385,7 +391,7 @@ inline hipError_t direct_collect(uint8_t* out, const uint8_t* pin_out, PieceEven
         }
         size_t o, len;
         g.piece(si, j, o, len);
-        if (len) host_copy(out + o, pin_out + o, len);
+        if (len) host_copy(out + o, pin_out + o, len, nt);
     });
     return (hipError_t)err.load();
 }

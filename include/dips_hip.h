@@ -109,7 +109,9 @@ const char *dips_last_error(const dips_handle *h);
  * Switching streams orders the new stream after all work already issued on
  * the previous one (the handle's device scratch serves both), so the previous
  * stream must still exist at the switch; setting the current stream again is
- * free. */
+ * free.  A caller that binds an external stream and may destroy it should
+ * switch back to NULL before doing so (the Python wrappers do this after
+ * every call: dips_amd._lib.on_stream). */
 dips_status dips_set_stream(dips_handle *h, void *stream);
 
 /* Block until all work issued through `h` has finished. */

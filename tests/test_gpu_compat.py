@@ -369,6 +369,31 @@ def test_resume_window_matches_continuous_run(window):
             b.close()
 
 
+@pytest.mark.parametrize("window", [1, 3])
+def test_resume_after_deferred_add_texture(monkeypatch, window):
+    """dips_compat_resume on a handle whose last call was a deferred
+    add_texture (W = 1: its speculative stripes still in flight on two
+    streams): resume waits for them before rewriting the ring, so the resumed
+    handle gives the outputs of a fresh resumed one."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
+    monkeypatch.setenv("DIPS_PIECE_BYTES", str(3 * 96 * 4 + 4))  # many stripes on both streams
+    w, h, n = 96, 64, 30
+    frames = _frames(w, h, n, 900 + window)
+    params = (True, window, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+    want = _oracle_callbacks(frames, (True, window, 5.0, 0, 0))
+    a = ComputeState(*params)
+    try:
+        assert np.array_equal(a.frame_callback_batch(w, h, frames[:12]), want[:12])
+        start = a.start_texture()
+        a.add_texture(w, h, frames[12])  # deferred: no dispatch follows
+        t0 = 17
+        a.resume(w, h, start, frames[t0 - 3:t0], t0)
+        got = np.stack([frame_callback(w, h, f, a) for f in frames[t0:]])
+        assert np.array_equal(got, want[t0:]), np.argwhere(got != want[t0:])[:4]
+    finally:
+        a.close()
+
+
 def test_resume_rejects_bad_arguments():
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter
     from dips_amd._lib import DipsError

@@ -73,7 +73,7 @@ int main() {
                 for (size_t dof = 0; dof < 40; dof += 13) {
                     if (so + n > src.size() || dof + n + 8 > dst.size()) continue;
                     std::fill(dst.begin(), dst.end(), 0xA5);
-                    dips_host::host_copy(dst.data() + dof, src.data() + so, n);
+                    dips_host::host_copy(dst.data() + dof, src.data() + so, n, dips_host::nt_copy());
                     for (size_t i = 0; i < dof; ++i) bad += dst[i] != 0xA5;
                     bad += std::memcmp(dst.data() + dof, src.data() + so, n) != 0;
                     for (size_t i = dof + n; i < dof + n + 8; ++i) bad += dst[i] != 0xA5;
