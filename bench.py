@@ -13,6 +13,19 @@ A step = one pass of the hot path over the rank's resident frame batch:
 series kernel + reduction (+ halo exchange + series gather when N > 1).
 Frames are generated into HBM by the shared integer generator before timing.
 
+After the timed steps, at every N (the driver's 8-GPU run included):
+  * "check": every rank re-derives its first series entries against the halo
+    / reference it received, rank 0 the gathered rows at every shard boundary
+    and 8 random frames (dips_amd.shard.verify_sharded_series); a mismatch
+    makes the process exit non-zero after printing the line;
+  * "configs3" / "configs4": BASELINE.json configs[3] ('overall', reference
+    broadcast, 5000 4K frames per GPU) and configs[4] (7680x4320, tau 8/255,
+    1250 frames per GPU) on the same ranks, regenerated into the same
+    resident buffer, each with frames/s, roofline fraction, RCCL times and
+    its own check;
+  * at N = 1 also "per_frame_call": the reference's own pattern, one 4K RGBA8
+    frame per dips_frame_callback from pageable host memory.
+
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE).
 Prints ONE JSON line on rank 0.
@@ -58,6 +71,15 @@ def parse():
                     help="frames of the map_variant launch (frames + maps stay resident beside the batch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU work of the cpu_baseline sample")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the self-check after the timed steps (profiling runs only: its small launches of "
+                         "the series kernel would mix into the kernel statistics)")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the configs[3] / configs[4] legs (profiling runs)")
+    ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of each configs[3] / configs[4] leg")
+    ap.add_argument("--no-per-frame-call", action="store_true", help="skip the per_frame_call leg")
+    ap.add_argument("--per-frame-calls", type=int, default=200,
+                    help="timed dips_frame_callback calls of the per_frame_call leg (4K RGBA8)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="HBM traffic per launch measured by profiles/collect_pmc.sh")
     return ap.parse_args()
@@ -82,7 +104,7 @@ def _time_oracle(lib, frames, mode, tau, threads, target_s, max_passes=400):
     return frames.shape[0] * passes / dt, passes, dt, out4
 
 
-def cpu_baseline(frames_dev, series_dev, mode: int, tau: float, target_s: float, op_gray=None):
+def cpu_baseline(frames_dev, series_dev, mode: int, tau: float, target_s: float, op_gray=None, pf_sample=None):
     """The oracle ('port' of the reference semantics; the reference itself has
     no CPU loop) timed on this host's cores on a bounded
     prefix of the same frames (per-frame cost is constant): all usable cores
@@ -149,6 +171,26 @@ def cpu_baseline(frames_dev, series_dev, mode: int, tau: float, target_s: float,
         res["config0"] = cfg0
     except Exception as e:  # report, never hide
         res["config0"] = {"failed": str(e)}
+    # the per-frame call pattern: the oracle's ComputeState frame_callback
+    # (one core) over the first frames of the per_frame_call leg; its outputs
+    # must equal the GPU's
+    if pf_sample is not None:
+        try:
+            frames_pf, want_pf = pf_sample
+            n_pf, h_pf, w_pf = frames_pf.shape[:3]
+            cs = oracle.ComputeState(False, 1, 5.0, 255, 0)
+            same = True
+            t = time.perf_counter()
+            for k in range(n_pf):
+                o = oracle.frame_callback(w_pf, h_pf, frames_pf[k], cs)
+                same = same and bool(np.array_equal(o, want_pf[k]))
+            dt = time.perf_counter() - t
+            res["per_frame_call"] = {"value": round(n_pf / dt, 3), "unit": "frames/s", "cores": 1,
+                                     "sample": f"frame_callback of the first {n_pf} 4K RGBA8 frames of the "
+                                               f"per_frame_call leg, {dt:.2f} s (oracle ComputeState)",
+                                     "outputs_equal_gpu": same}
+        except Exception as e:  # report, never hide
+            res["per_frame_call"] = {"failed": str(e)}
     return res
 
 
@@ -298,6 +340,173 @@ def _map_variant(torch, op_cls, frames, n, W, H, mode_pf, tau):
         op.close()
 
 
+def _devices(torch, dist, world, local):
+    """PCI bus id of every rank's GPU (all_gather), so the line proves which
+    devices ran."""
+    props = torch.cuda.get_device_properties(local)
+    mine = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}"
+    if world == 1:
+        return [mine]
+    out = [None] * world
+    dist.all_gather_object(out, mine)
+    return out
+
+
+def _max_over_ranks(torch, dist, world, dev, values):
+    t = torch.tensor(values, dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t]
+
+
+def _config_leg(torch, dist, buf, *, name, W, H, F, mode, tau, steps, world, rank, local, dev, check=True):
+    """One more BASELINE.json config on the same ranks and the same resident
+    buffer (regenerated in place, so HBM holds one batch at a time): 'overall'
+    mode, the reference broadcast once (RCCL), each step the series kernel
+    over the rank's F frames + one gather of the series; then the same
+    self-check as the headline.  Returns its frames/s, roofline fraction,
+    RCCL times and check."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat, shard
+    fb = W * H * 3
+    if F * fb > buf.numel():
+        raise ValueError("leg does not fit the resident buffer")
+    op = DiffSeriesOperator(PixelFormat.RGB8, mode, tau, time_kernel=True, device=local)
+    try:
+        frames = buf.view(-1)[: F * fb].view(F, H, W, 3)
+        op.synth_device(frames, W, H, SEED, rank * F)
+        series = torch.zeros((F, 4), dtype=torch.int64, device=dev)
+        ref = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
+        gather = shard.SeriesGather(world * F, dev)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t = time.perf_counter()
+        if mode == Mode.Overall:
+            if rank == 0:
+                ref.copy_(frames[0])
+            shard.broadcast_reference(ref)
+        torch.cuda.synchronize()
+        ref_ms = (time.perf_counter() - t) * 1e3
+
+        def compute():
+            if mode == Mode.Overall:
+                op.run_device(frames, series, ref=ref)
+            elif world == 1:
+                op.run_device(frames, series)
+            else:
+                shard.per_frame_overlapped(frames, ref, series, lambda fr, r, out: op.run_device(fr, out, ref=r))
+
+        compute()
+        gather(series)  # warm
+        torch.cuda.synchronize()
+        op.kernel_time(reset=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        final = None
+        for _ in range(steps):
+            compute()
+            final = gather(series)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t
+        kms, _ = op.kernel_time()
+        # the gather alone, once more (its share of a step)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        final = gather(series)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - t) * 1e3
+        elapsed, kms, gather_ms, ref_ms = _max_over_ranks(torch, dist, world, dev,
+                                                          [elapsed, kms / steps, gather_ms, ref_ms])
+        chk = None
+        if check:
+            chk = shard.verify_sharded_series(op, width=W, height=H, seed=SEED, n_total=world * F,
+                                              per_frame=(mode == Mode.PerFrame), local_series=series, ref=ref,
+                                              gathered=final, device=dev)
+            chk.pop("global_frames", None)
+        algo = F * fb
+        ach = algo / (kms / 1e3) / 1e9
+        return {"workload": name, "frames_per_gpu": F, "width": W, "height": H,
+                "mode": "overall" if mode == Mode.Overall else "per-frame", "tau": round(tau, 6),
+                "steps": steps, "frames_per_s": round(world * F * steps / elapsed, 2),
+                "ms_per_step": round(elapsed / steps * 1e3, 4),
+                "kernel_ms": round(kms, 4), "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                "rccl_gather_ms": round(gather_ms, 4) if world > 1 else 0.0,
+                "rccl_reference_ms": round(ref_ms, 4) if world > 1 else 0.0,
+                "kernel": f"series_v2_kernel<3,0,4,{'true' if mode == Mode.PerFrame else 'false'},false>",
+                "check": chk}
+    finally:
+        op.close()
+
+
+def _per_frame_call(torch, n_timed: int, warm: int = 8):
+    """The reference's own per-frame pattern (dips/src/frame_extractor.rs:
+    206-276 -> lib.rs:233-246 -> gpu/mod.rs:170-397): one 4K RGBA8 frame per
+    dips_frame_callback from pageable host memory, the output in host memory
+    when the call returns, DiPsProperties defaults (lib.rs:74-86).  Every
+    output is compared with the device batch path (frame_callback_batch over
+    the same frames in HBM; that path is oracle-tested), outside the timed
+    calls.  Returns the record and a small sample for the CPU baseline."""
+    from dips_amd import ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, PixelFormat
+    W, H = 3840, 2160
+    n = warm + n_timed
+    props = (False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
+    gen = DiffSeriesOperator(PixelFormat.RGBA8)
+    try:
+        dev = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+        gen.synth_device(dev, W, H, SEED ^ 0x4A, 0)
+    finally:
+        gen.close()
+    host = dev.cpu().numpy()
+    batch = ComputeState(*props)
+    try:
+        out_dev = torch.empty_like(dev)
+        batch.frame_callback_batch_device(dev, out_dev)
+        torch.cuda.synchronize()
+        want = out_dev.cpu().numpy()
+        del out_dev
+    finally:
+        batch.close()
+    del dev
+    torch.cuda.empty_cache()
+    cs = ComputeState(*props)
+    lib, hd = cs._hd._lib, cs._hd
+    out = np.empty((H, W, 4), dtype=np.uint8)
+    out.fill(0)  # faulted in before the timed calls
+    times, equal = [], True
+    try:
+        for t in range(n):
+            t0 = time.perf_counter()
+            hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
+                                             out.ctypes.data, out.nbytes))
+            dt = time.perf_counter() - t0
+            if t >= warm:
+                times.append(dt)
+            equal = equal and bool(np.array_equal(out, want[t]))
+    finally:
+        cs.close()
+    fb = W * H * 4
+    tot = float(np.sum(times))
+    rec = {"frames_per_s": round(n_timed / tot, 1), "calls": n_timed,
+           "ms_per_call_median": round(float(np.median(times)) * 1e3, 4),
+           "ms_per_call_p90": round(float(np.percentile(times, 90)) * 1e3, 4),
+           "host_to_device_GBps": round(n_timed * fb / tot / 1e9, 2),
+           "device_to_host_GBps": round(n_timed * fb / tot / 1e9, 2),
+           "outputs_equal_batch_path": equal,
+           "workload": "3840x2160 RGBA8, DiPsProperties defaults (Unfiltered, window 1, no colour); "
+                       f"{warm} untimed calls, then {n_timed} timed dips_frame_callback calls from pageable "
+                       "host memory into a reused host output buffer",
+           "path": "zero-copy stripes: the copy pool stages each row stripe into pinned memory and launches "
+                   "compat_main_host_kernel on it (PCIe reads + writes by the kernel), stripes copied out as "
+                   "their events fire (dips_abi.hip frame_callback_striped)"}
+    return rec, (host[:warm].copy(), want[:warm].copy())
+
+
 def main():
     args = parse()
     import torch
@@ -389,14 +598,29 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     elapsed_max, kernel_ms = float(tt[0]), float(tt[1])
 
+    devices = _devices(torch, dist, world, local)
+    # Self-check of the timed step at every world size (collective): each
+    # rank re-derives its first entries against the halo / reference it
+    # received, rank 0 re-derives the gathered rows at every shard boundary
+    # and 8 random frames (dips_amd.shard.verify_sharded_series)
+    check = None
+    if not args.no_check:
+        check = shard.verify_sharded_series(op, width=W, height=H, seed=SEED, n_total=world * F,
+                                            per_frame=(mode == Mode.PerFrame), local_series=series, ref=ref,
+                                            gathered=final, device=dev)
+        picks = check.pop("global_frames")
+        log(f"check: {check['frames_checked']} frames re-derived (global {picks[:12]}...), equal={check['equal']}")
+    waves, tiles, pbytes = op.geometry(W, H, F)
+    algo_bytes = F * fb  # each frame read once per launch
+    achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
+    value = world * F * args.steps / elapsed_max
+
+    pcie = mapv = cpu = pfc = None
     if rank == 0:
-        # validity: the gathered series must be the series of frames 0..N*F-1
-        final = final.cpu().numpy().view(np.uint64)
-        assert final.shape == (world * F, 4)
-        if mode == Mode.PerFrame:
-            assert final[0].sum() == 0  # frame 0 against itself
+        final_np = final.cpu().numpy().view(np.uint64)
+        assert final_np.shape == (world * F, 4)
         if args.check and world * F * fb > (64 << 30):
-            log("check skipped: the N*F frames would not fit beside the resident batch (small sizes only)")
+            log("--check skipped: the N*F frames would not fit beside the resident batch (small sizes only)")
         elif args.check:
             # the same N*F frames in one launch on one device (small sizes only)
             allf = torch.empty((world * F, H, W, C), dtype=torch.uint8, device=dev)
@@ -404,36 +628,14 @@ def main():
             one = torch.zeros((world * F, 4), dtype=torch.int64, device=dev)
             op.run_device(allf, one, ref=None if mode == Mode.PerFrame else allf[0])
             torch.cuda.synchronize()
-            assert np.array_equal(final, one.cpu().numpy().view(np.uint64)), "gathered series != single-device series"
-            log(f"check: gathered series of {world}x{F} frames equals the single-device series")
+            assert np.array_equal(final_np, one.cpu().numpy().view(np.uint64)), "gathered series != single-device series"
+            log(f"--check: gathered series of {world}x{F} frames equals the single-device series")
             del allf, one
-        waves, tiles, pbytes = op.geometry(W, H, F)
-        algo_bytes = F * fb  # each frame read once per launch
-        achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
-        traffic = None
-        pmc_note = None
-        lib_sha = _lib_sha256()
-        if os.path.exists(args.pmc_json):
-            try:
-                with open(args.pmc_json) as f:
-                    pmc = json.load(f)
-                same_run = (pmc.get("width"), pmc.get("height"), pmc.get("frames"), pmc.get("mode")) == (W, H, F, args.mode)
-                if same_run and pmc.get("lib_sha256") == lib_sha:
-                    traffic = pmc.get("hbm_bytes_per_launch")
-                    pmc_note = pmc.get("source")
-                else:
-                    pmc_note = ("traffic null: profiles/pmc_traffic.json was collected with another build of "
-                                "libdips_hip.so or another workload")
-            except Exception:
-                traffic = None
-        value = world * F * args.steps / elapsed_max
+    if world == 1:
         # PCIe-inclusive rate, reported beside (never as) `value` (BASELINE.md:
         # "the H2D end-to-end rate separately"): the first 96 frames copied to
         # pageable host memory and fed back through dips_diff_series_streamed
-        pcie = None
         try:
-            if world > 1:
-                raise RuntimeError("measured at N = 1 only")
             if args.no_pcie:
                 raise RuntimeError("--no-pcie")
             nh = min(F, 96)
@@ -450,21 +652,75 @@ def main():
             del host
         except Exception as e:  # report, never hide
             pcie = {"skipped": str(e)}
-        mapv = None
-        if world == 1 and not args.no_map:
+        if not args.no_map:
             try:
                 mapv = _map_variant(torch, DiffSeriesOperator, frames, min(F, args.map_frames), W, H,
                                     mode == Mode.PerFrame, args.tau)
             except Exception as e:  # report, never hide
                 mapv = {"skipped": str(e)}
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        pf_sample = None
+        if not args.no_per_frame_call:
+            try:
+                pfc, pf_sample = _per_frame_call(torch, args.per_frame_calls)
+                log(f"per_frame_call: {pfc['frames_per_s']} frames/s, outputs equal: {pfc['outputs_equal_batch_path']}")
+            except Exception as e:  # report, never hide
+                pfc = {"skipped": str(e)}
+        if not args.no_cpu_baseline:
             try:
                 cpu = cpu_baseline(frames, series, int(mode), args.tau, args.cpu_seconds,
-                                   op_gray=lambda fr, want: _config0_gpu(torch, fr, want))
+                                   op_gray=lambda fr, want: _config0_gpu(torch, fr, want), pf_sample=pf_sample)
             except Exception as e:  # report, never hide
                 cpu = {"value": None, "unit": "frames/s", "cores": 0, "kind": "port",
                        "sample": f"failed: {e}"}
+            pf_sample = None
+
+    # configs[3] and configs[4] on the same ranks, regenerated into the same
+    # resident buffer (collective at N > 1)
+    legs = {}
+    if not args.no_legs:
+        op.close()
+        op = None
+        del series
+        buf = frames
+        del frames
+        W8, H8 = 2 * W, 2 * H
+        for key, name, lw, lh, lf in (
+                ("configs3", "BASELINE.json configs[3]: 3840x2160 RGB8, 'overall', reference broadcast, "
+                             f"{F} frames per GPU", W, H, F),
+                ("configs4", "BASELINE.json configs[4]: 7680x4320 RGB8, 'overall', f32 intensity with threshold "
+                             f"tau={args.tau:.6g}, {(F * fb) // (W8 * H8 * 3)} frames per GPU", W8, H8,
+                 (F * fb) // (W8 * H8 * 3))):
+            try:
+                if lf < 2:
+                    raise ValueError("fewer than 2 frames per GPU at this size")
+                legs[key] = _config_leg(torch, dist, buf, name=name, W=lw, H=lh, F=lf, mode=Mode.Overall,
+                                        tau=args.tau, steps=args.leg_steps, world=world, rank=rank, local=local,
+                                        dev=dev, check=not args.no_check)
+                log(f"{key}: {legs[key]['frames_per_s']} frames/s, frac {legs[key]['frac']}, "
+                    f"check {legs[key]['check']}")
+            except Exception as e:  # report, never hide
+                legs[key] = {"failed": f"{type(e).__name__}: {e}"}
+        del buf
+
+    ok = all(c is None or c.get("equal") for c in [check] + [l.get("check") for l in legs.values()])
+    ok = ok and all("failed" not in l for l in legs.values())
+    if rank == 0:
+        traffic = None
+        pmc_note = None
+        lib_sha = _lib_sha256()
+        if os.path.exists(args.pmc_json):
+            try:
+                with open(args.pmc_json) as f:
+                    pmc = json.load(f)
+                same_run = (pmc.get("width"), pmc.get("height"), pmc.get("frames"), pmc.get("mode")) == (W, H, F, args.mode)
+                if same_run and pmc.get("lib_sha256") == lib_sha:
+                    traffic = pmc.get("hbm_bytes_per_launch")
+                    pmc_note = pmc.get("source")
+                else:
+                    pmc_note = ("traffic null: profiles/pmc_traffic.json was collected with another build of "
+                                "libdips_hip.so or another workload")
+            except Exception:
+                traffic = None
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -484,6 +740,9 @@ def main():
                 "frames_per_gpu": F, "width": W, "height": H, "mode": args.mode,
                 "parallelism": f"frame-range x{world}" + (" + RCCL halo send/recv + gather" if world > 1 else ""),
             },
+            "ranks": world,
+            "devices": devices,
+            "check": check,
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -518,11 +777,17 @@ def main():
             "power": power,
             "pcie_inclusive": pcie,
             "map_variant": mapv,
+            "per_frame_call": pfc,
+            **legs,
         }
         print(json.dumps(out), flush=True)
-    op.close()
+    if op is not None:
+        op.close()
     if world > 1:
         dist.destroy_process_group()
+    if not ok:
+        log("FAILED: a self-check of the sharded series did not match (see 'check' in the JSON line)")
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -123,6 +123,117 @@ class SeriesGather:
         return torch.cat([buf[: e - s] for buf, (s, e) in zip(self.recv, self.ranges)], dim=0)
 
 
+def _comm_device(device: torch.device, group=None) -> torch.device:
+    """Where collective tensors live: the GPU under RCCL ("nccl"), the host
+    under gloo."""
+    if dist.is_initialized() and dist.get_backend(group) == "nccl":
+        return device
+    return torch.device("cpu")
+
+
+def check_frames(n_total: int, world: int, n_random: int = 8, seed: int = 0x5EED) -> List[int]:
+    """Global frames rank 0 re-derives after a sharded step: the first and
+    last frame, both sides of every shard boundary (k*F-1, k*F, k*F+1) and
+    `n_random` frames drawn with a fixed seed."""
+    import numpy as np
+    picks = {0, n_total - 1}
+    for s, _ in frame_ranges(n_total, world)[1:]:
+        picks.update((s - 1, s, s + 1))
+    if n_total > 0:
+        picks.update(int(g) for g in np.random.default_rng(seed).integers(0, n_total, n_random))
+    return sorted(g for g in picks if 0 <= g < n_total)
+
+
+def verify_sharded_series(op, *, width: int, height: int, seed: int, n_total: int, per_frame: bool,
+                          local_series: torch.Tensor, ref: Optional[torch.Tensor],
+                          gathered: Optional[torch.Tensor], device: torch.device,
+                          n_random: int = 8, group=None) -> dict:
+    """Self-check of one sharded step over frames the shared generator makes
+    (op.synth_device), run after the timed steps at any world size.
+
+    * every rank regenerates its first two frames (and, per-frame, the frame
+      before them) and requires its own first two series entries to match a
+      fresh launch: entry 0 against the received halo ('per-frame', rank > 0)
+      or the broadcast reference ('overall'), whose bytes must also equal the
+      regenerated frame -- this is what tests the RCCL halo / broadcast;
+    * rank 0 regenerates every global frame of check_frames() with its
+      reference and requires the gathered series rows to match -- this tests
+      the gather's ordering and padding.
+
+    `op` is a DiffSeriesOperator of the batch's format, mode and tau; `ref`
+    is the halo ('per-frame') or the reference ('overall') the step used.
+    Returns the same {"frames_checked", "equal", "local_equal",
+    "gathered_equal"} on every rank."""
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    s, e = frame_range(n_total, world, rank)
+    n = e - s
+    c = int(op.fmt)
+    shape = (height, width) if c == 1 else (height, width, c)
+
+    def synth(t0: int, count: int) -> torch.Tensor:
+        buf = torch.empty((count,) + shape, dtype=torch.uint8, device=device)
+        op.synth_device(buf, width, height, seed, t0)
+        return buf
+
+    def series_of(frames: torch.Tensor, r: Optional[torch.Tensor]) -> torch.Tensor:
+        out = torch.zeros((frames.shape[0], SERIES_COLS), dtype=torch.int64, device=device)
+        op.run_device(frames, out, ref=r)
+        return out
+
+    # -- local: this rank's first entries and the reference it received ------
+    local_ok = True
+    k = min(n, 2)
+    if k > 0:
+        mine = local_series[:k].to(device)
+        if per_frame:
+            if s > 0:
+                buf = synth(s - 1, k + 1)
+                want = series_of(buf, None)[1:]
+                local_ok = ref is not None and torch.equal(ref.to(device).reshape(shape), buf[0])
+            else:
+                want = series_of(synth(0, k), None)
+        else:
+            frame0 = synth(0, 1)[0]
+            local_ok = ref is not None and torch.equal(ref.to(device).reshape(shape), frame0)
+            want = series_of(synth(s, k), frame0)
+        local_ok = bool(local_ok) and bool(torch.equal(mine, want))
+    cdev = _comm_device(device, group)
+    # [ranks that failed, frames checked], summed over ranks
+    flag = torch.tensor([0 if local_ok else 1, k], dtype=torch.int64, device=cdev)
+    if world > 1:
+        dist.all_reduce(flag, group=group)
+    all_local_ok = int(flag[0]) == 0
+
+    # -- global: rank 0 re-derives boundary and random rows of the gather -----
+    picks = check_frames(n_total, world, n_random)
+    res = torch.tensor([0, len(picks)], dtype=torch.int64, device=cdev)
+    if rank == 0:
+        got = gathered.to(device)[picks] if gathered is not None and gathered.shape[0] == n_total else None
+        if per_frame:
+            # pairs (g-1, g) in one per-frame launch: the entry at 2i+1 is g's
+            buf = torch.empty((2 * len(picks),) + shape, dtype=torch.uint8, device=device)
+            for i, g in enumerate(picks):
+                if g == 0:  # frame 0 against itself
+                    op.synth_device(buf[2 * i:2 * i + 1], width, height, seed, 0)
+                    op.synth_device(buf[2 * i + 1:2 * i + 2], width, height, seed, 0)
+                else:
+                    op.synth_device(buf[2 * i:2 * i + 2], width, height, seed, g - 1)
+            want = series_of(buf, None)[1::2]
+        else:
+            buf = torch.empty((len(picks),) + shape, dtype=torch.uint8, device=device)
+            for i, g in enumerate(picks):
+                op.synth_device(buf[i:i + 1], width, height, seed, g)
+            want = series_of(buf, synth(0, 1)[0])
+        res[0] = 1 if got is not None and torch.equal(got, want) else 0
+        del buf
+    if world > 1:
+        dist.broadcast(res, src=0, group=group)
+    gathered_ok = bool(int(res[0]) == 1)
+    return {"frames_checked": int(res[1]) + int(flag[1]), "equal": all_local_ok and gathered_ok,
+            "local_equal": all_local_ok, "gathered_equal": gathered_ok, "global_frames": picks}
+
+
 # ---------------------------------------------------------------------------
 # dips-compat ComputeState over frame ranges (SURVEY.md s8e: "dips-compat T=4
 # needs a 3-frame halo").  Output frame t depends on the start texture S

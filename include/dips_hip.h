@@ -92,6 +92,29 @@ typedef struct dips_series_entry {
 
 typedef struct dips_handle dips_handle;
 
+/* Layouts pinned for foreign bindings: the Rust crate rust/dips-hip
+ * (src/ffi.rs) asserts the same sizes and offsets on its #[repr(C)] twins. */
+#ifdef __cplusplus
+#define DIPS_LAYOUT_ASSERT(cond, msg) static_assert(cond, msg)
+#else
+#define DIPS_LAYOUT_ASSERT(cond, msg) _Static_assert(cond, msg)
+#endif
+DIPS_LAYOUT_ASSERT(sizeof(dips_params) == 36, "dips_params size");
+DIPS_LAYOUT_ASSERT(offsetof(dips_params, colorize) == 0, "dips_params.colorize");
+DIPS_LAYOUT_ASSERT(offsetof(dips_params, spatial_window_size) == 4, "dips_params.spatial_window_size");
+DIPS_LAYOUT_ASSERT(offsetof(dips_params, sensitivity) == 8, "dips_params.sensitivity");
+DIPS_LAYOUT_ASSERT(offsetof(dips_params, filter_type) == 12, "dips_params.filter_type");
+DIPS_LAYOUT_ASSERT(offsetof(dips_params, chroma_filter) == 16, "dips_params.chroma_filter");
+DIPS_LAYOUT_ASSERT(offsetof(dips_params, mode) == 20, "dips_params.mode");
+DIPS_LAYOUT_ASSERT(offsetof(dips_params, format) == 24, "dips_params.format");
+DIPS_LAYOUT_ASSERT(offsetof(dips_params, tau) == 28, "dips_params.tau");
+DIPS_LAYOUT_ASSERT(offsetof(dips_params, flags) == 32, "dips_params.flags");
+DIPS_LAYOUT_ASSERT(sizeof(dips_series_entry) == 32, "dips_series_entry size");
+DIPS_LAYOUT_ASSERT(offsetof(dips_series_entry, sad) == 0, "dips_series_entry.sad");
+DIPS_LAYOUT_ASSERT(offsetof(dips_series_entry, sj) == 8, "dips_series_entry.sj");
+DIPS_LAYOUT_ASSERT(offsetof(dips_series_entry, count) == 16, "dips_series_entry.count");
+DIPS_LAYOUT_ASSERT(offsetof(dips_series_entry, si_fixed) == 24, "dips_series_entry.si_fixed");
+
 /* Fill `p` with DiPsProperties::new() defaults (dips/src/lib.rs:74-86). */
 dips_status dips_params_default(dips_params *p);
 
@@ -257,6 +280,16 @@ typedef struct dips_alt_params {
 } dips_alt_params;
 
 typedef struct dips_alt_handle dips_alt_handle;
+
+DIPS_LAYOUT_ASSERT(sizeof(dips_alt_params) == 28, "dips_alt_params size");
+DIPS_LAYOUT_ASSERT(offsetof(dips_alt_params, colorize) == 0, "dips_alt_params.colorize");
+DIPS_LAYOUT_ASSERT(offsetof(dips_alt_params, window_size) == 4, "dips_alt_params.window_size");
+DIPS_LAYOUT_ASSERT(offsetof(dips_alt_params, sigmoid_horizontal_scalar) == 8,
+                   "dips_alt_params.sigmoid_horizontal_scalar");
+DIPS_LAYOUT_ASSERT(offsetof(dips_alt_params, filter_type) == 12, "dips_alt_params.filter_type");
+DIPS_LAYOUT_ASSERT(offsetof(dips_alt_params, chroma_filter) == 16, "dips_alt_params.chroma_filter");
+DIPS_LAYOUT_ASSERT(offsetof(dips_alt_params, num_textures) == 20, "dips_alt_params.num_textures");
+DIPS_LAYOUT_ASSERT(offsetof(dips_alt_params, flags) == 24, "dips_alt_params.flags");
 
 /* Fill `p` with DiPsProperties::default() (mod.rs:176-186), num_textures 2. */
 dips_status dips_alt_params_default(dips_alt_params *p);

@@ -262,3 +262,101 @@ def test_compat_sharded_bad_layout_fails_on_every_rank(world, n_total):
     assert [r for r, _ in got] == list(range(world))
     msgs = {m for _, m in got}
     assert len(msgs) == 1 and "frame >= 7" in msgs.pop()
+
+
+class _OracleOp:
+    """CPU stand-in for DiffSeriesOperator's device calls (test seam for
+    shard.verify_sharded_series): synth_device / run_device on host tensors
+    through the oracle."""
+
+    def __init__(self, mode, tau, channels=3):
+        from dips_amd import PixelFormat
+        self.fmt = PixelFormat(channels)
+        self.mode, self.tau = mode, tau
+
+    def synth_device(self, dst, width, height, seed, t0):
+        from oracle import oracle
+        dst.copy_(torch.from_numpy(oracle.synth(int(self.fmt), width, height, seed, t0, dst.shape[0])))
+
+    def run_device(self, frames, out, ref=None):
+        from oracle import oracle
+        out4, _, _ = oracle.series(frames.numpy(), mode=self.mode, tau=self.tau,
+                                   ref=ref.numpy() if ref is not None else None)
+        out.copy_(torch.from_numpy(out4.view(np.int64)))
+
+
+def _verify_worker(rank, world, port, n_total, mode, corrupt, result_q):
+    """bench.py's N > 1 step (broadcast or overlapped halo + one gather) then
+    its self-check; `corrupt` damages one exchange on purpose."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        W, H, SEED, tau = 32, 16, 5, 2 / 255
+        op = _OracleOp(mode, tau)
+        s, e = shard.frame_range(n_total, world, rank)
+        local = torch.empty((e - s, H, W, 3), dtype=torch.uint8)
+        op.synth_device(local, W, H, SEED, s)
+        ref = torch.empty_like(local[0])
+        series = torch.zeros((e - s, shard.SERIES_COLS), dtype=torch.int64)
+
+        def compute(fr, r, out):
+            if corrupt == "halo" and rank == 1 and r is not None and fr.shape[0] == 1:
+                r[3, 5, 1] ^= 0x5A  # the received halo damaged before frame 0 uses it
+            op.run_device(fr, out, ref=r)
+
+        if mode == 0:
+            if rank == 0:
+                ref.copy_(local[0])
+            shard.broadcast_reference(ref)
+            if corrupt == "ref" and rank == world - 1:
+                ref[0, 0, 0] ^= 0x01
+            compute(local, ref, series)
+        else:
+            shard.per_frame_overlapped(local, ref, series, compute)
+        full = shard.SeriesGather(n_total, torch.device("cpu"))(series)
+        if corrupt == "gather" and rank == 0:
+            b = shard.frame_range(n_total, world, 1)[0]
+            full = full.clone()
+            full[[b - 1, b]] = full[[b, b - 1]]  # two rows of a boundary swapped
+        chk = shard.verify_sharded_series(op, width=W, height=H, seed=SEED, n_total=n_total,
+                                          per_frame=(mode == 1), local_series=series, ref=ref,
+                                          gathered=full, device=torch.device("cpu"))
+        result_q.put((rank, chk))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total,mode,corrupt", [
+    (2, 9, 1, None), (3, 14, 1, None), (2, 9, 0, None), (3, 14, 0, None),
+    (2, 9, 1, "halo"), (3, 14, 1, "gather"), (3, 14, 0, "ref"), (2, 9, 0, "gather")])
+def test_verify_sharded_series(world, n_total, mode, corrupt):
+    """bench.py's N > 1 self-check passes on a correct sharded step and
+    fails, on every rank, when the halo, the broadcast reference or the
+    gather is damaged."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_verify_worker, args=(r, world, port, n_total, mode, corrupt, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r for r, _ in got] == list(range(world))
+    for _, chk in got:
+        assert chk["equal"] is (corrupt is None), chk
+        assert chk["frames_checked"] >= len(shard.check_frames(n_total, world))
+    if corrupt in ("halo", "ref"):
+        assert not got[0][1]["local_equal"]
+    if corrupt == "gather":
+        assert got[0][1]["local_equal"] and not got[0][1]["gathered_equal"]
+
+
+def test_check_frames_cover_boundaries():
+    picks = shard.check_frames(40000, 8)
+    for s, _ in shard.frame_ranges(40000, 8)[1:]:
+        assert {s - 1, s, s + 1} <= set(picks)
+    assert 0 in picks and 39999 in picks and len(picks) >= 2 + 21

@@ -108,3 +108,74 @@ def test_sharded_hip_equals_single_launch(mode, overlapped):
     assert got.shape == want.shape
     assert np.array_equal(got, want)
     assert want[:, 0].any()  # non-trivial series
+
+
+def _verify_worker(rank, world, port, n_total, mode, corrupt, result_q):
+    """The bench's N > 1 step with the HIP operator, then its self-check
+    (shard.verify_sharded_series) with the HIP operator regenerating frames
+    on the device; `corrupt` = "halo" damages rank 1's received halo."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["DIPS_SERIES_WAVES_PER_SIMD"] = "4"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    op = None
+    try:
+        from dips_amd import DiffSeriesOperator, Mode, PixelFormat, shard
+        torch.cuda.set_device(0)
+        s, e = shard.frame_range(n_total, world, rank)
+        op = DiffSeriesOperator(PixelFormat.RGB8, Mode(mode), TAU)
+        dev = torch.empty((e - s, H, W, 3), dtype=torch.uint8, device="cuda")
+        op.synth_device(dev, W, H, SEED, s)
+        torch.cuda.synchronize()
+        local = dev.cpu()
+        hip = _hip_compute(op)
+
+        def compute(fr, r, out):
+            if corrupt == "halo" and rank == 1 and r is not None and fr.shape[0] == 1:
+                r[7, 9, 2] ^= 0x33
+            hip(fr, r, out)
+
+        ref = torch.empty_like(local[0])
+        series = torch.zeros((e - s, shard.SERIES_COLS), dtype=torch.int64)
+        if mode == 0:
+            if rank == 0:
+                ref.copy_(local[0])
+            shard.broadcast_reference(ref)
+            compute(local, ref, series)
+        else:
+            shard.per_frame_overlapped(local, ref, series, compute)
+        full = shard.SeriesGather(n_total, torch.device("cpu"))(series)
+        chk = shard.verify_sharded_series(op, width=W, height=H, seed=SEED, n_total=n_total,
+                                          per_frame=(mode == 1), local_series=series, ref=ref,
+                                          gathered=full, device=torch.device("cuda", 0))
+        torch.cuda.synchronize()
+        result_q.put((rank, chk))
+    finally:
+        if op is not None:
+            op.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,corrupt", [(1, None), (0, None), (1, "halo")])
+def test_bench_self_check(mode, corrupt):
+    """bench.py's N > 1 self-check with the HIP operator in two processes:
+    equal on a correct step, not equal on every rank when the halo is
+    damaged."""
+    from dips_amd import shard
+    world, n_total = 2, 29
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_verify_worker, args=(r, world, port, n_total, mode, corrupt, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = sorted(q.get(timeout=300) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    for _, chk in got:
+        assert chk["equal"] is (corrupt is None), chk
+        assert chk["frames_checked"] >= len(shard.check_frames(n_total, world))

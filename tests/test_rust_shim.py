@@ -1,0 +1,198 @@
+"""CPU checks of the Rust binding crate rust/dips-hip against the C ABI it
+binds (no Rust toolchain in this image, so the crate is checked as source):
+
+* every #[repr(C)] struct of src/ffi.rs has the header struct's fields, in
+  order, with the mapped types;
+* every function include/dips_hip.h declares is declared in the extern block
+  with the same parameter and return types (and nothing else is);
+* the sizes / offsets the Rust `const` asserts pin equal the ones gcc
+  computes for the C structs, and the header's own DIPS_LAYOUT_ASSERTs hold
+  under C99 and C++17.
+
+Reference items replaced: dips/src/gpu/mod.rs:59-65, :170, :306 and
+dips/src/lib.rs:23, :32-61 (ComputeState, CallbackFunction, the filter codes)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dips_hip.h")
+CRATE = os.path.join(ROOT, "rust", "dips-hip")
+FFI = os.path.join(CRATE, "src", "ffi.rs")
+
+STRUCTS = {"dips_params": "DipsParams", "dips_series_entry": "DipsSeriesEntry", "dips_alt_params": "DipsAltParams"}
+BASE = {"uint8_t": "u8", "uint16_t": "u16", "int32_t": "i32", "uint32_t": "u32", "uint64_t": "u64",
+        "float": "f32", "double": "f64", "size_t": "usize", "int": "c_int", "void": "c_void", "char": "c_char",
+        "dips_status": "DipsStatus", "dips_handle": "DipsHandle", "dips_alt_handle": "DipsAltHandle",
+        **STRUCTS}
+
+
+def _strip_c_comments(s):
+    s = re.sub(r"/\*.*?\*/", " ", s, flags=re.S)
+    return re.sub(r"//[^\n]*", " ", s)
+
+
+def _c_to_rust(decl):
+    """'const uint8_t *frame' -> '*const u8' (the name dropped)."""
+    decl = decl.strip()
+    stars = decl.count("*")
+    toks = decl.replace("*", " ").split()
+    const = "const" in toks
+    toks = [t for t in toks if t != "const"]
+    base = BASE[toks[0]]
+    if stars == 0:
+        return base
+    inner = base
+    for level in range(stars):
+        # the innermost pointer carries the const of the pointee
+        inner = f"*{'const' if const and level == 0 else 'mut'} {inner}"
+    return inner
+
+
+def _c_ret(ret):
+    ret = ret.strip()
+    if ret == "void":
+        return None
+    return _c_to_rust(ret)
+
+
+def header_structs():
+    src = _strip_c_comments(open(HEADER).read())
+    out = {}
+    for name in STRUCTS:
+        m = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), src, flags=re.S)
+        assert m, name
+        fields = []
+        for line in m.group(1).split(";"):
+            line = line.strip()
+            if line:
+                *ty, field = line.split()
+                fields.append((field, BASE[" ".join(ty)]))
+        out[name] = fields
+    return out
+
+
+def header_functions():
+    src = _strip_c_comments(open(HEADER).read())
+    src = re.sub(r"\s+", " ", src)
+    out = {}
+    for m in re.finditer(r"([A-Za-z_][A-Za-z_0-9 ]*?)\s*(\*?)\s*\b(dips_\w+)\(([^)]*)\);", src):
+        ret, star, name, args = m.group(1), m.group(2), m.group(3), m.group(4)
+        ret = (ret + " " + star).strip()
+        params = [] if args.strip() in ("", "void") else [_c_to_rust(a) for a in args.split(",")]
+        out[name] = (_c_ret(ret), params)
+    return out
+
+
+def rust_structs():
+    src = open(FFI).read()
+    out = {}
+    for m in re.finditer(r"#\[repr\(C\)\]\s*(?:#\[derive[^\]]*\]\s*)?pub struct (\w+) \{(.*?)\}", src, flags=re.S):
+        fields = re.findall(r"pub (\w+): ([^,]+),", m.group(2))
+        out[m.group(1)] = [(f, t.strip()) for f, t in fields]
+    return out
+
+
+def _norm(t):
+    return re.sub(r"\s+", " ", t.strip()) if t else None
+
+
+def rust_functions():
+    src = open(FFI).read()
+    block = src[src.index('extern "C" {'):]
+    block = re.sub(r"//[^\n]*", " ", block)
+    out = {}
+    for m in re.finditer(r"pub fn (\w+)\((.*?)\)\s*(?:->\s*([^;]+))?;", block, flags=re.S):
+        params = [p.split(":", 1)[1] for p in m.group(2).split(",") if p.strip()]
+        out[m.group(1)] = (_norm(m.group(3)), [_norm(p) for p in params])
+    return out
+
+
+def test_structs_match_header():
+    h, r = header_structs(), rust_structs()
+    for c_name, r_name in STRUCTS.items():
+        assert r[r_name] == h[c_name], (c_name, r[r_name], h[c_name])
+
+
+def test_functions_match_header():
+    h, r = header_functions(), rust_functions()
+    assert len(h) >= 37
+    assert set(r) == set(h), (set(h) - set(r), set(r) - set(h))
+    for name, (ret, params) in h.items():
+        assert r[name] == (ret, params), (name, r[name], (ret, params))
+
+
+def _c_layout():
+    """sizeof / offsetof of every field of the three structs, from gcc."""
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "dips_hip.h"', "int main(void) {"]
+    for c_name, fields in header_structs().items():
+        lines.append(f'printf("{c_name} size %zu\\n", sizeof({c_name}));')
+        for f, _ in fields:
+            lines.append(f'printf("{c_name} {f} %zu\\n", offsetof({c_name}, {f}));')
+    lines.append("return 0; }")
+    return "\n".join(lines)
+
+
+def test_rust_layout_asserts_match_c(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(_c_layout())
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-pedantic", "-I", os.path.join(ROOT, "include"), str(src),
+                    "-o", str(exe)], check=True)
+    c = {}
+    for line in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        s, f, v = line.split()
+        c[(STRUCTS[s], f)] = int(v)
+    rs = open(FFI).read()
+    r = {}
+    for name, v in re.findall(r"assert!\(size_of::<(\w+)>\(\) == (\d+)\);", rs):
+        r[(name, "size")] = int(v)
+    for name, f, v in re.findall(r"assert!\(offset_of!\((\w+), (\w+)\) == (\d+)\);", rs):
+        r[(name, f)] = int(v)
+    assert r == c
+
+
+def test_header_layout_asserts_compile(tmp_path):
+    """DIPS_LAYOUT_ASSERT holds in C99 and C++17 (a wrong size fails the build)."""
+    src = tmp_path / "inc.c"
+    src.write_text('#include "dips_hip.h"\nint main(void) { return 0; }\n')
+    inc = os.path.join(ROOT, "include")
+    subprocess.run(["gcc", "-std=c99", "-pedantic", "-Werror", "-I", inc, "-c", str(src), "-o",
+                    str(tmp_path / "a.o")], check=True)
+    subprocess.run(["g++", "-std=c++17", "-Werror", "-x", "c++", "-I", inc, "-c", str(src), "-o",
+                    str(tmp_path / "b.o")], check=True)
+    bad = tmp_path / "bad.c"
+    bad.write_text('#include "dips_hip.h"\nDIPS_LAYOUT_ASSERT(sizeof(dips_params) == 40, "x");\n')
+    r = subprocess.run(["gcc", "-std=c99", "-I", inc, "-c", str(bad), "-o", str(tmp_path / "c.o")],
+                       capture_output=True)
+    assert r.returncode != 0
+
+
+def test_filter_codes_match_reference_into_f64():
+    """`Into<f64>` of DiPsFilter / ChromaFilter (dips/src/lib.rs:32-61): the
+    crate's code() values are the header's constants and the reference's."""
+    src = open(os.path.join(CRATE, "src", "lib.rs")).read()
+    consts = dict(re.findall(r"pub const (DIPS_\w+): u32 = (\w+);", open(FFI).read()))
+    want = {"Unfiltered": 255, "Sigmoid": 0, "InverseSigmoid": 1, "None": 0, "Red": 1, "Green": 2, "Blue": 3}
+    for variant, const in re.findall(r"(?:DiPsFilter|ChromaFilter)::(\w+) => ffi::(DIPS_\w+),", src):
+        assert int(consts[const], 0) == want[variant], (variant, const)
+    hdr = open(HEADER).read()
+    for name, v in consts.items():
+        m = re.search(r"#define %s (\w+?)u?\b" % name, hdr)
+        assert m and int(m.group(1).rstrip("u"), 0) == int(v, 0), name
+
+
+def test_crate_files_and_integration_doc():
+    for p in ("Cargo.toml", "build.rs", "src/lib.rs", "src/ffi.rs", "examples/frame_callback.rs"):
+        assert os.path.exists(os.path.join(CRATE, p)), p
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "rust/dips-hip" in doc
+    lib = open(os.path.join(CRATE, "src", "lib.rs")).read()
+    # the reference's operator surface, same names
+    for sig in ("pub fn new(colorize: bool, spatial_window_size: i32, sensitivity: f32, filter_type: DiPsFilter,",
+                "pub fn add_texture(&mut self, width: u32, height: u32, frame_data: &[u8])",
+                "pub fn dispatch(&mut self) -> Option<Vec<u8>>",
+                "pub fn frame_callback(width: u32, height: u32, frame_data: &[u8], compute: &mut ComputeState) -> Vec<u8>"):
+        assert sig in lib, sig
