@@ -539,7 +539,7 @@ dips_status dips_alt_create(const dips_alt_params* params, uint32_t width, uint3
     h->height = height;
     e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&h->cu_count, hipDeviceAttributeMultiprocessorCount, device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamDefault);  // blocking: ordered with stream 0 (see dips_set_stream)
     for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&h->meta_done[k], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->meta_free, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventRecord(h->meta_free, h->own_stream);

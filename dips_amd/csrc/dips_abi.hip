@@ -409,7 +409,7 @@ dips_status dips_create(const dips_params* params, int device, dips_handle** out
     h->device = device;
     e = hipSetDevice(device);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&h->cu_count, hipDeviceAttributeMultiprocessorCount, device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamDefault);  // blocking: ordered with stream 0 (see dips_set_stream)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->copy_stream, hipStreamNonBlocking);
     for (int i = 0; i < 3 && e == hipSuccess; ++i) {
         e = hipEventCreateWithFlags(&h->copy_done[i], hipEventDisableTiming);

@@ -129,7 +129,10 @@ void dips_destroy(dips_handle *h);
 const char *dips_last_error(const dips_handle *h);
 
 /* Run subsequent work on `stream` (a hipStream_t; NULL = the handle's own).
- * Switching streams orders the new stream after all work already issued on
+ * The handle's own stream is a blocking stream: its work is ordered with the
+ * legacy default stream (stream 0) both ways, so a caller whose work runs on
+ * stream 0 -- torch's default stream reports cuda_stream 0, which the Python
+ * wrappers pass as NULL -- needs no extra synchronisation.  Switching streams orders the new stream after all work already issued on
  * the previous one (the handle's device scratch serves both), so the previous
  * stream must still exist at the switch; setting the current stream again is
  * free.  A caller that binds an external stream and may destroy it should

@@ -448,3 +448,32 @@ def test_stream_switch_orders_shared_scratch(c):
             assert np.array_equal(sb.cpu().numpy().view(np.uint64), want[1])
     finally:
         op.close()
+
+
+def test_device_calls_ordered_with_torch_default_stream():
+    """torch's default stream is stream 0 (cuda_stream 0), which the wrappers
+    pass as NULL = the handle's own stream; that stream is a blocking one, so
+    library work and torch work on the default stream are ordered both ways
+    with no synchronisation in between (round 3: with a non-blocking own
+    stream a torch read right after synth_device saw stale frames)."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    assert torch.cuda.current_stream().cuda_stream == 0
+    W, H, n = 3840, 2160, 48
+    op = DiffSeriesOperator(PixelFormat.RGB8, Mode.PerFrame, 8 / 255)
+    try:
+        fr = torch.zeros((n, H, W, 3), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        op.synth_device(fr, W, H, 0xD1B5, 0)
+        racy = fr[n - 1].to(torch.int64).sum()  # torch kernel right behind the library's
+        torch.cuda.synchronize()
+        assert int(racy) == int(fr[n - 1].to(torch.int64).sum())
+        # the other way: a torch fill, then the series kernel reading it at once
+        fr.fill_(3)
+        fr[1:].fill_(200)
+        ser = torch.full((n, 4), -1, dtype=torch.int64, device="cuda")
+        op.run_device(fr, ser)
+        torch.cuda.synchronize()
+        assert int(ser[1, 0]) == W * H * 3 * 197 and int(ser[2, 0]) == 0
+    finally:
+        op.close()
