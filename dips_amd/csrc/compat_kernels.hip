@@ -183,6 +183,14 @@ __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
 // contiguous bytes each way.  (Four pixels per thread through 16-B
 // system-coherent buffer loads / stores measured slower: 557-575 against
 // 695-701 frames/s of 4K per-frame calls, tools/callback_direct_ab.py.)
+//
+// The output goes back as the RGBA8 texel (out_key 0) or as its key
+// (out_key 1 / 2): every texel of visual_epilogue has A = 255, gray has
+// R = G = B (COLORIZE off) and the two HSL cases have B = min(R, G)
+// (dips_shader.wgsl:30-62, 231-239; q is monotonic), so one or two bytes per
+// pixel carry it exactly and the copy-out threads rebuild the RGBA8 texel
+// (host_stream.h expand_keys): 8.3 instead of 33.2 MB per 4K frame on the
+// PCIe link that the frame's upload shares.
 template <int SLOT_MODE>
 __global__ __launch_bounds__(256) void compat_main_host_kernel(CompatArgs a) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
@@ -191,8 +199,56 @@ __global__ __launch_bounds__(256) void compat_main_host_kernel(CompatArgs a) {
     const uint32_t v = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a.raw + 4 * p), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_SYSTEM);
     const float fi = intensity_rgb(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, a.chroma);
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 4 * p), compat_texel(a, p, fi, SLOT_MODE, v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t texel = compat_texel(a, p, fi, SLOT_MODE, v);
+    if (a.out_key == 1u)
+        __hip_atomic_store(a.out + p, (uint8_t)texel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else if (a.out_key == 2u)
+        __hip_atomic_store(reinterpret_cast<uint16_t*>(a.out + 2 * p), (uint16_t)texel, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 4 * p), texel, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The same, two pixels per thread (out_key 1 / 2 only): one 8-byte
+// system-scope load of the pair's RGBA8 texels and one 2- / 4-byte store of
+// their keys per thread, over the absolute pixel pairs (2k, 2k + 1) that the
+// rows [y0, y1) touch, so every full pair is naturally aligned; a pair cut by
+// the range's ends (odd y0 * width or y1 * width) does its pixel alone.
+// Wider host reads per thread (the host copy kernels' 8-byte words reach the
+// DMA rate, host_stream.h pipe_h2d).
+template <int SLOT_MODE>
+__global__ __launch_bounds__(256) void compat_main_host2_kernel(CompatArgs a) {
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    const uint64_t p0 = (uint64_t)a.y0 * a.width, p1 = (uint64_t)yend * a.width;
+    const uint64_t q = (p0 & ~1ull) + 2u * ((uint64_t)blockIdx.x * 256u + threadIdx.x);  // even pixel
+    if (q >= p1) return;
+    if (q >= p0 && q + 2u <= p1) {
+        const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a.raw + 4 * q), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t v0 = (uint32_t)v, v1 = (uint32_t)(v >> 32);
+        const uint32_t t0 =
+            compat_texel(a, q, intensity_rgb(v0 & 0xFFu, (v0 >> 8) & 0xFFu, (v0 >> 16) & 0xFFu, a.chroma), SLOT_MODE, v0);
+        const uint32_t t1 = compat_texel(a, q + 1, intensity_rgb(v1 & 0xFFu, (v1 >> 8) & 0xFFu, (v1 >> 16) & 0xFFu, a.chroma),
+                                         SLOT_MODE, v1);
+        if (a.out_key == 1u)
+            __hip_atomic_store(reinterpret_cast<uint16_t*>(a.out + q), (uint16_t)((t0 & 0xFFu) | ((t1 & 0xFFu) << 8)),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 2 * q), (t0 & 0xFFFFu) | (t1 << 16),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    const uint64_t p = q >= p0 ? q : q + 1u;  // the one pixel of a cut pair inside [p0, p1)
+    const uint32_t v = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a.raw + 4 * p), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t texel =
+        compat_texel(a, p, intensity_rgb(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, a.chroma), SLOT_MODE, v);
+    if (a.out_key == 1u)
+        __hip_atomic_store(a.out + p, (uint8_t)texel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+        __hip_atomic_store(reinterpret_cast<uint16_t*>(a.out + 2 * p), (uint16_t)texel, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // A ring slot as frame_callback leaves it for a W = 1 frame: the gray texel
@@ -365,6 +421,19 @@ hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, int slot_
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
     const uint64_t n_px = (uint64_t)(yend - a.y0) * a.width;
+    if (a.out_key != 0u && a.host_pairs != 0u) {
+        // two pixels per thread over the absolute pixel pairs the rows touch
+        const uint64_t p0 = (uint64_t)a.y0 * a.width, p1 = (uint64_t)yend * a.width;
+        const uint64_t pairs = (p1 + 1) / 2 - p0 / 2;
+        const dim3 g2((uint32_t)((pairs + 255) / 256));
+        switch (slot_mode) {
+            case kSlotQ: hipLaunchKernelGGL(compat_main_host2_kernel<kSlotQ>, g2, dim3(256), 0, s, a); break;
+            case kSlotRaw: hipLaunchKernelGGL(compat_main_host2_kernel<kSlotRaw>, g2, dim3(256), 0, s, a); break;
+            case kSlotNone: hipLaunchKernelGGL(compat_main_host2_kernel<kSlotNone>, g2, dim3(256), 0, s, a); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     const dim3 grid((uint32_t)((n_px + 255) / 256));
     switch (slot_mode) {
         case kSlotQ: hipLaunchKernelGGL(compat_main_host_kernel<kSlotQ>, grid, dim3(256), 0, s, a); break;

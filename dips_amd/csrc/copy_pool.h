@@ -173,6 +173,74 @@ inline void host_copy(uint8_t* dst, const uint8_t* src, size_t bytes, bool nt) {
         std::memcpy(dst, src, bytes);
 }
 
+// RGBA8 texels rebuilt from the per-pixel keys compat_main_host_kernel
+// writes (out_key): one byte k -> (k, k, k, 255); two bytes (r, g) ->
+// (r, g, min(r, g), 255).  `npx` pixels from `keys` to `dst` (4 npx bytes).
+// With `nt`, 32-B streaming stores (the caller's output is written once).
+__attribute__((target("avx2"))) inline void put32(uint8_t* d, __m256i v, bool nt) {
+    if (nt && ((uintptr_t)d & 31u) == 0)
+        _mm256_stream_si256(reinterpret_cast<__m256i*>(d), v);
+    else
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(d), v);
+}
+
+__attribute__((target("avx2"))) inline void expand_keys_avx2(uint8_t* dst, const uint8_t* keys, size_t npx,
+                                                            int key_bytes, bool nt) {
+    const __m256i alpha = _mm256_set1_epi32((int)0xFF000000u);
+    size_t i = 0;
+    if (key_bytes == 1) {
+        // 16 keys -> 64 B: each 128-bit lane of a broadcast picks 4 keys
+        const __m256i s0 = _mm256_setr_epi8(0, 0, 0, -1, 1, 1, 1, -1, 2, 2, 2, -1, 3, 3, 3, -1,  //
+                                            4, 4, 4, -1, 5, 5, 5, -1, 6, 6, 6, -1, 7, 7, 7, -1);
+        const __m256i s1 = _mm256_setr_epi8(8, 8, 8, -1, 9, 9, 9, -1, 10, 10, 10, -1, 11, 11, 11, -1,  //
+                                            12, 12, 12, -1, 13, 13, 13, -1, 14, 14, 14, -1, 15, 15, 15, -1);
+        for (; i + 16 <= npx; i += 16) {
+            const __m256i k = _mm256_broadcastsi128_si256(_mm_loadu_si128(reinterpret_cast<const __m128i*>(keys + i)));
+            put32(dst + 4 * i, _mm256_or_si256(_mm256_shuffle_epi8(k, s0), alpha), nt);
+            put32(dst + 4 * (i + 8), _mm256_or_si256(_mm256_shuffle_epi8(k, s1), alpha), nt);
+        }
+        for (; i < npx; ++i) {
+            const uint32_t k = keys[i];
+            const uint32_t t = k | (k << 8) | (k << 16) | 0xFF000000u;
+            std::memcpy(dst + 4 * i, &t, 4);
+        }
+    } else {
+        // 8 (r, g) keys -> 32 B: min of (r, g, r, .) and (r, g, g, .) puts min(r, g) in B
+        // (both 128-bit lanes hold their 4 keys in bytes 0..7)
+        const __m256i sa = _mm256_setr_epi8(0, 1, 0, -1, 2, 3, 2, -1, 4, 5, 4, -1, 6, 7, 6, -1,  //
+                                            0, 1, 0, -1, 2, 3, 2, -1, 4, 5, 4, -1, 6, 7, 6, -1);
+        const __m256i sb = _mm256_setr_epi8(0, 1, 1, -1, 2, 3, 3, -1, 4, 5, 5, -1, 6, 7, 7, -1,  //
+                                            0, 1, 1, -1, 2, 3, 3, -1, 4, 5, 5, -1, 6, 7, 7, -1);
+        for (; i + 8 <= npx; i += 8) {
+            // keys of pixels i..i+3 in the low lane, i+4..i+7 in the high lane
+            const __m128i lo = _mm_loadl_epi64(reinterpret_cast<const __m128i*>(keys + 2 * i));
+            const __m128i hi = _mm_loadl_epi64(reinterpret_cast<const __m128i*>(keys + 2 * i + 8));
+            const __m256i k = _mm256_inserti128_si256(_mm256_castsi128_si256(lo), hi, 1);
+            const __m256i v = _mm256_min_epu8(_mm256_shuffle_epi8(k, sa), _mm256_shuffle_epi8(k, sb));
+            put32(dst + 4 * i, _mm256_or_si256(v, alpha), nt);
+        }
+        for (; i < npx; ++i) {
+            const uint32_t r = keys[2 * i], g = keys[2 * i + 1];
+            const uint32_t t = r | (g << 8) | ((r < g ? r : g) << 16) | 0xFF000000u;
+            std::memcpy(dst + 4 * i, &t, 4);
+        }
+    }
+    if (nt) _mm_sfence();
+}
+
+inline void expand_keys(uint8_t* dst, const uint8_t* keys, size_t npx, int key_bytes, bool nt) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) {
+        expand_keys_avx2(dst, keys, npx, key_bytes, nt);
+        return;
+    }
+    for (size_t i = 0; i < npx; ++i) {
+        const uint32_t r = keys[key_bytes * i], g = key_bytes == 1 ? r : keys[2 * i + 1];
+        const uint32_t t = r | (g << 8) | ((r < g ? r : g) << 16) | 0xFF000000u;
+        std::memcpy(dst + 4 * i, &t, 4);
+    }
+}
+
 // Host copy in ~4 MiB pieces over the pool.
 inline void pool_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
     const size_t kPiece = 4u << 20;

@@ -92,6 +92,7 @@ struct dips_handle {
     bool pending = false;
     uint32_t pending_slot = 0;
     dips_host::DirectGeom pend_geom;  // stripes of the speculative dispatch
+    int pend_key = 0;                 // its output form in io_out (compact_out_keys)
     // slots holding a raw frame (added, not yet quantised by a dispatch): the
     // reference reads their unquantised intensity, which the
     // batch kernel's gray-texel ring cannot express
@@ -183,7 +184,7 @@ struct FastGeom {
 };
 
 FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, int C, bool pf,
-                       bool map) {
+                       bool map, bool align = false, bool isi = false) {
     FastGeom g;
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t fb = npx * (uint64_t)C;
@@ -199,7 +200,7 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
     g.tail_px0 = nvec * (uint64_t)ppv;
     g.n_tiles = (nvec + 64 * U - 1) / (64 * U);
     g.items = g.n_tiles * n_frames;
-    const void* k = dips::series_fast_kernel_ptr(C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map);
+    const void* k = dips::series_fast_kernel_ptr(C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map, align, isi);
     if (!k) return g;
     // waves per SIMD: the kernel's occupancy, optionally capped by
     // DIPS_SERIES_WAVES_PER_SIMD (bench.py sets 4 at N > 1 so that RCCL's
@@ -277,9 +278,19 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
 
     FastGeom g;
     const bool glut = C == 1 && gray_lut_enabled();
+    // RGB8 frames off a 4-byte boundary (an odd frame stride or an offset
+    // pointer) run the aligned-load form of the kernel (series_v2.hip ALIGN)
+    // (DIPS_SERIES_ALIGN=0: the byte-unaligned 12-B loads instead, A/B)
+    const char* align_env = std::getenv("DIPS_SERIES_ALIGN");
+    const bool align = C == 3 && ((((uintptr_t)frames | (uintptr_t)fb | (uintptr_t)ref0) & 3u) != 0u) &&
+                       !(align_env && align_env[0] == '0');
+    // RGB8 / RGBA8 with tau >= 2^-5: the integer intensity sum (series_v2.hip
+    // ISI; DIPS_SERIES_ISI=0 keeps the f64 sum, A/B)
+    const char* isi_env = std::getenv("DIPS_SERIES_ISI");
+    const bool isi = C != 1 && dips::series_v2_isi(h->p.tau) && !(isi_env && isi_env[0] == '0');
     if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC))
         g = glut ? gray_lut_geometry(h, width, height, n_frames)
-                 : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr);
+                 : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr, align, isi);
     auto launch_generic = [&](uint64_t px0) -> dips_status {
         const uint64_t bpf = (npx - px0 + 255u) / 256u;
         if (bpf * (uint64_t)n_frames >= (1ull << 31))
@@ -327,13 +338,13 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         a.n_frames = n_frames;
         a.n_tiles = (uint32_t)g.n_tiles;
         a.n_waves = (uint32_t)g.n_waves;
-        a.thr = dips::series_threshold(C, h->p.tau);
+        a.thr = dips::series_threshold(C, h->p.tau, isi);
         if (glut) {
             a.lut = h->gray_lut.p;
             DIPS_HIP(h, dips::launch_series_gray_lut(a, pf, map != nullptr, h->gray_lut_layout, (uint32_t)g.blocks, s));
         } else {
             DIPS_HIP(h, dips::launch_series_fast(a, C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map != nullptr,
-                                                 (uint32_t)g.blocks, s));
+                                                 (uint32_t)g.blocks, s, align, isi));
         }
         // the ragged tail (< pixels_per_vec pixels per frame): its sums go
         // straight into the series by atomics, so the order is free
@@ -522,6 +533,23 @@ dips_status flush_pending(dips_handle* h) {
     return DIPS_OK;
 }
 
+// Bytes per pixel the zero-copy compute_main writes into pinned memory: the
+// texel's key (1: gray, 2: colorized; compat_main_host_kernel) instead of the
+// RGBA8 texel, rebuilt by the copy-out threads.  DIPS_COMPACT_OUT=0 keeps
+// RGBA8 (A/B, tests).  Read on the calling thread.
+int compact_out_keys(const dips_handle* h) {
+    const char* e = std::getenv("DIPS_COMPACT_OUT");
+    if (e && e[0] == '0') return 0;
+    return h->p.colorize ? 2 : 1;
+}
+
+// Two pixels per thread in the keyed zero-copy kernel (DIPS_HOST_PX=1: one,
+// A/B).  Read on the calling thread: the launches run on the copy pool's.
+uint32_t host_pairs() {
+    const char* e = std::getenv("DIPS_HOST_PX");
+    return (e && e[0] == '1') ? 0u : 1u;
+}
+
 // Deferral of host frames in steady state (DIPS_DEFER_UPLOAD=0 turns it off).
 bool defer_upload(const dips_handle* h) {
     if (!h->main_init || (h->p.flags & DIPS_FLAG_DEVICE_PTRS)) return false;
@@ -573,6 +601,9 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
         a.filter = h->p.filter_type;
         a.sensitivity = h->p.sensitivity;
         a.colorize = h->p.colorize ? 1u : 0u;
+        a.out_key = (uint32_t)compact_out_keys(h);
+        a.host_pairs = host_pairs();
+        h->pend_key = (int)a.out_key;
         const size_t row = (size_t)width * 4u;
         h->pend_geom.init(height, row);
         const hipStream_t cs[2] = {h->stream, h->copy_stream};
@@ -677,7 +708,7 @@ int dispatch_impl(dips_handle* h, uint8_t* out, size_t cap, bool device_dst) {
         // stripe's kernel has finished once collected): W = 1 quantises the
         // raw frame in place, W > 1 copies the filtered texel from `raw`
         h->pending = false;
-        DIPS_HIP(h, dips_host::direct_collect(out, h->io_out.bytes(), h->pieces, h->pend_geom));
+        DIPS_HIP(h, dips_host::direct_collect(out, h->io_out.bytes(), h->pieces, h->pend_geom, h->pend_key));
         uint8_t* dslot = h->slots[h->pending_slot].as<uint8_t>();
         if (h->p.spatial_window_size == 1)
             DIPS_HIP(h, dips::launch_compat_quantise_slot(dslot, (uint64_t)h->width * h->height, h->p.chroma_filter,
@@ -943,6 +974,8 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
         DIPS_HIP(h, hipHostGetDevicePointer(&dout, h->io_out.p, 0));
         a.raw = static_cast<const uint8_t*>(din);
         a.out = static_cast<uint8_t*>(dout);
+        a.out_key = (uint32_t)compact_out_keys(h);
+        a.host_pairs = host_pairs();
         // odd stripes on copy_stream (idle here, synchronised above); every
         // stripe's kernel has finished when the call returns
         const char* one_env = std::getenv("DIPS_DIRECT_STREAMS");  // "1": every stripe on the compute stream (A/B)
@@ -953,7 +986,8 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
                                                             a.y0 = y0;
                                                             a.y1 = y1;
                                                             return dips::launch_compat_main_host(a, s);
-                                                        }));
+                                                        },
+                                                        (int)a.out_key));
         return 1;
     }
     DIPS_HIP(h, dips_host::run_striped_frame(frame, out, H, row, h->io.bytes(), h->io_out.bytes(), slot,

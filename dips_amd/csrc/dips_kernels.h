@@ -90,6 +90,10 @@ struct CompatArgs {
     float sensitivity;
     uint32_t colorize;
     uint32_t y0, y1;         // compat_main: rows [y0, y1) only (y1 = 0: all rows)
+    uint32_t out_key;        // compat_main_host: 0 RGBA8 texels; 1 one byte (gray: R = G = B, A = 255);
+                             // 2 two bytes R | G << 8 (colorized: B = min(R, G), A = 255) -- the host
+                             // expands them (host_stream.h expand_keys)
+    uint32_t host_pairs;     // out_key != 0: two pixels per thread (compat_main_host2_kernel)
 };
 
 // dips ComputeState over a batch in steady state (compat_batch.hip).
@@ -215,12 +219,16 @@ inline bool alt_fast_epilogue_ok(uint32_t filter, float k) {
 
 int pixels_per_vec(int channels);
 int fast_unroll(int channels);
-const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map);
-const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool map);
+const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align = false,
+                                   bool isi = false);
+const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align = false,
+                                 bool isi = false);
+// whether tau admits the integer intensity sum of series_v2 (tau >= 2^-5)
+bool series_v2_isi(float tau);
 // threshold argument (SeriesArgs::thr) of the kernel series_fast_kernel_ptr picks
-float series_threshold(int channels, float tau);
+float series_threshold(int channels, float tau, bool isi = false);
 hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, bool per_frame, bool map,
-                              uint32_t blocks, hipStream_t s);
+                              uint32_t blocks, hipStream_t s, bool align = false, bool isi = false);
 // record layout: 0 RGB(A), 1 gray (series_fast_kernel), 2 gray table kernel (series_gray_lut_kernel)
 hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
                                 dips_series_entry* series, hipStream_t s);

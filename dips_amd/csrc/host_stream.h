@@ -244,10 +244,21 @@ inline uint32_t direct_first_rows(uint32_t rows) {
     return std::max(1u, rows / 4u);
 }
 
+// copy-out of one piece [o, o + len) of the RGBA8 frame: from pin_out itself
+// (key_bytes 0) or rebuilt from the per-pixel keys the kernel wrote there
+// (key_bytes 1 / 2 per pixel, pin_out + o / 4 * key_bytes; expand_keys).
+inline void copy_out_piece(uint8_t* out, const uint8_t* pin_out, size_t o, size_t len, int key_bytes, bool nt) {
+    if (!len) return;
+    if (key_bytes)
+        expand_keys(out + o, pin_out + o / 4u * (size_t)key_bytes, len / 4u, key_bytes, nt);
+    else
+        host_copy(out + o, pin_out + o, len, nt);
+}
+
 template <typename Launch>
 hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t height, size_t row,
                                     uint8_t* pin_in, const uint8_t* pin_out, const hipStream_t (&compute)[2],
-                                    int device, PieceEvents& ev, Launch&& launch) {
+                                    int device, PieceEvents& ev, Launch&& launch, int key_bytes = 0) {
     const bool nt = nt_copy();  // on the calling thread, never in the workers
     const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
     const uint32_t first = std::min(height, direct_first_rows(rows));
@@ -305,7 +316,7 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
             err.store((int)r);
             return;
         }
-        if (len) host_copy(out + o, pin_out + o, len, nt);
+        copy_out_piece(out, pin_out, o, len, key_bytes, nt);
         if (trace) ts[2 * n_s + pi] = since();
     });
     if (trace) {
@@ -379,7 +390,8 @@ hipError_t direct_stage_launch(const uint8_t* frame, uint8_t* pin_in, const hipS
 
 // Second half: the pool copies each stripe's pieces from `pin_out` to `out`
 // as soon as the stripe's event (recorded by direct_stage_launch) has fired.
-inline hipError_t direct_collect(uint8_t* out, const uint8_t* pin_out, PieceEvents& ev, const DirectGeom& g) {
+inline hipError_t direct_collect(uint8_t* out, const uint8_t* pin_out, PieceEvents& ev, const DirectGeom& g,
+                                 int key_bytes = 0) {
     const bool nt = nt_copy();  // on the calling thread, never in the workers
     std::atomic<int> err{(int)hipSuccess};
     CopyPool::global().run((size_t)g.n_s * g.k, [&](size_t i) {
@@ -391,7 +403,7 @@ inline hipError_t direct_collect(uint8_t* out, const uint8_t* pin_out, PieceEven
         }
         size_t o, len;
         g.piece(si, j, o, len);
-        if (len) host_copy(out + o, pin_out + o, len, nt);
+        copy_out_piece(out, pin_out, o, len, key_bytes, nt);
     });
     return (hipError_t)err.load();
 }

@@ -577,24 +577,27 @@ static const void* pick_fast_u(int chroma, bool pf, bool map) {
 // RGB8 / RGBA8 run series_v2_kernel (series_v2.hip); GRAY8 the kernel above.
 int fast_unroll(int channels) { return channels == 1 ? kUnrollGray : kUnrollV2; }
 
-const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map) {
+const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align, bool isi) {
     switch (channels) {
         case 1: return pick_fast_u<1, kUnrollGray>(chroma, per_frame, map);
         case 3:
-        case 4: return series_v2_kernel_ptr(channels, chroma, per_frame, map);
+        case 4: return series_v2_kernel_ptr(channels, chroma, per_frame, map, align, isi);
         default: return nullptr;
     }
 }
 
 // gray: dI > tau on the f32 intensity; RGB(A) v2: |dI2s| > tau * 2^23 with
 // I2s = 2 I * 2^22 (exact power-of-two scalings of the reference comparison)
-float series_threshold(int channels, float tau) { return channels == 1 ? tau : tau * 8388608.0f; }
+// (integer-sum form, isi: |dI| * 2^28 > tau * 2^28, series_v2.hip)
+float series_threshold(int channels, float tau, bool isi) {
+    return channels == 1 ? tau : tau * (isi ? 268435456.0f : 8388608.0f);
+}
 
 int pixels_per_vec(int channels) { return channels == 1 ? 16 : 4; }
 
 hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, bool per_frame, bool map,
-                              uint32_t blocks, hipStream_t s) {
-    const void* k = series_fast_kernel_ptr(channels, chroma, per_frame, map);
+                              uint32_t blocks, hipStream_t s, bool align, bool isi) {
+    const void* k = series_fast_kernel_ptr(channels, chroma, per_frame, map, align, isi);
     if (!k) return hipErrorInvalidValue;
     SeriesArgs args = a;
     void* params[] = {&args};

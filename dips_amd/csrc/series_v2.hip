@@ -35,20 +35,37 @@ namespace dips {
 // <= 2^-11 per add) is within 0.01 of the integer SJ.
 constexpr float kSjMul = 255.0f / 4194304.0f;
 
+// The integer intensity sum (ISI): for tau >= 2^-5 every selected dI is an
+// f32 in [2^-5, 1] whose ulp is >= 2^-28, so a = |dI| * 2^28 -- the
+// difference of intensities taken 32 times as large (norm_h2<true>, an exact
+// power-of-two scaling of the reference's f32 subtraction) -- is an integer
+// <= 2^28 for every selected pixel: one v_cvt_u32_f32 + v_add_u32 per pixel
+// instead of v_cvt_f64_f32 + v_add_f64 (the f64 add is the most
+// power-hungry VALU class this kernel issues, profiles/
+// r02_energy_per_instruction.jsonl).  Two accumulators of 8 pixels each stay
+// below 2^31.  The record carries n = sum dI * 2^32 = 16 sum a as H = n >> 15,
+// L = n mod 2^15, exactly as the f64 form.
+constexpr float kIsiMinTau = 0.03125f;  // 2^-5
+
 // One frame of one tile: accumulate against the reference state `st`
 // (updated to this frame's state in per-frame mode) and the reference bytes
 // `rb`; produce the 4 per-lane values {SAD, SJ, H, L} and the wave-wide count.
-template <int C, int CH, int U, bool PF, bool MAP, int SAUX = kAuxNT>
-__device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], const uint32_t (&rb)[U][Fmt<C>::NDW],
-                                         const uint32_t (&cur)[U][Fmt<C>::NDW], uint32_t voff, uint32_t t,
+// rb / cur rows hold LR / LC dwords, the first Fmt<C>::NDW of which are the
+// vec's bytes (LC = 4 for RGB8 in the aligned-load form, see load_frame).
+template <int C, int CH, int U, bool PF, bool MAP, int SAUX = kAuxNT, int LR = Fmt<C>::NDW, int LC = Fmt<C>::NDW,
+          bool ISI = false>
+__device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], const uint32_t (&rb)[U][LR],
+                                         const uint32_t (&cur)[U][LC], uint32_t voff, uint32_t t,
                                          uint32_t* vals, uint32_t& cnt) {
     using F = Fmt<C>;
     uint32_t sad = 0, c = 0;
     float sj = 0.5f;  // + 0.5: the final truncation rounds to nearest
+    constexpr float sj_mul = ISI ? kSjMul / 32.0f : kSjMul;
     // exact per-lane intensity sum, offset by 2^43 so that the f64's low 52
     // mantissa bits ARE the fixed-point value n = sum(a_s) * 2^9 (ulp(2^43)
     // = 2^-9, the a_s granularity; n < 2^35 keeps every add exact)
     double si = 0x1p43;
+    uint32_t si0 = 0, si1 = 0;  // ISI: sum of a over vecs 0 .. U/2-1 and U/2 .. U-1
     uint32_t map[U][F::NDW];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -58,13 +75,18 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
             if constexpr (MAP) map[u][k] = absdiff_bytes(cur[u][k], rb[u][k]);
         }
         St2 n;
-        derive_v2<C, CH>(cur[u], n);
+        {
+            uint32_t cv[F::NDW];
+#pragma unroll
+            for (int k = 0; k < F::NDW; ++k) cv[k] = cur[u][k];
+            derive_v2<C, CH, ISI>(cv, n);
+        }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const f32x2 d = n.i[k] - st[u].i[k];
             const float a0 = fabsf(d.x), a1 = fabsf(d.y);
-            sj = __builtin_fmaf(a0, kSjMul, sj);
-            sj = __builtin_fmaf(a1, kSjMul, sj);
+            sj = __builtin_fmaf(a0, sj_mul, sj);
+            sj = __builtin_fmaf(a1, sj_mul, sj);
             const bool s0 = a0 > a.thr, s1 = a1 > a.thr;
             const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
             c += (uint32_t)__builtin_popcountll(m0) + (uint32_t)__builtin_popcountll(m1);
@@ -73,7 +95,15 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
             // as a forced branch it costs registers and occupancy)
             // (the lane-predicated form `if (s0) si += a0` compiles to an
             // unconditional add and two 32-bit selects of the f64: slower)
-            si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
+            if constexpr (ISI) {
+                const uint32_t v = (uint32_t)(s0 ? a0 : 0.0f) + (uint32_t)(s1 ? a1 : 0.0f);
+                if (u < U / 2)
+                    si0 += v;
+                else
+                    si1 += v;
+            } else {
+                si += (double)(s0 ? a0 : 0.0f) + (double)(s1 ? a1 : 0.0f);
+            }
         }
         if constexpr (PF) st[u] = n;
     }
@@ -82,12 +112,20 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
 #pragma unroll
         for (int u = 0; u < U; ++u) store_vec<C, SAUX>(rm, voff + (uint32_t)(u * 64 * F::VB), map[u]);
     }
-    const uint64_t yb = __builtin_bit_cast(uint64_t, si);
-    const uint32_t lo = (uint32_t)yb, hi = (uint32_t)(yb >> 32);
     vals[0] = sad;
     vals[1] = (uint32_t)sj;
-    vals[2] = __builtin_amdgcn_alignbit(hi, lo, 15);  // H = n >> 15 (n < 2^35: no exponent bits)
-    vals[3] = lo & 0x7FFFu;                           // L = n mod 2^15
+    if constexpr (ISI) {
+        // n = 16 (si0 + si1): H = n >> 15, L = n mod 2^15 without forming
+        // the 33-bit sum
+        const uint32_t low = (si0 & 0x7FFu) + (si1 & 0x7FFu);
+        vals[2] = (si0 >> 11) + (si1 >> 11) + (low >> 11);
+        vals[3] = (low & 0x7FFu) << 4;
+    } else {
+        const uint64_t yb = __builtin_bit_cast(uint64_t, si);
+        const uint32_t lo = (uint32_t)yb, hi = (uint32_t)(yb >> 32);
+        vals[2] = __builtin_amdgcn_alignbit(hi, lo, 15);  // H = n >> 15 (n < 2^35: no exponent bits)
+        vals[3] = lo & 0x7FFFu;                           // L = n mod 2^15
+    }
     cnt = c;
 }
 
@@ -108,8 +146,24 @@ __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t
 // per-frame kernel fits 64 VGPRs (8 waves) without spilling; the other
 // variants hold more state (fixed reference bytes, RGBA vecs, map stores) and
 // keep their natural allocation (5-7 waves).
-template <int C, int U, bool PF, bool MAP>
-constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : 5)) : 1; }
+template <int C, int U, bool PF, bool MAP, bool ALIGN = false>
+constexpr int v2_min_waves() {
+    return ALIGN ? (MAP ? 1 : 4) : ((C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : 5)) : 1);
+}
+
+// The aligned-load form of an RGB8 vec (ALIGN): a frame whose base address
+// is not a multiple of 4 (a frame stride W*H*3 that is not, or an offset
+// pointer) is read through a descriptor at the dword below its base, one
+// aligned dwordx4 per vec, and the vec's 12 bytes are funnel-shifted out of
+// the 16 (v_alignbyte_b32 by the wave-uniform byte offset, at first use).
+// Byte-unaligned 12-B buffer loads return the same bytes but cost extra
+// cache-line requests (62-63 % of 8 TB/s against 71.7 % aligned,
+// profiles/r02_fallback_rate_after.jsonl, r02_unaligned_probe.txt).
+__device__ __forceinline__ void funnel3(uint32_t (&v)[4], uint32_t sh) {
+    v[0] = __builtin_amdgcn_alignbyte(v[1], v[0], sh);
+    v[1] = __builtin_amdgcn_alignbyte(v[2], v[1], sh);
+    v[2] = __builtin_amdgcn_alignbyte(v[3], v[2], sh);
+}
 
 // The kernel body; AUX / SAUX are the cache-policy bits of the frame loads /
 // map stores (the library kernel below uses nt; probe builds instantiate
@@ -118,9 +172,12 @@ constexpr int v2_min_waves() { return (C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U 
 // 1 -- frames cut into parts of a.part_frames, items (part, tile) taken
 // part-major with stride n_waves, so concurrent waves read the same frames of
 // adjacent tiles (probe builds, tools/sched_ab.hip).
-template <int C, int CH, int U, bool PF, bool MAP, int AUX, int SAUX, int SCHED = 0>
+template <int C, int CH, int U, bool PF, bool MAP, int AUX, int SAUX, int SCHED = 0, bool ALIGN = false,
+          bool ISI = false>
 __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
     using F = Fmt<C>;
+    static_assert(!ALIGN || C == 3, "the aligned-load form is the RGB8 one");
+    constexpr int LW = ALIGN ? 4 : F::NDW;  // dwords loaded per vec
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -159,41 +216,76 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
         const __amdgpu_buffer_rsrc_t rpart =
             make_rsrc(a.partials + 2 * (uint64_t)tile * a.n_frames, a.n_frames * 16u);
 
-        auto load_frame = [&](uint32_t tf, uint32_t (&dst)[U][F::NDW]) {
+        // ALIGN: a descriptor at the dword below p (range rounded up to whole
+        // dwords: the dword holding the last byte never crosses a page), one
+        // dwordx4 per vec, *sh = p's byte offset in that dword
+        auto load_at = [&](const uint8_t* p, uint32_t (&dst)[U][LW], uint32_t* sh) {
+            if constexpr (ALIGN) {
+                const uint32_t d = (uint32_t)(uintptr_t)p & 3u;
+                *sh = d;
+                const __amdgpu_buffer_rsrc_t r = make_rsrc(p - d, (vb + d + 3u) & ~3u);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(r, voff + (uint32_t)(u * 64 * F::VB), 0, AUX);
+                    dst[u][0] = x.x;
+                    dst[u][1] = x.y;
+                    dst[u][2] = x.z;
+                    dst[u][3] = x.w;
+                }
+            } else {
+                const __amdgpu_buffer_rsrc_t r = make_rsrc(p, vb);
+#pragma unroll
+                for (int u = 0; u < U; ++u) load_vec<C, AUX>(r, voff + (uint32_t)(u * 64 * F::VB), dst[u]);
+            }
+        };
+        uint32_t sh[4] = {0u, 0u, 0u, 0u};  // ALIGN: byte offset of each ring slot's frame
+        auto load_frame = [&](uint32_t tf, uint32_t (&dst)[U][LW], uint32_t* shp) {
 #ifdef DIPS_PROBE_SAMEFRAME
             // probe build only (tools/probe.hip): every load re-reads the
             // segment's first frame -- the kernel's compute-only time
             tf = t0;
 #endif
-            const __amdgpu_buffer_rsrc_t r = make_rsrc(a.frames + (uint64_t)min(tf, tlast) * fb, vb);
-#pragma unroll
-            for (int u = 0; u < U; ++u) load_vec<C, AUX>(r, voff + (uint32_t)(u * 64 * F::VB), dst[u]);
+            load_at(a.frames + (uint64_t)min(tf, tlast) * fb, dst, shp);
         };
 
         // ring: PF -- frame k of the segment in slot (k+1)&3, its reference
         // (frame k-1) in slot k&3; overall -- frame k in slot k&3, the fixed
         // reference bytes in rb
-        uint32_t buf[4][U][F::NDW];
-        uint32_t rb[U][F::NDW];  // overall mode only
+        uint32_t buf[4][U][LW];
+        uint32_t rb[U][LW];  // overall mode only
         St2 st[U];
+        // ALIGN: the vec bytes of ring slot j in place (done once per frame, at
+        // its first use; in 'per-frame' mode the slot then serves as the next
+        // frame's reference as it is)
+        auto settle = [&](int j) {
+            if constexpr (ALIGN) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) funnel3(buf[j][u], sh[j]);
+            }
+        };
         {
             const uint8_t* rp = PF ? (t0 == 0 ? a.ref0 : a.frames + (uint64_t)(t0 - 1) * fb) : a.ref0;
-            const __amdgpu_buffer_rsrc_t rr = make_rsrc(rp, vb);
-            uint32_t (&dref)[U][F::NDW] = PF ? buf[0] : rb;
-#pragma unroll
-            for (int u = 0; u < U; ++u) load_vec<C>(rr, voff + (uint32_t)(u * 64 * F::VB), dref[u]);
+            uint32_t (&dref)[U][LW] = PF ? buf[0] : rb;
+            uint32_t rsh = 0;
+            load_at(rp, dref, &rsh);
             if constexpr (PF) {
-                load_frame(t0, buf[1]);
-                load_frame(t0 + 1, buf[2]);
-                load_frame(t0 + 2, buf[3]);
+                load_frame(t0, buf[1], &sh[1]);
+                load_frame(t0 + 1, buf[2], &sh[2]);
+                load_frame(t0 + 2, buf[3], &sh[3]);
             } else {
-                load_frame(t0, buf[0]);
-                load_frame(t0 + 1, buf[1]);
-                load_frame(t0 + 2, buf[2]);
-                load_frame(t0 + 3, buf[3]);
+                load_frame(t0, buf[0], &sh[0]);
+                load_frame(t0 + 1, buf[1], &sh[1]);
+                load_frame(t0 + 2, buf[2], &sh[2]);
+                load_frame(t0 + 3, buf[3], &sh[3]);
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u) derive_v2<C, CH>(dref[u], st[u]);
+            for (int u = 0; u < U; ++u) {
+                if constexpr (ALIGN) funnel3(dref[u], rsh);
+                uint32_t dv[F::NDW];
+#pragma unroll
+                for (int k2 = 0; k2 < F::NDW; ++k2) dv[k2] = dref[u][k2];
+                derive_v2<C, CH, ISI>(dv, st[u]);
+            }
         }
 
         uint32_t k = 0;
@@ -206,14 +298,17 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
                     const int j = 2 * h + q;
                     const uint32_t tf = t0 + k + (uint32_t)j;
                     if constexpr (PF) {
-                        frame_v2<C, CH, U, PF, MAP, SAUX>(a, st, buf[j], buf[(j + 1) & 3], voff, tf, v + 4 * q,
-                                                    q ? c1 : c0);
+                        settle((j + 1) & 3);
+                        frame_v2<C, CH, U, PF, MAP, SAUX, LW, LW, ISI>(a, st, buf[j], buf[(j + 1) & 3], voff, tf,
+                                                                  v + 4 * q, q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
-                        load_frame(tf + 3, buf[j]);
+                        load_frame(tf + 3, buf[j], &sh[j]);
                     } else {
-                        frame_v2<C, CH, U, PF, MAP, SAUX>(a, st, rb, buf[j], voff, tf, v + 4 * q, q ? c1 : c0);
+                        settle(j);
+                        frame_v2<C, CH, U, PF, MAP, SAUX, LW, LW, ISI>(a, st, rb, buf[j], voff, tf, v + 4 * q,
+                                                                  q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
-                        load_frame(tf + 4, buf[j]);
+                        load_frame(tf + 4, buf[j], &sh[j]);
                     }
                 }
                 const uint32_t y = wave_sum8_lanes(v, lane);
@@ -226,10 +321,13 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
             if (k + (uint32_t)j < n) {
                 uint32_t v[4], c;
                 const uint32_t tf = t0 + k + (uint32_t)j;
-                if constexpr (PF)
-                    frame_v2<C, CH, U, PF, MAP, SAUX>(a, st, buf[j], buf[j + 1], voff, tf, v, c);
-                else
-                    frame_v2<C, CH, U, PF, MAP, SAUX>(a, st, rb, buf[j], voff, tf, v, c);
+                if constexpr (PF) {
+                    settle(j + 1);
+                    frame_v2<C, CH, U, PF, MAP, SAUX, LW, LW, ISI>(a, st, buf[j], buf[j + 1], voff, tf, v, c);
+                } else {
+                    settle(j);
+                    frame_v2<C, CH, U, PF, MAP, SAUX, LW, LW, ISI>(a, st, rb, buf[j], voff, tf, v, c);
+                }
                 const uint32_t y = wave_sum4_lanes(v);
                 store_one(rpart, tf, rec_off4, lane, y, c);
             }
@@ -237,25 +335,26 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
     }
 }
 
-template <int C, int CH, int U, bool PF, bool MAP>
-__global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP>())) void series_v2_kernel(SeriesArgs a) {
-    series_v2_body<C, CH, U, PF, MAP, kAuxNT, kAuxNT>(a);
+template <int C, int CH, int U, bool PF, bool MAP, bool ALIGN = false, bool ISI = false>
+__global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP, ALIGN>())) void series_v2_kernel(SeriesArgs a) {
+    series_v2_body<C, CH, U, PF, MAP, kAuxNT, kAuxNT, 0, ALIGN, ISI>(a);
 }
 
 // ---------------------------------------------------------------------------
 // instantiation table
 // ---------------------------------------------------------------------------
-template <int C, int CH, bool PF, bool MAP>
+template <int C, int CH, bool PF, bool MAP, bool ALIGN, bool ISI>
 static const void* v2_ptr() {
-    return reinterpret_cast<const void*>(&series_v2_kernel<C, CH, kUnrollV2, PF, MAP>);
+    return reinterpret_cast<const void*>(&series_v2_kernel<C, CH, kUnrollV2, PF, MAP, ALIGN && C == 3, ISI>);
 }
 
-template <int C>
+template <int C, bool ALIGN, bool ISI>
 static const void* pick_v2(int chroma, bool pf, bool map) {
-#define DIPS_PICK_V2(CHV)                                                                        \
-    case CHV:                                                                                    \
-        return pf ? (map ? v2_ptr<C, CHV, true, true>() : v2_ptr<C, CHV, true, false>())         \
-                  : (map ? v2_ptr<C, CHV, false, true>() : v2_ptr<C, CHV, false, false>());
+#define DIPS_PICK_V2(CHV)                                                                                   \
+    case CHV:                                                                                               \
+        return pf ? (map ? v2_ptr<C, CHV, true, true, ALIGN, ISI>() : v2_ptr<C, CHV, true, false, ALIGN, ISI>()) \
+                  : (map ? v2_ptr<C, CHV, false, true, ALIGN, ISI>()                                        \
+                         : v2_ptr<C, CHV, false, false, ALIGN, ISI>());
     switch (chroma) {
         DIPS_PICK_V2(0)
         DIPS_PICK_V2(1)
@@ -266,12 +365,20 @@ static const void* pick_v2(int chroma, bool pf, bool map) {
 #undef DIPS_PICK_V2
 }
 
-const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool map) {
+const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align, bool isi) {
     switch (channels) {
-        case 3: return pick_v2<3>(chroma, per_frame, map);
-        case 4: return pick_v2<4>(chroma, per_frame, map);
+        case 3:
+            if (isi)
+                return align ? pick_v2<3, true, true>(chroma, per_frame, map)
+                             : pick_v2<3, false, true>(chroma, per_frame, map);
+            return align ? pick_v2<3, true, false>(chroma, per_frame, map)
+                         : pick_v2<3, false, false>(chroma, per_frame, map);
+        case 4:
+            return isi ? pick_v2<4, false, true>(chroma, per_frame, map) : pick_v2<4, false, false>(chroma, per_frame, map);
         default: return nullptr;
     }
 }
+
+bool series_v2_isi(float tau) { return tau >= kIsiMinTau; }
 
 }  // namespace dips

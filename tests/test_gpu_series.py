@@ -324,8 +324,9 @@ RAGGED_SHAPES = [(37, 23), (5, 3), (1, 1), (641, 3), (17, 1)]
 
 @pytest.mark.parametrize("c", [1, 3, 4])
 @pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("with_map", [True, False])
 @pytest.mark.parametrize("offsets", [(0, 0, 0), (1, 2, 3), (3, 1, 2), (2, 3, 1)])
-def test_unaligned_device_batches(c, mode, offsets):
+def test_unaligned_device_batches(c, mode, offsets, with_map):
     """The vectorised kernel on frame batches, references and maps at byte
     offsets 1-3 from an aligned address and with ragged pixel counts (frame
     strides that are not a multiple of 4, < pixels_per_vec trailing pixels
@@ -335,7 +336,10 @@ def test_unaligned_device_batches(c, mode, offsets):
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     fo, ro, mo = offsets
-    for (w, h) in [(64, 48)] + RAGGED_SHAPES:
+    # (RGB8 frames off a 4-byte boundary -- an offset batch, or a stride
+    # W*H*3 that is not a multiple of 4 such as (62, 33)'s 6138 -- run the
+    # aligned-load kernel, series_v2.hip ALIGN)
+    for (w, h) in [(64, 48), (62, 33)] + RAGGED_SHAPES:
         for tau, chroma in [(0.0, 0), (8 / 255, 0 if c == 1 else 2)]:
             n = 9
             frames = _frames(c, w, h, n, 5 + w, "random" if w % 2 else "synth")
@@ -353,7 +357,7 @@ def test_unaligned_device_batches(c, mode, offsets):
             series = torch.zeros((n, 4), dtype=torch.int64, device=dev)
             op = DiffSeriesOperator(PixelFormat(c), Mode(mode), tau, chroma)
             try:
-                op.run_device(fdev, series, ref=rdev if mode == 0 else None, map_out=mdev)
+                op.run_device(fdev, series, ref=rdev if mode == 0 else None, map_out=mdev if with_map else None)
                 torch.cuda.synchronize()
             finally:
                 op.close()
@@ -361,6 +365,8 @@ def test_unaligned_device_batches(c, mode, offsets):
                                           ref=ref if mode == 0 else None, want_map=True)
             got = series.cpu().numpy().view(np.uint64)
             assert np.array_equal(got, out4), ((w, h), tau, got, out4)
+            if not with_map:
+                continue
             m = mbuf.cpu().numpy()
             assert np.array_equal(m[mo:mo + n * fb].reshape(frames.shape), dmap), (w, h)
             # nothing written outside the map

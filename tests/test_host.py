@@ -172,3 +172,53 @@ def test_zero_copy_stripe_geometry(tmp_path):
     env = dict(os.environ, LD_LIBRARY_PATH="/opt/rocm/lib:" + os.environ.get("LD_LIBRARY_PATH", ""))
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout + r.stderr
+
+
+_KEYS_CHECK = r"""
+#include "copy_pool.h"
+#include <cstdio>
+#include <random>
+#include <vector>
+int main() {
+    std::mt19937_64 rng(11);
+    int bad = 0;
+    const size_t sizes[] = {0, 1, 7, 8, 9, 15, 16, 17, 33, 1000, 4099};
+    for (int kb = 1; kb <= 2; ++kb)
+        for (int nt = 0; nt < 2; ++nt)
+            for (size_t npx : sizes)
+                for (size_t dof = 0; dof < 40; dof += 4) {  // destination offsets in bytes (RGBA8: 4-aligned)
+                    std::vector<uint8_t> keys(npx * kb + 1), dst(4 * npx + dof + 8, 0xA5);
+                    for (auto& b : keys) b = (uint8_t)rng();
+                    dips_host::expand_keys(dst.data() + dof, keys.data(), npx, kb, nt != 0);
+                    for (size_t i = 0; i < dof; ++i) bad += dst[i] != 0xA5;
+                    for (size_t p = 0; p < npx; ++p) {
+                        const uint8_t r = keys[kb * p], g = kb == 1 ? r : keys[2 * p + 1];
+                        const uint8_t want[4] = {r, g, r < g ? r : g, 255};
+                        for (int c = 0; c < 4; ++c) bad += dst[dof + 4 * p + c] != want[c];
+                    }
+                    for (size_t i = dof + 4 * npx; i < dst.size(); ++i) bad += dst[i] != 0xA5;
+                }
+    std::printf("bad=%d\n", bad);
+    return bad != 0;
+}
+"""
+
+
+def test_expand_keys_rebuilds_rgba(tmp_path):
+    """copy_pool.h expand_keys: the per-pixel keys of the zero-copy per-frame
+    output (one byte gray / two bytes R, G; compat_main_host_kernel out_key)
+    become (k, k, k, 255) / (r, g, min(r, g), 255) for every length and
+    destination offset, AVX2 and streaming stores included, and nothing
+    outside the destination is written."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dips_amd", "csrc")
+    src = tmp_path / "keys_check.cpp"
+    src.write_text(_KEYS_CHECK)
+    exe = tmp_path / "keys_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", f"-I{csrc}", str(src), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout + r.stderr

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""compact_out_ab.py -- one 4K RGBA8 frame per call (the reference's pattern,
+dips/src/lib.rs:233-246), the zero-copy output as RGBA8 texels
+(DIPS_COMPACT_OUT=0) against per-pixel keys expanded by the copy-out threads
+(the default: 1 byte gray, 2 bytes colorized), alternated in one process, for
+dips_frame_callback and for the add_texture + dispatch pair, colorize off and
+on.  Every output of every variant is compared with the first variant's."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from dips_amd import ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, PixelFormat
+
+    W, H = 3840, 2160
+    F = int(sys.argv[1]) if len(sys.argv) > 1 else 48
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    dev = torch.empty((F, H, W, 4), dtype=torch.uint8, device="cuda")
+    op = DiffSeriesOperator(PixelFormat.RGBA8)
+    op.synth_device(dev, W, H, 0xD1B5, 0)
+    op.close()
+    host = dev.cpu().numpy()
+    del dev
+    out = np.zeros((H, W, 4), dtype=np.uint8)
+    res = {}
+    for colorize in (False, True):
+        cs = ComputeState(colorize, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+        lib, hd = cs._hd._lib, cs._hd
+        for t in range(8):  # warm: steady state before the timed passes
+            hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
+                                             out.ctypes.data, out.nbytes))
+        want = {}
+        for rnd in range(rounds):
+            order = [("rgba", "0", "2"), ("keys px1", "1", "1"), ("keys px2", "1", "2")]
+            for name, env, px in (order if rnd % 2 == 0 else order[::-1]):
+                os.environ["DIPS_COMPACT_OUT"] = env
+                os.environ["DIPS_HOST_PX"] = px
+                for call in ("frame_callback", "add+dispatch"):
+                    ok = True
+                    dt = 0.0
+                    # each pass replays frames 8..F-1 after the same 3-frame
+                    # prefix F-3..F-1, so every pass sees the same ring
+                    for pos, t in enumerate(list(range(F - 3, F)) + list(range(8, F))):
+                        t0 = time.perf_counter()
+                        if call == "frame_callback":
+                            hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
+                                                             out.ctypes.data, out.nbytes))
+                        else:
+                            hd.check(lib.dips_add_texture(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes))
+                            hd.check(lib.dips_dispatch(hd.ptr, out.ctypes.data, out.nbytes))
+                        dt += time.perf_counter() - t0
+                        if pos in (3, F // 2, F - 6):  # the same pass position sees the same ring
+                            key = (colorize, pos)
+                            if key not in want:
+                                want[key] = out.copy()
+                            ok = ok and bool(np.array_equal(out, want[key]))
+                    n = F - 8 + 3
+                    k = f"{call} colorize={colorize} {name}"
+                    res.setdefault(k, []).append(n / dt)
+                    print(json.dumps({"variant": k, "round": rnd, "frames_per_s": round(n / dt, 1),
+                                      "ms_per_frame": round(dt / n * 1e3, 4),
+                                      "outputs_equal_first_variant": ok}), flush=True)
+        cs.close()
+    os.environ.pop("DIPS_COMPACT_OUT", None)
+    os.environ.pop("DIPS_HOST_PX", None)
+    for k, v in res.items():
+        print(json.dumps({"variant": k, "summary": True, "median_frames_per_s": round(float(np.median(v)), 1)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

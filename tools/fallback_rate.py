@@ -46,7 +46,17 @@ def main():
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     from oracle import oracle
 
+    cases = []
     for name, W, H, C, off, generic in CASES:
+        cases.append((name, W, H, C, off, generic, None))
+        if C == 3 and not generic and ((W * H * C) % 4 or off % 4):
+            # the same unaligned batch with the byte-unaligned 12-B loads (A/B)
+            cases.append((name + " [DIPS_SERIES_ALIGN=0]", W, H, C, off, generic, "0"))
+    for name, W, H, C, off, generic, align_env in cases:
+        if align_env is None:
+            os.environ.pop("DIPS_SERIES_ALIGN", None)
+        else:
+            os.environ["DIPS_SERIES_ALIGN"] = align_env
         F = args.frames if C != 1 else args.frames * 4
         fb = W * H * C
         flat = torch.empty(F * fb + 64, dtype=torch.uint8, device="cuda")
