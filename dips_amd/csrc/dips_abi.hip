@@ -543,11 +543,13 @@ int compact_out_keys(const dips_handle* h) {
     return h->p.colorize ? 2 : 1;
 }
 
-// Two pixels per thread in the keyed zero-copy kernel (DIPS_HOST_PX=1: one,
-// A/B).  Read on the calling thread: the launches run on the copy pool's.
+// Two pixels per thread in the keyed zero-copy kernel (DIPS_HOST_PX=2; the
+// default one pixel per thread measured faster: 1,042-1,089 against 950-975
+// 4K frames/s, profiles/r03/compact_out_ab_px.jsonl).  Read on the calling
+// thread: the launches run on the copy pool's.
 uint32_t host_pairs() {
     const char* e = std::getenv("DIPS_HOST_PX");
-    return (e && e[0] == '1') ? 0u : 1u;
+    return (e && e[0] == '2') ? 1u : 0u;
 }
 
 // Deferral of host frames in steady state (DIPS_DEFER_UPLOAD=0 turns it off).

@@ -9,7 +9,7 @@
 // device by tools/i2check.hip).  J enters one v_fma_mix_f32 as J * 2^-9 (a
 // normal f16) and E comes from the exponent field of the f16 value c * 2^-9
 // (one packed f16 multiply + an AND).  Results live in the exactly scaled
-// domain I2s = 2 * I * 2^22 (X32: I * 2^28, see norm_h2).
+// domain I2s = 2 * I * 2^22.
 #pragma once
 
 #include "series_common.h"
@@ -41,15 +41,8 @@ __device__ __forceinline__ float fma_mix_hi(uint32_t j, float k, uint32_t e) {
 }
 
 // c * 2^-9 as normal f16s from the u16 pair read as f16 denormals
-// (c * 2^-24) times 2^15 (exact); with X32, c * 2^-4 (times 2^20, still
-// exact: c * 2^-4 <= 15.94 and J * 2^-4 <= 31.9 are normal f16 with room
-// for J's 9 bits), which makes every intensity below come out 32 times as
-// large at no cost: J * 2^-4 * kI2Mul + E * 2^-4 = 32 (J * 65793 / 4 + E / 512).
-template <bool X32 = false>
-__device__ __forceinline__ h2 norm_h2(h2 c) {
-    constexpr float f = X32 ? 1048576.0f : 32768.0f;
-    return c * (h2){(_Float16)f, (_Float16)f};
-}
+// (c * 2^-24) times 2^15 (exact).
+__device__ __forceinline__ h2 norm_h2(h2 c) { return c * (h2){(_Float16)32768.0f, (_Float16)32768.0f}; }
 // sign and exponent bits only: the largest power of two <= x (0 for 0)
 __device__ __forceinline__ h2 pow2_floor_h2(h2 x) {
     return __builtin_bit_cast(h2, __builtin_bit_cast(uint32_t, x) & 0xFC00FC00u);
@@ -61,6 +54,10 @@ struct St2 {
     f32x2 i[2];
 };
 
+// X32: the same intensities times 32 (I2s * 32 = I * 2^28): k * 32 is a
+// free constant, E * 32 one packed f16 multiply per pixel pair (E * 2^-9 <=
+// 0.5, so E * 2^-4 <= 16 stays exact), and the fused multiply-add rounds the
+// exactly scaled sum -- a power-of-two scaling of the same f32 results.
 template <int C, int CH, bool X32 = false>
 __device__ __forceinline__ void derive_v2(const uint32_t (&d)[Fmt<C>::NDW], St2& s) {
     u16x2 r[2], g[2], b[2];
@@ -78,10 +75,13 @@ __device__ __forceinline__ void derive_v2(const uint32_t (&d)[Fmt<C>::NDW], St2&
         } else {
             mx = mn = __builtin_bit_cast(h2, CH == 1 ? r[k] : (CH == 2 ? g[k] : b[k]));
         }
-        const h2 xn = norm_h2<X32>(mx), nn = norm_h2<X32>(mn);
+        const h2 xn = norm_h2(mx), nn = norm_h2(mn);
         const uint32_t jn = __builtin_bit_cast(uint32_t, xn + nn);  // J * 2^-9, exact
-        const uint32_t e = __builtin_bit_cast(uint32_t, pow2_floor_h2(xn) + pow2_floor_h2(nn));
-        s.i[k] = f32x2{fma_mix_lo(jn, kI2Mul, e), fma_mix_hi(jn, kI2Mul, e)};
+        h2 eh = pow2_floor_h2(xn) + pow2_floor_h2(nn);
+        if constexpr (X32) eh = eh * (h2){(_Float16)32.0f, (_Float16)32.0f};
+        const uint32_t e = __builtin_bit_cast(uint32_t, eh);
+        constexpr float kmul = X32 ? kI2Mul * 32.0f : kI2Mul;
+        s.i[k] = f32x2{fma_mix_lo(jn, kmul, e), fma_mix_hi(jn, kmul, e)};
     }
 }
 

@@ -588,7 +588,7 @@ const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, boo
 
 // gray: dI > tau on the f32 intensity; RGB(A) v2: |dI2s| > tau * 2^23 with
 // I2s = 2 I * 2^22 (exact power-of-two scalings of the reference comparison)
-// (integer-sum form, isi: |dI| * 2^28 > tau * 2^28, series_v2.hip)
+// (integer-sum form, isi: intensities x32, series_v2.hip ISI)
 float series_threshold(int channels, float tau, bool isi) {
     return channels == 1 ? tau : tau * (isi ? 268435456.0f : 8388608.0f);
 }

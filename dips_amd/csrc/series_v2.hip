@@ -37,13 +37,14 @@ constexpr float kSjMul = 255.0f / 4194304.0f;
 
 // The integer intensity sum (ISI): for tau >= 2^-5 every selected dI is an
 // f32 in [2^-5, 1] whose ulp is >= 2^-28, so a = |dI| * 2^28 -- the
-// difference of intensities taken 32 times as large (norm_h2<true>, an exact
-// power-of-two scaling of the reference's f32 subtraction) -- is an integer
-// <= 2^28 for every selected pixel: one v_cvt_u32_f32 + v_add_u32 per pixel
-// instead of v_cvt_f64_f32 + v_add_f64 (the f64 add is the most
-// power-hungry VALU class this kernel issues, profiles/
-// r02_energy_per_instruction.jsonl).  Two accumulators of 8 pixels each stay
-// below 2^31.  The record carries n = sum dI * 2^32 = 16 sum a as H = n >> 15,
+// intensities taken 32 times as large (derive_v2<X32>, an exact power-of-two
+// scaling of the reference's f32 arithmetic; threshold and SJ multiplier
+// scaled with them) -- is an integer <= 2^28 for every selected pixel: one
+// v_cvt_u32_f32 and an integer add per pixel replace v_cvt_f64_f32 +
+// v_add_f64 (the f64 add is the most power-hungry VALU class this kernel
+// issues, profiles/r02_energy_per_instruction.jsonl), for one packed f16
+// multiply per pixel pair.  Two accumulators of 8 pixels each stay below
+// 2^31.  The record carries n = sum dI * 2^32 = 16 sum a as H = n >> 15,
 // L = n mod 2^15, exactly as the f64 form.
 constexpr float kIsiMinTau = 0.03125f;  // 2^-5
 
@@ -257,10 +258,21 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
         // ALIGN: the vec bytes of ring slot j in place (done once per frame, at
         // its first use; in 'per-frame' mode the slot then serves as the next
         // frame's reference as it is)
+        // ALIGN: a vec at or past the frame's whole vecs must read as zero,
+        // like the plain form's out-of-range loads; with the descriptor range
+        // rounded up to a whole dword, the vec right after the last whole one
+        // would see the first trailing-pixel bytes in its first dword
+        // (which the generic kernel counts), so that dword is masked
+        uint32_t keep[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) keep[u] = voff + (uint32_t)(u * 64 * F::VB) < vb ? 0xFFFFFFFFu : 0u;
         auto settle = [&](int j) {
             if constexpr (ALIGN) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) funnel3(buf[j][u], sh[j]);
+                for (int u = 0; u < U; ++u) {
+                    funnel3(buf[j][u], sh[j]);
+                    buf[j][u][0] &= keep[u];
+                }
             }
         };
         {
@@ -280,7 +292,10 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                if constexpr (ALIGN) funnel3(dref[u], rsh);
+                if constexpr (ALIGN) {
+                    funnel3(dref[u], rsh);
+                    dref[u][0] &= keep[u];
+                }
                 uint32_t dv[F::NDW];
 #pragma unroll
                 for (int k2 = 0; k2 < F::NDW; ++k2) dv[k2] = dref[u][k2];
