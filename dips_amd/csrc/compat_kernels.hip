@@ -251,6 +251,81 @@ __global__ __launch_bounds__(256) void compat_main_host2_kernel(CompatArgs a) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The same from the packed input (in_key 1 / 2, pack_frame): a pixel is its
+// chroma channel v, or its (max, min) of R, G, B, which is all get_intensity
+// reads (dips_shader.wgsl:64-82): the intensity of (max, min, min) equals the
+// pixel's under chroma None, of (v, v, v) the pixel's under chroma R/G/B.  A
+// raw ring slot (kSlotRaw) receives that texel, whose intensity -- the only
+// thing the ring's readers take from it -- is the frame's.  G = 4 / IN
+// pixels per thread, one 4-byte system-scope load (a wave reads 256
+// contiguous bytes, the one-pixel-per-thread kernel's shape, which measured
+// best); their keys in one store.  Groups at absolute pixel indices
+// multiple of G, so loads and stores are naturally aligned; a group cut by
+// the rows' ends does its pixels one by one.
+template <int IN>
+__device__ __forceinline__ uint32_t packed_texel_in(uint32_t w, int g, uint32_t& mx) {
+    if constexpr (IN == 2) {
+        mx = (w >> (16 * g)) & 0xFFu;
+        const uint32_t mn = (w >> (16 * g + 8)) & 0xFFu;
+        return mx | (mn << 8) | (mn << 16) | 0xFF000000u;
+    } else {
+        mx = (w >> (8 * g)) & 0xFFu;
+        return mx * 0x010101u | 0xFF000000u;
+    }
+}
+
+template <int SLOT_MODE, int IN>
+__global__ __launch_bounds__(256) void compat_main_host_packed_kernel(CompatArgs a) {
+    constexpr int G = 4 / IN;
+    const uint32_t yend = a.y1 ? a.y1 : a.height;
+    const uint64_t p0 = (uint64_t)a.y0 * a.width, p1 = (uint64_t)yend * a.width;
+    const uint64_t q = (p0 / G) * G + (uint64_t)G * ((uint64_t)blockIdx.x * 256u + threadIdx.x);
+    if (q >= p1) return;
+    const uint32_t kb = a.out_key;  // 1 or 2 key bytes per pixel
+    if (q >= p0 && q + G <= p1) {
+        const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a.raw + IN * q), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+        uint64_t keys = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            uint32_t mx;
+            const uint32_t raw = packed_texel_in<IN>(w, g, mx);
+            const float fi = intensity_rgb(raw & 0xFFu, (raw >> 8) & 0xFFu, (raw >> 16) & 0xFFu, a.chroma);
+            const uint32_t t = compat_texel(a, q + (uint64_t)g, fi, SLOT_MODE, raw);
+            keys |= (uint64_t)(kb == 1u ? (t & 0xFFu) : (t & 0xFFFFu)) << (8 * kb * g);
+        }
+        if (kb * G == 2)
+            __hip_atomic_store(reinterpret_cast<uint16_t*>(a.out + q), (uint16_t)keys, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        else if (kb * G == 4)
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + kb * q), (uint32_t)keys, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(a.out + 2 * q), keys, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    for (int g = 0; g < G; ++g) {
+        const uint64_t p = q + (uint64_t)g;
+        if (p < p0 || p >= p1) continue;
+        uint32_t w;
+        if constexpr (IN == 2)
+            w = __hip_atomic_load(reinterpret_cast<const uint16_t*>(a.raw + 2 * p), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            w = __hip_atomic_load(a.raw + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t mx;
+        const uint32_t raw = packed_texel_in<IN>(w, 0, mx);
+        const float fi = intensity_rgb(raw & 0xFFu, (raw >> 8) & 0xFFu, (raw >> 16) & 0xFFu, a.chroma);
+        const uint32_t t = compat_texel(a, p, fi, SLOT_MODE, raw);
+        if (kb == 1u)
+            __hip_atomic_store(a.out + p, (uint8_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            __hip_atomic_store(reinterpret_cast<uint16_t*>(a.out + 2 * p), (uint16_t)t, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // A ring slot as frame_callback leaves it for a W = 1 frame: the gray texel
 // q(get_intensity(frame)) (dips_shader.wgsl:123-126, 187) -- the state
 // compat_main writes in place, rebuilt from a raw frame for resume.
@@ -417,10 +492,36 @@ hipError_t launch_copy_to_host(const uint8_t* src, uint8_t* dst, uint64_t bytes,
     return launch_host_copy<true>(src, dst, bytes, s);
 }
 
+template <int IN>
+static hipError_t launch_packed_in(const CompatArgs& a, dim3 grid, hipStream_t s, int slot_mode) {
+    void (*k)(CompatArgs) = nullptr;
+    switch (slot_mode) {
+        case kSlotQ: k = compat_main_host_packed_kernel<kSlotQ, IN>; break;
+        case kSlotRaw: k = compat_main_host_packed_kernel<kSlotRaw, IN>; break;
+        case kSlotNone: k = compat_main_host_packed_kernel<kSlotNone, IN>; break;
+        default: return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+static hipError_t launch_packed(const CompatArgs& a, dim3 grid, hipStream_t s, int slot_mode) {
+    if (a.in_key == 2u) return launch_packed_in<2>(a, grid, s, slot_mode);
+    if (a.in_key == 1u) return launch_packed_in<1>(a, grid, s, slot_mode);
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, int slot_mode) {
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
     const uint64_t n_px = (uint64_t)(yend - a.y0) * a.width;
+    if (a.out_key != 0u && a.in_key != 0u) {
+        const uint32_t G = 4u / a.in_key;
+        const uint64_t p0 = (uint64_t)a.y0 * a.width, p1 = (uint64_t)yend * a.width;
+        const uint64_t groups = (p1 + G - 1) / G - p0 / G;
+        const dim3 gp((uint32_t)((groups + 255) / 256));
+        return launch_packed(a, gp, s, slot_mode);
+    }
     if (a.out_key != 0u && a.host_pairs != 0u) {
         // two pixels per thread over the absolute pixel pairs the rows touch
         const uint64_t p0 = (uint64_t)a.y0 * a.width, p1 = (uint64_t)yend * a.width;

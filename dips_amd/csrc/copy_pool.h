@@ -241,6 +241,72 @@ inline void expand_keys(uint8_t* dst, const uint8_t* keys, size_t npx, int key_b
     }
 }
 
+// The per-frame zero-copy input in the form the kernel needs (compat_main_
+// host_packed_kernel, in_key): the RGBA8 frame's per-pixel (max, min) of
+// R, G, B (in_bytes 2, chroma None: get_intensity uses nothing else) or its
+// one chroma channel ch = 0 / 1 / 2 (in_bytes 1), `npx` pixels from `src` to
+// `dst` (npx * in_bytes bytes): half or a quarter of the frame's bytes over
+// PCIe.
+__attribute__((target("avx2"))) inline void pack_frame_avx2(uint8_t* dst, const uint8_t* src, size_t npx,
+                                                           int in_bytes, int ch, bool nt) {
+    size_t i = 0;
+    if (in_bytes == 2) {
+        // per 128-bit lane: R0..R3 | G0..G3 | B0..B3 of its 4 pixels
+        const __m256i s = _mm256_setr_epi8(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, -1, -1, -1, -1,  //
+                                           0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, -1, -1, -1, -1);
+        for (; i + 16 <= npx; i += 16) {
+            __m256i o[2];
+            for (int h = 0; h < 2; ++h) {
+                const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 4 * (i + 8 * h)));
+                const __m256i t = _mm256_shuffle_epi8(v, s);
+                const __m256i g = _mm256_srli_si256(t, 4), b = _mm256_srli_si256(t, 8);
+                const __m256i mx = _mm256_max_epu8(_mm256_max_epu8(t, g), b);
+                const __m256i mn = _mm256_min_epu8(_mm256_min_epu8(t, g), b);
+                // (max, min) of pixels 0..3 in each lane's low 8 bytes; lanes -> qwords 0, 2
+                o[h] = _mm256_permute4x64_epi64(_mm256_unpacklo_epi8(mx, mn), 0x08);
+            }
+            const __m256i w = _mm256_permute2x128_si256(o[0], o[1], 0x20);
+            put32(dst + 2 * i, w, nt);
+        }
+        for (; i < npx; ++i) {
+            const uint8_t r = src[4 * i], g = src[4 * i + 1], b = src[4 * i + 2];
+            dst[2 * i] = std::max(std::max(r, g), b);
+            dst[2 * i + 1] = std::min(std::min(r, g), b);
+        }
+    } else {
+        // the channel's byte of each of the 4 pixels of a 128-bit lane
+        const char c = (char)ch;
+        const __m256i sel = _mm256_setr_epi8(c, (char)(c + 4), (char)(c + 8), (char)(c + 12), -1, -1, -1, -1, -1, -1, -1,
+                                             -1, -1, -1, -1, -1, c, (char)(c + 4), (char)(c + 8), (char)(c + 12), -1, -1,
+                                             -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
+        const __m256i lanes = _mm256_setr_epi32(0, 4, 0, 0, 0, 0, 0, 0);
+        for (; i + 8 <= npx; i += 8) {
+            const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 4 * i));
+            const __m256i t = _mm256_permutevar8x32_epi32(_mm256_shuffle_epi8(v, sel), lanes);
+            _mm_storel_epi64(reinterpret_cast<__m128i*>(dst + i), _mm256_castsi256_si128(t));
+        }
+        for (; i < npx; ++i) dst[i] = src[4 * i + ch];
+    }
+    if (nt) _mm_sfence();
+}
+
+inline void pack_frame(uint8_t* dst, const uint8_t* src, size_t npx, int in_bytes, int ch, bool nt) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) {
+        pack_frame_avx2(dst, src, npx, in_bytes, ch, nt);
+        return;
+    }
+    for (size_t i = 0; i < npx; ++i) {
+        const uint8_t r = src[4 * i], g = src[4 * i + 1], b = src[4 * i + 2];
+        if (in_bytes == 2) {
+            dst[2 * i] = std::max(std::max(r, g), b);
+            dst[2 * i + 1] = std::min(std::min(r, g), b);
+        } else {
+            dst[i] = src[4 * i + ch];
+        }
+    }
+}
+
 // Host copy in ~4 MiB pieces over the pool.
 inline void pool_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
     const size_t kPiece = 4u << 20;

@@ -543,6 +543,16 @@ int compact_out_keys(const dips_handle* h) {
     return h->p.colorize ? 2 : 1;
 }
 
+// Bytes per pixel of the zero-copy input (W = 1, keyed output only): the
+// copy pool packs each staged piece into what get_intensity reads -- (max,
+// min) of R, G, B (2, chroma None) or the chroma channel (1) -- instead of
+// the RGBA8 texel (0: DIPS_COMPACT_IN=0, A/B).  Read on the calling thread.
+int compact_in_bytes(const dips_handle* h, int out_key) {
+    const char* e = std::getenv("DIPS_COMPACT_IN");
+    if (out_key == 0 || h->p.spatial_window_size != 1 || (e && e[0] == '0')) return 0;
+    return h->p.chroma_filter == DIPS_CHROMA_NONE ? 2 : 1;
+}
+
 // Two pixels per thread in the keyed zero-copy kernel (DIPS_HOST_PX=2; the
 // default one pixel per thread measured faster: 1,042-1,089 against 950-975
 // 4K frames/s, profiles/r03/compact_out_ab_px.jsonl).  Read on the calling
@@ -605,6 +615,7 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
         a.colorize = h->p.colorize ? 1u : 0u;
         a.out_key = (uint32_t)compact_out_keys(h);
         a.host_pairs = host_pairs();
+        a.in_key = (uint32_t)compact_in_bytes(h, (int)a.out_key);
         h->pend_key = (int)a.out_key;
         const size_t row = (size_t)width * 4u;
         h->pend_geom.init(height, row);
@@ -616,7 +627,8 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
                                                            a.y0 = y0;
                                                            a.y1 = y1;
                                                            return dips::launch_compat_main_host(a, st, 1);
-                                                       }));
+                                                       },
+                                                       (int)a.in_key, (int)a.chroma - 1));
         } else {
             // W > 1: the filter needs the whole frame, so the stripes first go
             // into the slot (copy kernels from the pinned buffer, launched as
@@ -637,6 +649,7 @@ dips_status add_texture_impl(dips_handle* h, uint32_t width, uint32_t height, co
             DIPS_HIP(h, dips::launch_compat_filter_frames(dslot, h->raw.as<uint8_t>(), width, height, 1, win,
                                                           h->p.chroma_filter, h->stream));
             a.raw = h->raw.as<uint8_t>();
+            a.in_key = 0;  // (compact_in_bytes is 0 for W > 1 anyway)
             DIPS_HIP(h, h->pieces.ensure(h->pend_geom.n_s));
             for (uint32_t si = 0; si < h->pend_geom.n_s; ++si) {
                 a.y0 = h->pend_geom.y0(si);
@@ -978,6 +991,7 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
         a.out = static_cast<uint8_t*>(dout);
         a.out_key = (uint32_t)compact_out_keys(h);
         a.host_pairs = host_pairs();
+        a.in_key = (uint32_t)compact_in_bytes(h, (int)a.out_key);
         // odd stripes on copy_stream (idle here, synchronised above); every
         // stripe's kernel has finished when the call returns
         const char* one_env = std::getenv("DIPS_DIRECT_STREAMS");  // "1": every stripe on the compute stream (A/B)
@@ -989,7 +1003,7 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
                                                             a.y1 = y1;
                                                             return dips::launch_compat_main_host(a, s);
                                                         },
-                                                        (int)a.out_key));
+                                                        (int)a.out_key, (int)a.in_key, (int)a.chroma - 1));
         return 1;
     }
     DIPS_HIP(h, dips_host::run_striped_frame(frame, out, H, row, h->io.bytes(), h->io_out.bytes(), slot,

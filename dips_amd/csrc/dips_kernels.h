@@ -94,6 +94,9 @@ struct CompatArgs {
                              // 2 two bytes R | G << 8 (colorized: B = min(R, G), A = 255) -- the host
                              // expands them (host_stream.h expand_keys)
     uint32_t host_pairs;     // out_key != 0: two pixels per thread (compat_main_host2_kernel)
+    uint32_t in_key;         // compat_main_host: raw holds RGBA8 texels (0), or per pixel the chroma
+                             // channel (1) / (max, min) of R, G, B (2) (copy_pool.h pack_frame);
+                             // compat_main_host_packed_kernel, out_key 1 / 2 only
 };
 
 // dips ComputeState over a batch in steady state (compat_batch.hip).

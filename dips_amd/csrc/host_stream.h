@@ -247,6 +247,17 @@ inline uint32_t direct_first_rows(uint32_t rows) {
 // copy-out of one piece [o, o + len) of the RGBA8 frame: from pin_out itself
 // (key_bytes 0) or rebuilt from the per-pixel keys the kernel wrote there
 // (key_bytes 1 / 2 per pixel, pin_out + o / 4 * key_bytes; expand_keys).
+// staging of one piece [o, o + len) of the RGBA8 frame: copied as it is
+// (in_bytes 0) or packed into the kernel's input form at pin_in + o / 4 *
+// in_bytes (in_bytes 1 / 2 per pixel: pack_frame, chroma channel ch)
+inline void stage_piece(uint8_t* pin_in, const uint8_t* frame, size_t o, size_t len, int in_bytes, int ch, bool nt) {
+    if (!len) return;
+    if (in_bytes)
+        pack_frame(pin_in + o / 4u * (size_t)in_bytes, frame + o, len / 4u, in_bytes, ch, nt);
+    else
+        host_copy(pin_in + o, frame + o, len, nt);
+}
+
 inline void copy_out_piece(uint8_t* out, const uint8_t* pin_out, size_t o, size_t len, int key_bytes, bool nt) {
     if (!len) return;
     if (key_bytes)
@@ -258,7 +269,8 @@ inline void copy_out_piece(uint8_t* out, const uint8_t* pin_out, size_t o, size_
 template <typename Launch>
 hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t height, size_t row,
                                     uint8_t* pin_in, const uint8_t* pin_out, const hipStream_t (&compute)[2],
-                                    int device, PieceEvents& ev, Launch&& launch, int key_bytes = 0) {
+                                    int device, PieceEvents& ev, Launch&& launch, int key_bytes = 0,
+                                    int in_bytes = 0, int ch = 0) {
     const bool nt = nt_copy();  // on the calling thread, never in the workers
     const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
     const uint32_t first = std::min(height, direct_first_rows(rows));
@@ -291,7 +303,7 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
         const size_t p1 = j + 1 == k ? slen : std::min(slen, (slen * (j + 1) / k) & ~(size_t)63);
         const size_t o = so + p0, len = p1 - p0;
         if (i < n_t) {
-            if (len && frame) host_copy(pin_in + o, frame + o, len, nt);  // frame == nullptr: already staged
+            if (frame) stage_piece(pin_in, frame, o, len, in_bytes, ch, nt);  // frame == nullptr: already staged
             if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != k) return;
             // the stripe's last piece: its kernel and event back to back on the stream
             if (trace) ts[2 * si] = since();
@@ -364,7 +376,7 @@ struct DirectGeom {
 // staged and launched; the kernels may still run (and read `pin_in`).
 template <typename Launch>
 hipError_t direct_stage_launch(const uint8_t* frame, uint8_t* pin_in, const hipStream_t (&compute)[2], int device,
-                               PieceEvents& ev, const DirectGeom& g, Launch&& launch) {
+                               PieceEvents& ev, const DirectGeom& g, Launch&& launch, int in_bytes = 0, int ch = 0) {
     const bool nt = nt_copy();  // on the calling thread, never in the workers
     hipError_t e = ev.ensure(g.n_s);
     if (e != hipSuccess) return e;
@@ -376,7 +388,7 @@ hipError_t direct_stage_launch(const uint8_t* frame, uint8_t* pin_in, const hipS
         const uint32_t si = (uint32_t)(i / g.k), j = (uint32_t)(i % g.k);
         size_t o, len;
         g.piece(si, j, o, len);
-        if (len) host_copy(pin_in + o, frame + o, len, nt);
+        stage_piece(pin_in, frame, o, len, in_bytes, ch, nt);
         if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != g.k) return;
         std::lock_guard<std::mutex> lk(launch_mu);
         hipStream_t cs = compute[si & 1u];

@@ -222,3 +222,55 @@ def test_expand_keys_rebuilds_rgba(tmp_path):
     subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", f"-I{csrc}", str(src), "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout + r.stderr
+
+
+_PACK_CHECK = r"""
+#include "copy_pool.h"
+#include <cstdio>
+#include <random>
+#include <vector>
+int main() {
+    std::mt19937_64 rng(5);
+    int bad = 0;
+    const size_t sizes[] = {0, 1, 7, 8, 15, 16, 17, 31, 33, 1000, 4099};
+    for (int ib = 1; ib <= 2; ++ib)
+        for (int ch = 0; ch < (ib == 1 ? 3 : 1); ++ch)
+            for (int nt = 0; nt < 2; ++nt)
+                for (size_t npx : sizes)
+                    for (size_t so = 0; so < 12; so += 4) {
+                        std::vector<uint8_t> src(4 * npx + so + 4), dst(ib * npx + 64, 0xA5);
+                        for (auto& b : src) b = (uint8_t)rng();
+                        dips_host::pack_frame(dst.data() + 32, src.data() + so, npx, ib, ch, nt != 0);
+                        for (size_t i = 0; i < 32; ++i) bad += dst[i] != 0xA5;
+                        for (size_t p = 0; p < npx; ++p) {
+                            const uint8_t* px = src.data() + so + 4 * p;
+                            const uint8_t mx = std::max(std::max(px[0], px[1]), px[2]);
+                            const uint8_t mn = std::min(std::min(px[0], px[1]), px[2]);
+                            if (ib == 2) bad += dst[32 + 2 * p] != mx || dst[32 + 2 * p + 1] != mn;
+                            else bad += dst[32 + p] != px[ch];
+                        }
+                        for (size_t i = 32 + ib * npx; i < dst.size(); ++i) bad += dst[i] != 0xA5;
+                    }
+    std::printf("bad=%d\n", bad);
+    return bad != 0;
+}
+"""
+
+
+def test_pack_frame_for_the_zero_copy_input(tmp_path):
+    """copy_pool.h pack_frame: the per-frame zero-copy input as the kernel
+    reads it (compat_main_host_packed_kernel in_key) -- per-pixel (max, min)
+    of R, G, B, or one chroma channel -- for every length, source offset and
+    channel, AVX2 and streaming stores included, nothing written outside."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dips_amd", "csrc")
+    src = tmp_path / "pack_check.cpp"
+    src.write_text(_PACK_CHECK)
+    exe = tmp_path / "pack_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", f"-I{csrc}", str(src), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout + r.stderr

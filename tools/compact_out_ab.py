@@ -2,9 +2,10 @@
 """compact_out_ab.py -- one 4K RGBA8 frame per call (the reference's pattern,
 dips/src/lib.rs:233-246), the zero-copy output as RGBA8 texels
 (DIPS_COMPACT_OUT=0) against per-pixel keys expanded by the copy-out threads
-(the default: 1 byte gray, 2 bytes colorized), alternated in one process, for
-dips_frame_callback and for the add_texture + dispatch pair, colorize off and
-on.  Every output of every variant is compared with the first variant's."""
+(1 byte gray, 2 bytes colorized), with the RGBA8 input (DIPS_COMPACT_IN=0) or
+the packed one (the default: (max, min) or the chroma channel), alternated in
+one process, for dips_frame_callback and for the add_texture + dispatch pair,
+colorize off / on and chroma None / Green.  Every output of every variant is compared with the first variant's."""
 from __future__ import annotations
 
 import json
@@ -33,18 +34,19 @@ def main():
     del dev
     out = np.zeros((H, W, 4), dtype=np.uint8)
     res = {}
-    for colorize in (False, True):
-        cs = ComputeState(colorize, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+    for colorize, chroma in ((False, ChromaFilter.None_), (True, ChromaFilter.None_), (False, ChromaFilter.Green)):
+        cs = ComputeState(colorize, 1, 5.0, DiPsFilter.Sigmoid, chroma)
         lib, hd = cs._hd._lib, cs._hd
         for t in range(8):  # warm: steady state before the timed passes
             hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
                                              out.ctypes.data, out.nbytes))
         want = {}
         for rnd in range(rounds):
-            order = [("rgba", "0", "2"), ("keys px1", "1", "1"), ("keys px2", "1", "2")]
-            for name, env, px in (order if rnd % 2 == 0 else order[::-1]):
+            order = [("rgba in, rgba out", "0", "0"), ("rgba in, keys out", "1", "0"),
+                     ("packed in, keys out", "1", "1")]
+            for name, env, cin in (order if rnd % 2 == 0 else order[::-1]):
                 os.environ["DIPS_COMPACT_OUT"] = env
-                os.environ["DIPS_HOST_PX"] = px
+                os.environ["DIPS_COMPACT_IN"] = cin
                 for call in ("frame_callback", "add+dispatch"):
                     ok = True
                     dt = 0.0
@@ -60,19 +62,19 @@ def main():
                             hd.check(lib.dips_dispatch(hd.ptr, out.ctypes.data, out.nbytes))
                         dt += time.perf_counter() - t0
                         if pos in (3, F // 2, F - 6):  # the same pass position sees the same ring
-                            key = (colorize, pos)
+                            key = (colorize, int(chroma), pos)
                             if key not in want:
                                 want[key] = out.copy()
                             ok = ok and bool(np.array_equal(out, want[key]))
                     n = F - 8 + 3
-                    k = f"{call} colorize={colorize} {name}"
+                    k = f"{call} colorize={colorize} chroma={int(chroma)} {name}"
                     res.setdefault(k, []).append(n / dt)
                     print(json.dumps({"variant": k, "round": rnd, "frames_per_s": round(n / dt, 1),
                                       "ms_per_frame": round(dt / n * 1e3, 4),
                                       "outputs_equal_first_variant": ok}), flush=True)
         cs.close()
     os.environ.pop("DIPS_COMPACT_OUT", None)
-    os.environ.pop("DIPS_HOST_PX", None)
+    os.environ.pop("DIPS_COMPACT_IN", None)
     for k, v in res.items():
         print(json.dumps({"variant": k, "summary": True, "median_frames_per_s": round(float(np.median(v)), 1)}),
               flush=True)
