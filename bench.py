@@ -85,6 +85,15 @@ def parse():
     return ap.parse_args()
 
 
+def _v2_kernel_name(per_frame: bool, tau: float, with_map: bool = False) -> str:
+    """The series_v2_kernel instantiation the library runs for an aligned RGB8
+    batch (series_v2.hip: <C, CH, U, PF, MAP, ALIGN, ISI>; ISI for tau >= 2^-5
+    unless DIPS_SERIES_ISI=0)."""
+    isi = tau >= 0.03125 and os.environ.get("DIPS_SERIES_ISI", "1")[:1] != "0"
+    b = lambda v: "true" if v else "false"  # noqa: E731
+    return f"series_v2_kernel<3,0,4,{b(per_frame)},{b(with_map)},false,{b(isi)}>"
+
+
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
@@ -328,7 +337,7 @@ def _map_variant(torch, op_cls, frames, n, W, H, mode_pf, tau):
             ok = ok and bool(torch.equal(dmap[k], want))
         kms = float(np.median(each))
         algo = 2 * n * fb
-        return {"kernel": f"series_v2_kernel<3,0,4,{'true' if mode_pf else 'false'},true>",
+        return {"kernel": _v2_kernel_name(mode_pf, tau, with_map=True),
                 "frames": n, "frames_per_s": round(n / (kms / 1e3), 1), "wall_frames_per_s": round(n / wall, 1),
                 "kernel_ms_median": round(kms, 4), "launches": len(each),
                 "algorithmic_bytes_per_launch": algo, "achieved_GBps": round(algo / (kms / 1e3) / 1e9, 1),
@@ -438,7 +447,7 @@ def _config_leg(torch, dist, buf, *, name, W, H, F, mode, tau, steps, world, ran
                 "kernel_ms": round(kms, 4), "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
                 "rccl_gather_ms": round(gather_ms, 4) if world > 1 else 0.0,
                 "rccl_reference_ms": round(ref_ms, 4) if world > 1 else 0.0,
-                "kernel": f"series_v2_kernel<3,0,4,{'true' if mode == Mode.PerFrame else 'false'},false>",
+                "kernel": _v2_kernel_name(mode == Mode.PerFrame, tau),
                 "check": chk}
     finally:
         op.close()
@@ -495,15 +504,19 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
     rec = {"frames_per_s": round(n_timed / tot, 1), "calls": n_timed,
            "ms_per_call_median": round(float(np.median(times)) * 1e3, 4),
            "ms_per_call_p90": round(float(np.percentile(times, 90)) * 1e3, 4),
-           "host_to_device_GBps": round(n_timed * fb / tot / 1e9, 2),
-           "device_to_host_GBps": round(n_timed * fb / tot / 1e9, 2),
+           "host_to_device_GBps": round(n_timed * W * H * 2 / tot / 1e9, 2),
+           "device_to_host_GBps": round(n_timed * W * H / tot / 1e9, 2),
+           "rgba8_GBps_each_way": round(n_timed * fb / tot / 1e9, 2),
            "outputs_equal_batch_path": equal,
            "workload": "3840x2160 RGBA8, DiPsProperties defaults (Unfiltered, window 1, no colour); "
                        f"{warm} untimed calls, then {n_timed} timed dips_frame_callback calls from pageable "
                        "host memory into a reused host output buffer",
-           "path": "zero-copy stripes: the copy pool stages each row stripe into pinned memory and launches "
-                   "compat_main_host_kernel on it (PCIe reads + writes by the kernel), stripes copied out as "
-                   "their events fire (dips_abi.hip frame_callback_striped)"}
+           "path": "zero-copy stripes: the copy pool packs each row stripe into pinned memory as what "
+                   "get_intensity reads ((max, min) of R, G, B: 2 B/px), and launches "
+                   "compat_main_host_packed_kernel on it (PCIe reads of the packed stripe, 1-B gray keys "
+                   "written back over PCIe); the pool expands the keys into the RGBA8 output as each stripe's "
+                   "event fires (dips_abi.hip frame_callback_striped, copy_pool.h pack_frame / expand_keys)",
+           "pcie_bytes_each_way_per_frame": {"host_to_device": W * H * 2, "device_to_host": W * H}}
     return rec, (host[:warm].copy(), want[:warm].copy())
 
 
@@ -750,7 +763,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": f"series_v2_kernel<3,0,4,{'true' if mode == Mode.PerFrame else 'false'},false>",
+                "kernel": _v2_kernel_name(mode == Mode.PerFrame, args.tau),
                 "kernel_ms": round(kernel_ms, 4),
                 "kernel_ms_median": round(float(np.median(each)), 4) if world == 1 and each else None,
                 "kernel_launches_timed": len(each),
