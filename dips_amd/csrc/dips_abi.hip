@@ -236,20 +236,22 @@ FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t nvec = npx / 16u;
     if (nvec == 0 || npx >= (1ull << 31) || n_frames == 0) return g;
-    const uint64_t U = (uint64_t)(gray_lut_layout() == 2 ? dips::gray_lut_unroll() : dips::kUnrollGrayLut);
+    const int alu = gray_lut_layout() == 2 ? dips::gray_alu_vecs(h->p.tau) : 0;
+    const uint64_t U = (uint64_t)(gray_lut_layout() == 2 ? (alu > 0 ? 4 : dips::gray_lut_unroll()) : dips::kUnrollGrayLut);
+    const uint64_t gw = dips::gray_lut_waves(gray_lut_layout(), alu);
     g.vec_bytes = nvec * 16u;
     g.tail_px0 = nvec * 16u;
     g.n_tiles = (nvec + 64 * U - 1) / (64 * U);
     g.items = g.n_tiles * n_frames;
-    // one 1024-thread group per CU (the tables fill its LDS): 4 waves per SIMD
-    uint64_t per_simd = dips::kGrayLutWaves / 4u;
+    // one group per CU (the tables fill its LDS): 4 (3) waves per SIMD
+    uint64_t per_simd = gw / 4u;
     if (const char* cap = std::getenv("DIPS_SERIES_WAVES_PER_SIMD")) {
         const unsigned long c = std::strtoul(cap, nullptr, 10);
         if (c >= 1 && c < per_simd) per_simd = c;
     }
     const uint64_t resident = per_simd * 4u * (uint64_t)h->cu_count;
     g.n_waves = g.items < resident ? g.items : resident;
-    g.blocks = (g.n_waves + dips::kGrayLutWaves - 1) / dips::kGrayLutWaves;
+    g.blocks = (g.n_waves + gw - 1) / gw;
     g.ok = g.n_tiles < (1ull << 32) && g.blocks < (1ull << 31);
     return g;
 }
@@ -341,7 +343,9 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         a.thr = dips::series_threshold(C, h->p.tau, isi);
         if (glut) {
             a.lut = h->gray_lut.p;
-            DIPS_HIP(h, dips::launch_series_gray_lut(a, pf, map != nullptr, h->gray_lut_layout, (uint32_t)g.blocks, s));
+            const int alu = h->gray_lut_layout == 2 ? dips::gray_alu_vecs(h->p.tau) : 0;
+            DIPS_HIP(h, dips::launch_series_gray_lut(a, pf, map != nullptr, h->gray_lut_layout, (uint32_t)g.blocks, s,
+                                                     alu));
         } else {
             DIPS_HIP(h, dips::launch_series_fast(a, C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map != nullptr,
                                                  (uint32_t)g.blocks, s, align, isi));

@@ -21,6 +21,15 @@ constexpr int kUnrollV2 = 4;    // series_v2_kernel (RGB8/RGBA8): 1024 px / wave
 #endif
 constexpr int kUnrollGrayLut = DIPS_UNROLL_GRAY_LUT;
 int gray_lut_unroll();  // U of this call's GRAY8 table kernel (DIPS_GRAY_LUT_U for A/B runs)
+// Arithmetic vecs of the U = 4 table kernel for tau >= 2^-5 (series_gray.hip)
+#ifndef DIPS_GRAY_ALU_VECS
+#define DIPS_GRAY_ALU_VECS 0
+#endif
+constexpr int kGrayAluVecs = DIPS_GRAY_ALU_VECS;
+#ifndef DIPS_GRAY_ALU_WAVES
+#define DIPS_GRAY_ALU_WAVES 12
+#endif
+constexpr uint32_t kGrayAluWaves = DIPS_GRAY_ALU_WAVES;
 constexpr uint32_t kGrayLutWaves = 16;  // its waves per workgroup (one 1024-thread group per CU)
 constexpr size_t kGrayLutBytes = 131072;  // its T_d / T_c tables
 // Prefetch depth: frames of loads each wave keeps in flight.
@@ -236,10 +245,12 @@ hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, boo
 hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
                                 dips_series_entry* series, hipStream_t s);
 // GRAY8 table kernel, table layout 1 (two byte tables) or 2 (one u16 table)
-const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout);
+const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs = 0, uint32_t waves = 16);
+int gray_alu_vecs(float tau);          // arithmetic vecs of this call's table kernel (0 for tau < 2^-5)
+uint32_t gray_lut_waves(int layout, int alu_vecs);  // waves per group of the table kernel
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s);
 hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
-                                  hipStream_t s);
+                                  hipStream_t s, int alu_vecs = 0);
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
 hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, hipStream_t s);

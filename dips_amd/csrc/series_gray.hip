@@ -54,6 +54,54 @@ constexpr uint32_t kGrayV = 8421504u;          // V = kGrayV * d + corr
 // reference dword is swizzled once before the index perms).
 constexpr uint32_t kGraySwizzle = 0x3Cu;
 
+// The arithmetic vecs (NA of the U vecs per lane, tau >= 2^-5 only).  The
+// table path is bound by its LDS gathers (profiles/r03/gray_lds_counters.json:
+// the LDS array busy 96 % of the kernel, 6.9 LDS cycles per wave-wide
+// ds_read_u16, 4.9 of them bank conflicts) while the VALU idles a third of
+// the time, so NA of the U vecs skip the table and compute the same numbers
+// from the spec: U'(c) = 2^28 u(c) = fma(c, 2^28 K_HI, c * 2^28 K_LO) exactly
+// (the unorm identity of series_common.h, scaled by a power of two),
+// D' = RN(U'(a) - U'(b)) = 2^28 RN(u(a) - u(b)) exactly, the pixel is
+// selected when |D'| > 2^28 tau, and then, dI >= tau >= 2^-5 having an ulp of
+// at least 2^-28, |D'| = dI 2^28 = V / 8 is an integer below 2^28 (v_cvt_u32
+// exact).  Per lane the selected |D'| of 8 pixels fit a u32 (< 2^31); their
+// sum S splits as S = 1052688 sum d + sum corr / 8 (8421504 = 8 * 1052688,
+// corr a multiple of 8, sum corr / 8 < 1052688), which lands in the record's
+// sum d / sum corr fields.  Per frame, a PF reference's U' is the previous
+// frame's, kept in registers.
+constexpr float kGrayAluHi = 0x1.010102p20f;   // kUnormHi * 2^28
+constexpr float kGrayAluLo = -0x1.fdfdfep-5f;  // kUnormLo * 2^28
+constexpr uint32_t kGrayAluDiv = 1052688u;     // 8421504 / 8
+constexpr float kGrayAluMinTau = 0.03125f;     // 2^-5
+
+__device__ __forceinline__ void gray_alu_unorm4(uint32_t w, f32x2& u01, f32x2& u23) {
+    const f32x2 c01 = {(float)(w & 0xFFu), (float)((w >> 8) & 0xFFu)};
+    const f32x2 c23 = {(float)((w >> 16) & 0xFFu), (float)(w >> 24)};
+    const f32x2 hi = {kGrayAluHi, kGrayAluHi}, lo = {kGrayAluLo, kGrayAluLo};
+    u01 = __builtin_elementwise_fma(c01, hi, c01 * lo);
+    u23 = __builtin_elementwise_fma(c23, hi, c23 * lo);
+}
+
+// Four pixels (frame dword f, reference dword r): the selected |D'| added to
+// sv, the number selected (wave-wide, on the scalar unit) to cnt.
+__device__ __forceinline__ void gray_alu_dword(uint32_t f, uint32_t r, float thr28, uint32_t& sv, uint32_t& cnt) {
+    // opaque copy: the reference's U' is derived again, not kept from the
+    // previous frame (that costs 16 VGPRs the table path needs)
+    asm volatile("" : "+v"(r));
+    f32x2 f01, f23, r01, r23;
+    gray_alu_unorm4(f, f01, f23);
+    gray_alu_unorm4(r, r01, r23);
+    const f32x2 d01 = f01 - r01, d23 = f23 - r23;
+    const float d[4] = {fabsf(d01.x), fabsf(d01.y), fabsf(d23.x), fabsf(d23.y)};
+#pragma unroll
+    for (int p = 0; p < 4; p += 2) {
+        const bool s0 = d[p] > thr28, s1 = d[p + 1] > thr28;
+        cnt += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(s0)) +
+               (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(s1));
+        sv = sv + (s0 ? (uint32_t)d[p] : 0u) + (s1 ? (uint32_t)d[p + 1] : 0u);
+    }
+}
+
 // The tables for threshold tau (65,536 spec evaluations), 131,072 bytes:
 // layout 1 -- T_d at byte 0 and T_c at byte kGrayLutTcOffset;
 // layout 2 -- one u16 table, entry d | corr << 8 at byte 2 idx.
@@ -94,12 +142,28 @@ __device__ __forceinline__ void gstore_one(__amdgpu_buffer_rsrc_t rpart, uint32_
 
 // One frame of one tile against the reference bytes rb: the 4 per-lane
 // values {SAD, sum d, sum corr, 0} and the wave-wide count.
-template <int U, bool MAP, int LAYOUT>
+// NA > 0 (layout 2): vecs U - NA .. U - 1 take the arithmetic path.
+template <int U, int NA, bool MAP, int LAYOUT>
 __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* lds, const uint32_t (&rb)[U][4],
-                                           const uint32_t (&cur)[U][4], uint32_t voff, uint32_t t, uint32_t* vals,
-                                           uint32_t& cnt) {
+                                           const uint32_t (&cur)[U][4], float thr28, uint32_t voff,
+                                           uint32_t t, uint32_t* vals, uint32_t& cnt) {
+    static_assert(NA == 0 || (LAYOUT == 2 && NA < U), "arithmetic vecs: layout 2, at least one table vec");
     uint32_t sad = 0, acc = 0, accd = 0, accc = 0, c = 0;
     uint32_t map[U][4];
+    uint32_t alu_s[NA > 0 ? 2 * NA : 1], alu_c = 0;
+    if constexpr (NA > 0) {
+#pragma unroll
+        for (int x = 0; x < NA; ++x) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint32_t sv = 0;
+#pragma unroll
+                for (int k = 2 * h; k < 2 * h + 2; ++k)
+                    gray_alu_dword(cur[U - NA + x][k], rb[U - NA + x][k], thr28, sv, alu_c);
+                alu_s[2 * x + h] = sv;
+            }
+        }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -107,6 +171,7 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
             const uint32_t f = cur[u][k], r = rb[u][k];
             sad = __builtin_amdgcn_sad_u8(f, r, sad);
             if constexpr (MAP) map[u][k] = absdiff_bytes(f, r);
+            if (u >= U - NA) continue;
             // table indices f_i * 256 + r_i of pixels (0, 2) and (1, 3) as u16
             // pairs (layout 2: r_i ^ sw(f_i), per byte of the dword at once)
             const uint32_t rs = LAYOUT == 2 ? r ^ ((f << 2) & (kGraySwizzle * 0x01010101u)) : r;
@@ -146,10 +211,20 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
         // sb = accc, s0 = accd, s1 = acc (all < 2^22 for 64 px per lane):
         // sum corr = (s0 - sb) / 255, sum d = sb - sum corr,
         // count = (s0 + n - s1) / 2
-        constexpr uint32_t n = (uint32_t)U * 16u;
-        const uint32_t sc = (accd - accc) / 255u;
+        constexpr uint32_t n = (uint32_t)(U - NA) * 16u;
+        uint32_t sc = (accd - accc) / 255u;
+        uint32_t sd = accc - sc;
         c = (accd + n - acc) >> 1;
-        acc = (accc - sc) | (sc << 16);  // sum d < 2^15, sum corr < 2^14
+        if constexpr (NA > 0) {
+#pragma unroll
+            for (int g = 0; g < 2 * NA; ++g) {
+                const uint32_t q = alu_s[g] / kGrayAluDiv;
+                sd += q;
+                sc += (alu_s[g] - q * kGrayAluDiv) << 3;
+            }
+            c += (threadIdx.x & 63u) == 0u ? alu_c : 0u;  // alu_c is wave-wide
+        }
+        acc = sd | (sc << 16);  // sum d < 2^15, sum corr < 2^14
     }
     if constexpr (MAP) {
         const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.vec_bytes);
@@ -168,23 +243,24 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
     }
 }
 
-template <int U, bool PF, bool MAP, int LAYOUT>
-__global__ __launch_bounds__(64 * kGrayWaves) void series_gray_lut_kernel(SeriesArgs a) {
+template <int U, bool PF, bool MAP, int LAYOUT, int NA = 0, int GW = kGrayWaves>
+__global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) {
     __shared__ uint32_t lds32[32768];  // T_d at byte 0, T_c at byte kGrayLutTcOffset
     {
         const u32x4* src = reinterpret_cast<const u32x4*>(a.lut);
         u32x4* dst = reinterpret_cast<u32x4*>(lds32);
-        for (uint32_t i = threadIdx.x; i < 8192u; i += 64u * kGrayWaves) dst[i] = src[i];
+        for (uint32_t i = threadIdx.x; i < 8192u; i += 64u * GW) dst[i] = src[i];
     }
     __syncthreads();
     const uint8_t* lds = reinterpret_cast<const uint8_t*>(lds32);
     static_assert(U * 64 * 16 <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)kGrayWaves + (threadIdx.x >> 6));
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)GW + (threadIdx.x >> 6));
     if (wave >= a.n_waves) return;
     const uint32_t fb = a.frame_bytes, vb = a.vec_bytes;
     const uint32_t rec_off8 = (lane & 7u) == 0u ? (lane >> 5) * 16u + ((lane >> 3) & 3u) * 4u : 0x80000000u;
     const uint32_t rec_off4 = (lane & 15u) == 0u ? (lane >> 4) * 4u : 0x80000000u;
+    const float thr28 = a.thr * 268435456.0f;  // 2^28 tau (exact)
 
     uint64_t i = (uint64_t)wave * a.items / a.n_waves;
     const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
@@ -239,11 +315,13 @@ __global__ __launch_bounds__(64 * kGrayWaves) void series_gray_lut_kernel(Series
                     const int j = 2 * h + q;
                     const uint32_t tf = t0 + k + (uint32_t)j;
                     if constexpr (PF) {
-                        gray_frame<U, MAP, LAYOUT>(a, lds, buf[j], buf[(j + 1) & 3], voff, tf, v + 4 * q, q ? c1 : c0);
+                        gray_frame<U, NA, MAP, LAYOUT>(a, lds, buf[j], buf[(j + 1) & 3], thr28, voff, tf,
+                                                       v + 4 * q, q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 3, buf[j]);
                     } else {
-                        gray_frame<U, MAP, LAYOUT>(a, lds, rb, buf[j], voff, tf, v + 4 * q, q ? c1 : c0);
+                        gray_frame<U, NA, MAP, LAYOUT>(a, lds, rb, buf[j], thr28, voff, tf, v + 4 * q,
+                                                       q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 4, buf[j]);
                     }
@@ -258,9 +336,9 @@ __global__ __launch_bounds__(64 * kGrayWaves) void series_gray_lut_kernel(Series
                 uint32_t v[4], c;
                 const uint32_t tf = t0 + k + (uint32_t)j;
                 if constexpr (PF)
-                    gray_frame<U, MAP, LAYOUT>(a, lds, buf[j], buf[j + 1], voff, tf, v, c);
+                    gray_frame<U, NA, MAP, LAYOUT>(a, lds, buf[j], buf[j + 1], thr28, voff, tf, v, c);
                 else
-                    gray_frame<U, MAP, LAYOUT>(a, lds, rb, buf[j], voff, tf, v, c);
+                    gray_frame<U, NA, MAP, LAYOUT>(a, lds, rb, buf[j], thr28, voff, tf, v, c);
                 const uint32_t y = wave_sum4_lanes(v);
                 gstore_one(rpart, tf, rec_off4, lane, y, c);
             }
@@ -270,12 +348,39 @@ __global__ __launch_bounds__(64 * kGrayWaves) void series_gray_lut_kernel(Series
 
 }  // namespace
 
-template <int U, int L>
+template <int U, int L, int NA = 0, int GW = kGrayWaves>
 static const void* gray_ptr(bool per_frame, bool map) {
-    return per_frame ? (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<U, true, true, L>)
-                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<U, true, false, L>))
-                     : (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<U, false, true, L>)
-                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<U, false, false, L>));
+    return per_frame ? (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<U, true, true, L, NA, GW>)
+                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<U, true, false, L, NA, GW>))
+                     : (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<U, false, true, L, NA, GW>)
+                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<U, false, false, L, NA, GW>));
+}
+
+bool gray_alu_allowed(float tau) { return tau >= kGrayAluMinTau; }
+
+uint32_t gray_lut_waves(int layout, int alu_vecs) {
+    // waves per group of the table kernel: 16, or with arithmetic vecs
+    // kGrayAluWaves; DIPS_GRAY_ALU_WAVES = 12 / 16 for A/B runs of the u16
+    // table at U = 4 (12 waves leave 168 VGPRs; the arithmetic vecs spill at 16)
+    if (layout != 2) return (uint32_t)kGrayWaves;
+    if (alu_vecs == 0 && gray_lut_unroll() != 4) return (uint32_t)kGrayWaves;
+    if (const char* e = std::getenv("DIPS_GRAY_ALU_WAVES")) {
+        const int w = std::atoi(e);
+        if (w == 12 || w == 16) return (uint32_t)w;
+    }
+    return alu_vecs == 0 ? (uint32_t)kGrayWaves : kGrayAluWaves;
+}
+
+int gray_alu_vecs(float tau) {
+    // DIPS_GRAY_ALU = 0 / 1 / 2 arithmetic vecs of the U = 4 table kernel
+    // (A/B runs), else the default; only for tau >= 2^-5
+    if (!gray_alu_allowed(tau)) return 0;
+    int na = kGrayAluVecs;
+    if (const char* e = std::getenv("DIPS_GRAY_ALU")) {
+        const int v = std::atoi(e);
+        if (v >= 0 && v <= 2) na = v;
+    }
+    return na;
 }
 
 int gray_lut_unroll() {
@@ -287,8 +392,12 @@ int gray_lut_unroll() {
     return kUnrollGrayLut;
 }
 
-const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout) {
+const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs, uint32_t waves) {
     if (layout != 2) return gray_ptr<kUnrollGrayLut, 1>(per_frame, map);
+    if (waves != 12u && waves != 16u) return nullptr;
+    if (alu_vecs == 0 && waves == 12u) return gray_lut_unroll() == 4 ? gray_ptr<4, 2, 0, 12>(per_frame, map) : nullptr;
+    if (alu_vecs == 1) return waves == 12u ? gray_ptr<4, 2, 1, 12>(per_frame, map) : gray_ptr<4, 2, 1, 16>(per_frame, map);
+    if (alu_vecs == 2) return waves == 12u ? gray_ptr<4, 2, 2, 12>(per_frame, map) : gray_ptr<4, 2, 2, 16>(per_frame, map);
     switch (gray_lut_unroll()) {
         case 2: return gray_ptr<2, 2>(per_frame, map);
         case 3: return gray_ptr<3, 2>(per_frame, map);
@@ -302,12 +411,14 @@ hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
 }
 
 hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
-                                  hipStream_t s) {
-    const void* k = series_gray_lut_kernel_ptr(per_frame, map, layout);
+                                  hipStream_t s, int alu_vecs) {
+    if (alu_vecs != 0 && (layout != 2 || !gray_alu_allowed(a.thr))) return hipErrorInvalidValue;
+    const uint32_t waves = gray_lut_waves(layout, alu_vecs);
+    const void* k = series_gray_lut_kernel_ptr(per_frame, map, layout, alu_vecs, waves);
     if (!k || !a.lut || blocks == 0) return hipErrorInvalidValue;
     SeriesArgs args = a;
     void* params[] = {&args};
-    return hipLaunchKernel(k, dim3(blocks), dim3(64 * kGrayWaves), params, 0, s);
+    return hipLaunchKernel(k, dim3(blocks), dim3(64 * waves), params, 0, s);
 }
 
 }  // namespace dips

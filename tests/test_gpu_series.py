@@ -422,6 +422,40 @@ def test_gray_table_every_byte_pair(tau):
         _check(got, out4, si)
 
 
+@pytest.mark.parametrize("alu,waves", [("1", "12"), ("1", "16"), ("2", "12"), ("2", "16")])
+def test_gray_alu_vecs_match_oracle(alu, waves, monkeypatch):
+    """The GRAY8 table kernel with 1 or 2 of its 4 vecs per lane on the
+    arithmetic path (series_gray.hip gray_alu_dword; DIPS_GRAY_ALU, tau >=
+    2^-5 only) at 12 and 16 waves per group, against the oracle: all 65,536
+    byte pairs, alternating black / white frames (every pixel dI = 1, the
+    largest per-lane sums), random and synthetic clips with a ragged shape,
+    both modes, with and without the map; tau below 2^-5 keeps the table."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    monkeypatch.setenv("DIPS_GRAY_ALU", alu)
+    monkeypatch.setenv("DIPS_GRAY_ALU_WAVES", waves)
+    x = np.arange(256, dtype=np.uint8)
+    pairs = np.empty((258, 256, 256), dtype=np.uint8)
+    pairs[0] = x[None, :]
+    pairs[1:257] = x[:, None, None]
+    pairs[257] = x[:, None]
+    bw = np.zeros((7, 64, 256), dtype=np.uint8)
+    bw[1::2] = 255
+    clips = [pairs, bw, _frames(1, 640, 48, 9, 77, "synth"), _frames(1, 256, 64, 9, 78, "random"),
+             _frames(1, 1000, 37, 6, 79, "random")]
+    for tau in (1 / 32, 8 / 255, 0.5, 1.0, 1 / 64):
+        for fr in clips:
+            for mode in (0, 1):
+                out4, si, dmap = oracle.series(fr, mode=mode, tau=tau, want_map=True)
+                op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
+                try:
+                    got, gmap = op(fr, want_map=True)
+                    got_nomap, _ = op(fr)
+                finally:
+                    op.close()
+                _check(got, out4, si, gmap, dmap)
+                _check(got_nomap, out4, si)
+
+
 @pytest.mark.parametrize("c", [1, 3])
 def test_stream_switch_orders_shared_scratch(c):
     """Back-to-back batches on two different streams through one operator,

@@ -341,6 +341,58 @@ def test_gray_si_decomposition():
     assert int(out4[1, 3]) == int(2 * v.sum())
 
 
+def test_gray_alu_vec_identity():
+    """The arithmetic vecs of series_gray_lut_kernel (series_gray.hip
+    gray_alu_dword), exhaustively over the 65,536 byte pairs and several
+    tau >= 2^-5: U'(c) = fma(c, 2^28 K_HI, c * 2^28 K_LO) = 2^28 u(c), the
+    f32 difference D' = 2^28 RN(u(a) - u(b)), the pixel is selected exactly
+    when dI > tau, a selected |D'| is an integer with 8 |D'| = V (the table's
+    8421504 d + corr), and a per-lane sum S of 8 selected |D'| splits into
+    sum d = S // 1052688 and sum corr = 8 (S mod 1052688)."""
+    from fractions import Fraction
+    F32 = np.float32
+    k_hi = F32(float.fromhex("0x1.010102p20"))
+    k_lo = F32(float.fromhex("-0x1.fdfdfep-5"))
+    assert k_hi == F32(float.fromhex("0x1.010102p-8")) * F32(2.0 ** 28)
+    assert k_lo == F32(float.fromhex("-0x1.fdfdfep-33")) * F32(2.0 ** 28)
+    u28 = np.empty(256, F32)
+    for c in range(256):
+        lo = F32(F32(c) * k_lo)
+        x = Fraction(c) * Fraction(float(k_hi)) + Fraction(float(lo))
+        cand = F32(float(x))
+        for nb in (np.nextafter(cand, F32(-1)), np.nextafter(cand, F32(2 ** 30))):
+            if abs(Fraction(float(nb)) - x) < abs(Fraction(float(cand)) - x):
+                cand = nb
+        u28[c] = cand
+    assert np.array_equal(u28.astype(np.float64), nr.U_LUT.astype(np.float64) * 2.0 ** 28)
+    a, b = np.meshgrid(np.arange(256), np.arange(256), indexing="ij")
+    dp = np.abs((u28[a] - u28[b]).astype(F32))
+    di = np.abs((nr.U_LUT[a] - nr.U_LUT[b]).astype(F32))
+    assert np.array_equal(dp.astype(np.float64), di.astype(np.float64) * 2.0 ** 28)
+    v = (di.astype(np.float64) * 2.0 ** 31).astype(np.int64)
+    d = np.abs(a - b)
+    rng = np.random.default_rng(5)
+    for tau in (0.03125, 8.0 / 255.0, 0.05, 0.1, 0.5, 0.999, 1.0):
+        tau = F32(tau)
+        thr28 = F32(tau * F32(2.0 ** 28))
+        assert float(thr28) == float(tau) * 2.0 ** 28 and float(thr28) == int(thr28)
+        sel_alu = dp > thr28
+        assert np.array_equal(sel_alu, di > tau)
+        s = dp[sel_alu].astype(np.float64)
+        assert np.all(s == np.floor(s)) and s.max(initial=0) <= 2.0 ** 28
+        assert np.array_equal(8 * s.astype(np.int64), v[sel_alu])
+        # random lanes of 8 selected pixels (worst case: 8 * 2^28 < 2^32)
+        idx = np.flatnonzero(sel_alu.ravel())
+        if idx.size == 0:
+            continue
+        lanes = rng.choice(idx, size=(4096, 8))
+        S = dp.ravel()[lanes].astype(np.int64).sum(axis=1)
+        assert S.max() < 2 ** 32
+        sum_d, sum_corr = S // 1052688, 8 * (S % 1052688)
+        assert np.array_equal(sum_d, d.ravel()[lanes].sum(axis=1))
+        assert np.array_equal(8421504 * sum_d + sum_corr, v.ravel()[lanes].sum(axis=1))
+
+
 @pytest.mark.parametrize("filt", [0, 1, 255])
 @pytest.mark.parametrize("colorize", [False, True])
 def test_epilogue_table_encoding(filt, colorize):

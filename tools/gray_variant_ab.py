@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""gray_variant_ab.py -- in-process A/B of the GRAY8 table kernel's vecs per
-lane (DIPS_GRAY_LUT_U, read per call): one batch of 4K gray8 frames,
-per-frame, tau 8/255; variants alternated over rounds, kernel time by
-hipEvents, series compared with the first variant's.
-Run on the GPU box: python tools/gray_variant_ab.py [rounds] [frames] [variants]
+"""gray_variant_ab.py -- in-process A/B of the GRAY8 table kernel's variants,
+read per call: vecs per lane (a number: DIPS_GRAY_LUT_U) or arithmetic vecs
+and waves per group ("a<NA>w<W>": DIPS_GRAY_ALU / DIPS_GRAY_ALU_WAVES); one
+batch of 4K gray8 frames, per-frame, tau 8/255; variants alternated over
+rounds, kernel time by hipEvents, series compared with the first variant's.
+Run on the GPU box: python tools/gray_variant_ab.py [rounds] [frames] [variants] [pf|overall] [map|nomap]
+(with the map, GBps counts the map's writes too).
 """
 import json
 import os
@@ -19,29 +21,39 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 6000
     variants = (sys.argv[3] if len(sys.argv) > 3 else "4,2,3").split(",")
+    mode = sys.argv[4] if len(sys.argv) > 4 else "pf"
+    with_map = len(sys.argv) > 5 and sys.argv[5] == "map"
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     W, H = 3840, 2160
-    op = DiffSeriesOperator(PixelFormat.Gray8, Mode.PerFrame, 8.0 / 255.0, time_kernel=True)
+    op = DiffSeriesOperator(PixelFormat.Gray8, Mode.PerFrame if mode == "pf" else Mode.Overall, 8.0 / 255.0,
+                            time_kernel=True)
     frames = torch.empty((n, H, W), dtype=torch.uint8, device="cuda")
+    dmap = torch.empty_like(frames) if with_map else None
     op.synth_device(frames, W, H, 0xD1B5, 0)
     ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
     ref = None
     for r in range(rounds):
         for v in variants:
-            os.environ["DIPS_GRAY_LUT_U"] = v
-            op.run_device(frames, ser)
+            if v.startswith("a"):
+                na, w = v[1:].split("w")
+                os.environ["DIPS_GRAY_ALU"], os.environ["DIPS_GRAY_ALU_WAVES"] = na, w
+                os.environ["DIPS_GRAY_LUT_U"] = "4"
+            else:
+                os.environ["DIPS_GRAY_ALU"] = "0"
+                os.environ["DIPS_GRAY_LUT_U"] = v
+            op.run_device(frames, ser, map_out=dmap)
             torch.cuda.synchronize()
             op.kernel_time(reset=True)
             for _ in range(5):
-                op.run_device(frames, ser)
+                op.run_device(frames, ser, map_out=dmap)
             torch.cuda.synchronize()
             ms = float(np.median(op.kernel_times()))
             h = ser.cpu().numpy()
             if ref is None:
                 ref = h
-            gbs = n * W * H / (ms / 1e3) / 1e9
-            print(json.dumps({"round": r, "U": int(v), "kernel_ms": round(ms, 4), "GBps": round(gbs, 1),
+            gbs = n * W * H * (2 if with_map else 1) / (ms / 1e3) / 1e9
+            print(json.dumps({"round": r, "variant": v, "mode": mode, "map": with_map, "kernel_ms": round(ms, 4), "GBps": round(gbs, 1),
                               "frac_of_8TBps": round(gbs / 8000, 4), "series_equal_first": bool(np.array_equal(h, ref))}),
                   flush=True)
     op.close()
