@@ -534,6 +534,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    # Rehearsal of the N > 1 path on one GPU (tests/test_gpu_bench_rehearsal.py):
+    # DIPS_BENCH_BACKEND=gloo with DIPS_BENCH_ONE_DEVICE=1 runs every rank on
+    # device 0 over gloo, which on this torch build moves device tensors for
+    # every collective the step uses (tools/gloo_cuda_probe.py).  The line then
+    # says so in "parallelism"; the driver's runs use RCCL, one rank per GPU.
+    backend = os.environ.get("DIPS_BENCH_BACKEND", "nccl")
+    if os.environ.get("DIPS_BENCH_ONE_DEVICE") == "1":
+        local = 0
+    corrupt_halo = os.environ.get("DIPS_BENCH_CORRUPT_HALO") == "1"  # the self-check must catch it (tests)
     torch.cuda.set_device(local)  # one rank per GPU (RCCL rejects two ranks on one device)
     if world > 1:
         # leave one wave slot per SIMD to RCCL's send/recv kernels (the halo
@@ -542,7 +551,10 @@ def main():
         os.environ.setdefault("DIPS_SERIES_WAVES_PER_SIMD", "4")
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat, shard
 
@@ -570,6 +582,8 @@ def main():
     gather = shard.SeriesGather(world * F, dev)
 
     def compute(fr, r, out):
+        if corrupt_halo and rank == 1 and r is ref:
+            r.view(-1)[12345] ^= 0x5A  # the received halo frame, damaged on purpose
         op.run_device(fr, out, ref=r)
 
     def step():
@@ -755,7 +769,10 @@ def main():
                 "workload": f"{W}x{H} RGB8, {F} frames per GPU, '{args.mode}' mode, tau={args.tau:.6g} "
                             f"(BASELINE.json configs[{2 if mode == Mode.PerFrame else 3}] per-GPU slice)",
                 "frames_per_gpu": F, "width": W, "height": H, "mode": args.mode,
-                "parallelism": f"frame-range x{world}" + (" + RCCL halo send/recv + gather" if world > 1 else ""),
+                "parallelism": f"frame-range x{world}" + ((" + RCCL halo send/recv + gather" if backend == "nccl"
+                                                             else f" + {backend} halo send/recv + gather "
+                                                                  "(rehearsal, ranks share one GPU)")
+                                                            if world > 1 else ""),
             },
             "ranks": world,
             "devices": devices,
