@@ -222,12 +222,16 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
 // GRAY8 runs on the table kernel (series_gray.hip) unless DIPS_GRAY_LUT=0
 // (the f32 kernel series_fast_kernel; kept for A/B runs and as a cross-check).
 // table layout: 1 two byte tables, 2 one u16 table, 0 off (DIPS_GRAY_LUT)
+// GRAY8 kernel: 3 the u16 table keyed by (a ^ b, a) with the band clamp
+// (default), 2 the u16 table keyed by (a, b), 1 two byte tables, 0 the f32
+// series_fast_kernel (DIPS_GRAY_LUT, read per call: A/B runs and tests)
 int gray_lut_layout() {
     if (const char* e = std::getenv("DIPS_GRAY_LUT")) {
         if (e[0] == '0') return 0;
         if (e[0] == '1') return 1;
+        if (e[0] == '2') return 2;
     }
-    return 2;
+    return 3;
 }
 bool gray_lut_enabled() { return gray_lut_layout() != 0; }
 
@@ -236,9 +240,10 @@ FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t nvec = npx / 16u;
     if (nvec == 0 || npx >= (1ull << 31) || n_frames == 0) return g;
-    const int alu = gray_lut_layout() == 2 ? dips::gray_alu_vecs(h->p.tau) : 0;
-    const uint64_t U = (uint64_t)(gray_lut_layout() == 2 ? (alu > 0 ? 4 : dips::gray_lut_unroll()) : dips::kUnrollGrayLut);
-    const uint64_t gw = dips::gray_lut_waves(gray_lut_layout(), alu);
+    const int layout = gray_lut_layout();
+    const int alu = layout == 2 ? dips::gray_alu_vecs(h->p.tau) : 0;
+    const uint64_t U = (uint64_t)(layout >= 2 ? (alu > 0 ? 4 : dips::gray_lut_unroll()) : dips::kUnrollGrayLut);
+    const uint64_t gw = dips::gray_lut_waves(layout, alu);
     g.vec_bytes = nvec * 16u;
     g.tail_px0 = nvec * 16u;
     g.n_tiles = (nvec + 64 * U - 1) / (64 * U);
@@ -260,7 +265,7 @@ FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint
 dips_status ensure_gray_lut(dips_handle* h, hipStream_t s) {
     const int layout = gray_lut_layout();
     if (h->gray_lut_valid && h->gray_lut_tau == h->p.tau && h->gray_lut_layout == layout) return DIPS_OK;
-    DIPS_HIP(h, h->gray_lut.ensure(dips::kGrayLutBytes));
+    DIPS_HIP(h, h->gray_lut.ensure(dips::kGrayLutAllocBytes));
     DIPS_HIP(h, dips::launch_gray_lut(h->gray_lut.as<uint8_t>(), h->p.tau, layout, s));
     h->gray_lut_valid = true;
     h->gray_lut_tau = h->p.tau;

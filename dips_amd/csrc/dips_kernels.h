@@ -32,6 +32,7 @@ constexpr int kGrayAluVecs = DIPS_GRAY_ALU_VECS;
 constexpr uint32_t kGrayAluWaves = DIPS_GRAY_ALU_WAVES;
 constexpr uint32_t kGrayLutWaves = 16;  // its waves per workgroup (one 1024-thread group per CU)
 constexpr size_t kGrayLutBytes = 131072;  // its T_d / T_c tables
+constexpr size_t kGrayLutAllocBytes = kGrayLutBytes + 256;  // + layout 3's band word (series_gray.hip)
 // Prefetch depth: frames of loads each wave keeps in flight.
 #ifndef DIPS_DEPTH_RGB
 #define DIPS_DEPTH_RGB 2
@@ -244,7 +245,8 @@ hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, boo
 // record layout: 0 RGB(A), 1 gray (series_fast_kernel), 2 gray table kernel (series_gray_lut_kernel)
 hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
                                 dips_series_entry* series, hipStream_t s);
-// GRAY8 table kernel, table layout 1 (two byte tables) or 2 (one u16 table)
+// GRAY8 table kernel, table layout 1 (two byte tables), 2 (one u16 table) or
+// 3 (the u16 table keyed by (a ^ b, a), band clamp: the default)
 const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs = 0, uint32_t waves = 16);
 int gray_alu_vecs(float tau);          // arithmetic vecs of this call's table kernel (0 for tau < 2^-5)
 uint32_t gray_lut_waves(int layout, int alu_vecs);  // waves per group of the table kernel

@@ -54,6 +54,22 @@ constexpr uint32_t kGrayV = 8421504u;          // V = kGrayV * d + corr
 // reference dword is swizzled once before the index perms).
 constexpr uint32_t kGraySwizzle = 0x3Cu;
 
+// Layout 3 (the default): the entry of (a, b) at u16 index
+// x * 256 + (a ^ sw(x)), x = a ^ b, sw(x) = (x << 1) & 0x7E.  Rows x < 2^m
+// hold only pairs with |a - b| < 2^m; when every one of them is below the
+// threshold (2^m - 1 <= the largest |a - b| that is never selected for tau),
+// all their entries are 0, and the kernel clamps every index below
+// K = 256 * 2^m - 1 up to K (one v_pk_max_u16 per pixel pair): all those
+// lanes read the one entry K, an LDS broadcast instead of a random gather.
+// Consecutive video frames put most pixels there -- the bench's synthetic
+// clips (+-4 noise per frame) ~63 % at tau = 8/255, flat content nearly all --
+// while the remaining lanes stay spread over the banks: bits 1-6 of the
+// column are bits 1-6 of a XOR bits 0-5 of x.  m comes from the band word the
+// table kernel leaves after the table (256 - the first row holding a selected
+// pair), so the clamp is exact by construction for any tau.
+constexpr uint32_t kGrayBandOffset = 131072u;  // byte offset of the band word (after the table)
+__host__ __device__ constexpr uint32_t gray_band_swizzle(uint32_t x) { return (x << 1) & 0x7Eu; }
+
 // The arithmetic vecs (NA of the U vecs per lane, tau >= 2^-5 only).  The
 // table path is bound by its LDS gathers (profiles/r03/gray_lds_counters.json:
 // the LDS array busy 96 % of the kernel, 6.9 LDS cycles per wave-wide
@@ -104,18 +120,32 @@ __device__ __forceinline__ void gray_alu_dword(uint32_t f, uint32_t r, float thr
 
 // The tables for threshold tau (65,536 spec evaluations), 131,072 bytes:
 // layout 1 -- T_d at byte 0 and T_c at byte kGrayLutTcOffset;
-// layout 2 -- one u16 table, entry d | corr << 8 at byte 2 idx.
+// layout 2 -- one u16 table, entry d | corr << 8 at byte 2 idx;
+// layout 3 -- the same entries keyed by (x = a ^ b, a) (see kGrayBandOffset),
+// plus the band word: max over the rows x holding a selected pair of 256 - x
+// (0 when none is), which the caller zeroes before the launch.  One block per
+// row x in layout 3.
 __global__ __launch_bounds__(256) void gray_lut_kernel(uint8_t* __restrict__ tab, float tau, uint32_t layout) {
     const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t a = idx >> 8, b = idx & 0xFFu;
+    uint32_t a = idx >> 8, b = idx & 0xFFu;
+    if (layout == 3u) {
+        const uint32_t x = idx >> 8;
+        a = (idx & 0xFFu) ^ gray_band_swizzle(x);
+        b = a ^ x;
+    }
     const float di = fabsf(unorm_load(a) - unorm_load(b));
     const bool sel = di > tau;
     const uint64_t v = (uint64_t)((double)di * 2147483648.0);  // exact: di is a multiple of 2^-31
     const uint32_t d = a > b ? a - b : b - a;
     const uint32_t corr = (uint32_t)(v - (uint64_t)kGrayV * d);  // in [0, 128] (exhaustive test)
-    if (layout == 2u) {
+    const uint16_t e = sel ? (uint16_t)(d | corr << 8) : (uint16_t)0;
+    if (layout == 3u) {
+        reinterpret_cast<uint16_t*>(tab)[idx] = e;
+        if (__syncthreads_or(sel) && threadIdx.x == 0u)
+            atomicMax(reinterpret_cast<uint32_t*>(tab + kGrayBandOffset), 256u - blockIdx.x);
+    } else if (layout == 2u) {
         const uint32_t pos = (a << 8) | (b ^ ((a << 2) & kGraySwizzle));
-        reinterpret_cast<uint16_t*>(tab)[pos] = sel ? (uint16_t)(d | corr << 8) : (uint16_t)0;
+        reinterpret_cast<uint16_t*>(tab)[pos] = e;
     } else {
         tab[idx] = sel ? (uint8_t)d : (uint8_t)0;
         if (idx != 0u) tab[kGrayLutTcOffset + idx] = sel ? (uint8_t)corr : (uint8_t)0;
@@ -143,11 +173,13 @@ __device__ __forceinline__ void gstore_one(__amdgpu_buffer_rsrc_t rpart, uint32_
 // One frame of one tile against the reference bytes rb: the 4 per-lane
 // values {SAD, sum d, sum corr, 0} and the wave-wide count.
 // NA > 0 (layout 2): vecs U - NA .. U - 1 take the arithmetic path.
+// LAYOUT 3: kk = the band clamp K in both u16 halves.
 template <int U, int NA, bool MAP, int LAYOUT>
 __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* lds, const uint32_t (&rb)[U][4],
-                                           const uint32_t (&cur)[U][4], float thr28, uint32_t voff,
+                                           const uint32_t (&cur)[U][4], float thr28, uint32_t kk, uint32_t voff,
                                            uint32_t t, uint32_t* vals, uint32_t& cnt) {
     static_assert(NA == 0 || (LAYOUT == 2 && NA < U), "arithmetic vecs: layout 2, at least one table vec");
+    constexpr bool U16 = LAYOUT >= 2;  // one u16 entry per pixel (layouts 2, 3)
     uint32_t sad = 0, acc = 0, accd = 0, accc = 0, c = 0;
     uint32_t map[U][4];
     uint32_t alu_s[NA > 0 ? 2 * NA : 1], alu_c = 0;
@@ -172,12 +204,24 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
             sad = __builtin_amdgcn_sad_u8(f, r, sad);
             if constexpr (MAP) map[u][k] = absdiff_bytes(f, r);
             if (u >= U - NA) continue;
-            // table indices f_i * 256 + r_i of pixels (0, 2) and (1, 3) as u16
-            // pairs (layout 2: r_i ^ sw(f_i), per byte of the dword at once)
-            const uint32_t rs = LAYOUT == 2 ? r ^ ((f << 2) & (kGraySwizzle * 0x01010101u)) : r;
-            const uint32_t i02 = __builtin_amdgcn_perm(f, rs, 0x06020400u);
-            const uint32_t i13 = __builtin_amdgcn_perm(f, rs, 0x07030501u);
-            if constexpr (LAYOUT == 2) {
+            // table indices of pixels (0, 2) and (1, 3) as u16 pairs, per byte
+            // of the dword at once: layouts 1 / 2 f_i * 256 + r_i (layout 2:
+            // r_i ^ sw(f_i)); layout 3 x_i * 256 + (f_i ^ sw3(x_i)),
+            // x_i = f_i ^ r_i, the indices below the band clamp raised to it
+            uint32_t i02, i13;
+            if constexpr (LAYOUT == 3) {
+                const uint32_t x = f ^ r;
+                const uint32_t col = f ^ ((x << 1) & (gray_band_swizzle(0xFFu) * 0x01010101u));
+                i02 = as_u32(__builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x06020400u)),
+                                                       as_u16x2(kk)));
+                i13 = as_u32(__builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x07030501u)),
+                                                       as_u16x2(kk)));
+            } else {
+                const uint32_t rs = LAYOUT == 2 ? r ^ ((f << 2) & (kGraySwizzle * 0x01010101u)) : r;
+                i02 = __builtin_amdgcn_perm(f, rs, 0x06020400u);
+                i13 = __builtin_amdgcn_perm(f, rs, 0x07030501u);
+            }
+            if constexpr (U16) {
                 // one u16 entry e = d | corr << 8 per pixel (0: not selected,
                 // else d >= 1), two pixels' entries in one register.  Three
                 // SAD sums per pixel pair carry everything:
@@ -207,7 +251,7 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
             }
         }
     }
-    if constexpr (LAYOUT == 2) {
+    if constexpr (U16) {
         // sb = accc, s0 = accd, s1 = acc (all < 2^22 for 64 px per lane):
         // sum corr = (s0 - sb) / 255, sum d = sb - sum corr,
         // count = (s0 + n - s1) / 2
@@ -234,7 +278,7 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
     vals[0] = sad;
     vals[1] = acc & 0xFFFFu;
     vals[2] = acc >> 16;
-    if constexpr (LAYOUT == 2) {
+    if constexpr (U16) {
         vals[3] = c;  // per-lane count, summed with the other values
         cnt = 0u;
     } else {
@@ -261,6 +305,15 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
     const uint32_t rec_off8 = (lane & 7u) == 0u ? (lane >> 5) * 16u + ((lane >> 3) & 3u) * 4u : 0x80000000u;
     const uint32_t rec_off4 = (lane & 15u) == 0u ? (lane >> 4) * 4u : 0x80000000u;
     const float thr28 = a.thr * 268435456.0f;  // 2^28 tau (exact)
+    uint32_t kk = 0u;
+    if constexpr (LAYOUT == 3) {
+        // the band clamp from the word after the table: rows x < 2^m hold no
+        // selected pair, m = floor(log2(the first row that does)), K = 256 * 2^m - 1
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(a.lut) + kGrayBandOffset);
+        const uint32_t first = 256u - min(w, 255u);  // 1 .. 256 (row 0, a == b, is never selected)
+        const uint32_t kc = (256u << (31u - __builtin_clz(first))) - 1u;
+        kk = kc | (kc << 16);
+    }
 
     uint64_t i = (uint64_t)wave * a.items / a.n_waves;
     const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
@@ -315,12 +368,12 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
                     const int j = 2 * h + q;
                     const uint32_t tf = t0 + k + (uint32_t)j;
                     if constexpr (PF) {
-                        gray_frame<U, NA, MAP, LAYOUT>(a, lds, buf[j], buf[(j + 1) & 3], thr28, voff, tf,
+                        gray_frame<U, NA, MAP, LAYOUT>(a, lds, buf[j], buf[(j + 1) & 3], thr28, kk, voff, tf,
                                                        v + 4 * q, q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 3, buf[j]);
                     } else {
-                        gray_frame<U, NA, MAP, LAYOUT>(a, lds, rb, buf[j], thr28, voff, tf, v + 4 * q,
+                        gray_frame<U, NA, MAP, LAYOUT>(a, lds, rb, buf[j], thr28, kk, voff, tf, v + 4 * q,
                                                        q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 4, buf[j]);
@@ -336,9 +389,9 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
                 uint32_t v[4], c;
                 const uint32_t tf = t0 + k + (uint32_t)j;
                 if constexpr (PF)
-                    gray_frame<U, NA, MAP, LAYOUT>(a, lds, buf[j], buf[j + 1], thr28, voff, tf, v, c);
+                    gray_frame<U, NA, MAP, LAYOUT>(a, lds, buf[j], buf[j + 1], thr28, kk, voff, tf, v, c);
                 else
-                    gray_frame<U, NA, MAP, LAYOUT>(a, lds, rb, buf[j], thr28, voff, tf, v, c);
+                    gray_frame<U, NA, MAP, LAYOUT>(a, lds, rb, buf[j], thr28, kk, voff, tf, v, c);
                 const uint32_t y = wave_sum4_lanes(v);
                 gstore_one(rpart, tf, rec_off4, lane, y, c);
             }
@@ -362,7 +415,7 @@ uint32_t gray_lut_waves(int layout, int alu_vecs) {
     // waves per group of the table kernel: 16, or with arithmetic vecs
     // kGrayAluWaves; DIPS_GRAY_ALU_WAVES = 12 / 16 for A/B runs of the u16
     // table at U = 4 (12 waves leave 168 VGPRs; the arithmetic vecs spill at 16)
-    if (layout != 2) return (uint32_t)kGrayWaves;
+    if (layout != 2) return (uint32_t)kGrayWaves;  // layouts 1, 3: 16 waves, no arithmetic vecs
     if (alu_vecs == 0 && gray_lut_unroll() != 4) return (uint32_t)kGrayWaves;
     if (const char* e = std::getenv("DIPS_GRAY_ALU_WAVES")) {
         const int w = std::atoi(e);
@@ -393,7 +446,16 @@ int gray_lut_unroll() {
 }
 
 const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs, uint32_t waves) {
-    if (layout != 2) return gray_ptr<kUnrollGrayLut, 1>(per_frame, map);
+    if (layout == 1) return gray_ptr<kUnrollGrayLut, 1>(per_frame, map);
+    if (layout == 3) {
+        if (alu_vecs != 0 || waves != 16u) return nullptr;
+        switch (gray_lut_unroll()) {
+            case 2: return gray_ptr<2, 3>(per_frame, map);
+            case 3: return gray_ptr<3, 3>(per_frame, map);
+            default: return gray_ptr<4, 3>(per_frame, map);
+        }
+    }
+    if (layout != 2) return nullptr;
     if (waves != 12u && waves != 16u) return nullptr;
     if (alu_vecs == 0 && waves == 12u) return gray_lut_unroll() == 4 ? gray_ptr<4, 2, 0, 12>(per_frame, map) : nullptr;
     if (alu_vecs == 1) return waves == 12u ? gray_ptr<4, 2, 1, 12>(per_frame, map) : gray_ptr<4, 2, 1, 16>(per_frame, map);
@@ -406,6 +468,10 @@ const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int
 }
 
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
+    if (layout == 3) {
+        const hipError_t e = hipMemsetAsync(tab + kGrayBandOffset, 0, 4, s);
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(gray_lut_kernel, dim3(256), dim3(256), 0, s, tab, tau, (uint32_t)layout);
     return hipGetLastError();
 }

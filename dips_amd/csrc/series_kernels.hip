@@ -304,6 +304,50 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 //   gray table kernel: {SAD, sum d, sum corr, count}
 //                                             SI_fixed = 2 (8421504 sum d + sum corr), SJ = 2 SAD
 // (H, L: the split of the exact per-lane fixed-point intensity sum).
+struct ReduceAcc {
+    uint64_t sad = 0, sj = 0, cnt = 0, h = 0;
+    int64_t l = 0;
+};
+
+template <uint32_t LAYOUT>
+__device__ __forceinline__ void reduce_add(ReduceAcc& s, const u32x4 rec) {
+    if constexpr (LAYOUT == 2u) {
+        s.sad += rec.x;
+        s.h += rec.y;  // sum d
+        s.l += rec.z;  // sum corr
+        s.cnt += rec.w;
+    } else if constexpr (LAYOUT == 1u) {
+        s.sad += rec.x & 0xFFFFFu;
+        s.cnt += rec.x >> 20;
+        s.h += rec.y;
+        s.l += (int64_t)(int32_t)rec.z;
+    } else {
+        s.sad += rec.x;
+        s.sj += rec.y & 0xFFFFFu;
+        s.cnt += rec.y >> 20;
+        s.h += rec.z;
+        s.l += (int64_t)(int32_t)rec.w;
+    }
+}
+
+// Records of tiles tile0 .. tile1-1 for frame t: eight independent loads in
+// flight per thread (a rolled loop with the layout test inside kept one and
+// ran latency-bound); each record is read once, hence non-temporal.
+template <uint32_t LAYOUT>
+__device__ __forceinline__ void reduce_tiles(ReduceAcc& s, const uint64_t* __restrict__ partials, uint32_t n_frames,
+                                             uint32_t t, uint32_t tile0, uint32_t tile1) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(partials) + ((uint64_t)tile0 * n_frames + t);
+    uint32_t tile = tile0;
+    for (; tile + 8u <= tile1; tile += 8u, p += 8u * (uint64_t)n_frames) {
+        u32x4 rec[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rec[k] = __builtin_nontemporal_load(p + (uint64_t)k * n_frames);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) reduce_add<LAYOUT>(s, rec[k]);
+    }
+    for (; tile < tile1; ++tile, p += n_frames) reduce_add<LAYOUT>(s, __builtin_nontemporal_load(p));
+}
+
 __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __restrict__ partials, uint32_t n_frames,
                                                             uint32_t n_tiles, uint32_t tiles_per_block, uint32_t layout,
                                                             dips_series_entry* __restrict__ series) {
@@ -311,29 +355,16 @@ __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __re
     if (t >= n_frames) return;
     const uint32_t tile0 = blockIdx.y * tiles_per_block;
     const uint32_t tile1 = min(n_tiles, tile0 + tiles_per_block);
-    uint64_t sad = 0, sj = 0, cnt = 0, h = 0;
-    int64_t l = 0;
-    for (uint32_t tile = tile0; tile < tile1; ++tile) {
-        const u32x4 rec = *reinterpret_cast<const u32x4*>(partials + 2 * ((uint64_t)tile * n_frames + t));
-        if (layout == 2u) {
-            sad += rec.x;
-            h += rec.y;  // sum d
-            l += rec.z;  // sum corr
-            cnt += rec.w;
-        } else if (layout == 1u) {
-            sad += rec.x & 0xFFFFFu;
-            cnt += rec.x >> 20;
-            h += rec.y;
-            l += (int64_t)(int32_t)rec.z;
-        } else {
-            sad += rec.x;
-            sj += rec.y & 0xFFFFFu;
-            cnt += rec.y >> 20;
-            h += rec.z;
-            l += (int64_t)(int32_t)rec.w;
-        }
-    }
-    if (layout != 0u) sj = 2u * sad;
+    ReduceAcc s;
+    if (layout == 2u)
+        reduce_tiles<2u>(s, partials, n_frames, t, tile0, tile1);
+    else if (layout == 1u)
+        reduce_tiles<1u>(s, partials, n_frames, t, tile0, tile1);
+    else
+        reduce_tiles<0u>(s, partials, n_frames, t, tile0, tile1);
+    const uint64_t sad = s.sad, cnt = s.cnt, h = s.h;
+    const int64_t l = s.l;
+    const uint64_t sj = layout != 0u ? 2u * sad : s.sj;
     const uint64_t sif = layout == 2u ? 2u * (8421504u * h + (uint64_t)l) : (h << (layout == 1u ? 16 : 15)) + (uint64_t)l;
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].sad), (unsigned long long)sad);
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].sj), (unsigned long long)sj);

@@ -376,7 +376,8 @@ def test_unaligned_device_batches(c, mode, offsets, with_map):
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.5, 1.0])
 def test_gray_kernels_agree(mode, tau, monkeypatch):
-    """GRAY8 on the table kernel (u16 table, the default; DIPS_GRAY_LUT=2),
+    """GRAY8 on the table kernel (u16 table keyed by (a ^ b, a) with the band
+    clamp, the default; DIPS_GRAY_LUT=3), the u16 table keyed by (a, b) (=2),
     its two-byte-table layout (=1) and the f32 series_fast_kernel (=0), with
     and without the map, against the oracle -- random and synthetic frames,
     ragged shape included."""
@@ -384,7 +385,7 @@ def test_gray_kernels_agree(mode, tau, monkeypatch):
     for (w, h), kind in [((256, 64), "random"), ((640, 48), "synth"), ((37, 23), "random")]:
         frames = _frames(1, w, h, 9, 40 + w, kind)
         out4, si, dmap = oracle.series(frames, mode=mode, tau=tau, want_map=True)
-        for layout in ("2", "1", "0"):
+        for layout in ("3", "2", "1", "0"):
             monkeypatch.setenv("DIPS_GRAY_LUT", layout)
             op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
             try:
@@ -396,15 +397,20 @@ def test_gray_kernels_agree(mode, tau, monkeypatch):
             _check(got_nomap, out4, si)
 
 
-@pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.1, 0.5])
-def test_gray_table_every_byte_pair(tau):
+@pytest.mark.parametrize("layout", ["3", "2"])
+@pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.1, 0.5, 1.0])
+def test_gray_table_every_byte_pair(tau, layout, monkeypatch):
     """Every (frame byte a, reference byte b) through the swizzled GRAY8
-    table, against the oracle: 'overall' against a reference with b = x;
-    frame t = 1..256 holds a = t - 1 everywhere (so each a value is its own
-    series entry), frame 257 holds a = y (all 65,536 pairs in one frame);
-    plus a flat low-noise clip, the content that piles LDS reads onto few
-    banks without the swizzle."""
+    table (layout 3: keyed by (a ^ b, a), indices below the band clamp raised
+    to it; layout 2: keyed by (a, b)), against the oracle: 'overall' against a
+    reference with b = x; frame t = 1..256 holds a = t - 1 everywhere (so each
+    a value is its own series entry), frame 257 holds a = y (all 65,536 pairs
+    in one frame); plus a flat low-noise clip (the content that piles LDS
+    reads onto few banks without a swizzle, and nearly all inside layout 3's
+    band) and a clip whose frames alternate between one flat frame and
+    random ones (a = const against varying b)."""
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    monkeypatch.setenv("DIPS_GRAY_LUT", layout)
     x = np.arange(256, dtype=np.uint8)
     frames = np.empty((258, 256, 256), dtype=np.uint8)
     frames[0] = x[None, :]
@@ -412,7 +418,9 @@ def test_gray_table_every_byte_pair(tau):
     frames[257] = x[:, None]
     rng = np.random.default_rng(11)
     flat = np.clip(128 + rng.integers(-3, 4, (12, 64, 512)), 0, 255).astype(np.uint8)
-    for fr, mode in ((frames, 0), (frames, 1), (flat, 1)):
+    alt = rng.integers(0, 256, (9, 32, 256), dtype=np.uint8)
+    alt[::2] = 77
+    for fr, mode in ((frames, 0), (frames, 1), (flat, 1), (alt, 1), (alt, 0)):
         out4, si, _ = oracle.series(fr, mode=mode, tau=tau)
         op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
         try:
@@ -431,6 +439,7 @@ def test_gray_alu_vecs_match_oracle(alu, waves, monkeypatch):
     largest per-lane sums), random and synthetic clips with a ragged shape,
     both modes, with and without the map; tau below 2^-5 keeps the table."""
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    monkeypatch.setenv("DIPS_GRAY_LUT", "2")  # the arithmetic vecs are a layout-2 option
     monkeypatch.setenv("DIPS_GRAY_ALU", alu)
     monkeypatch.setenv("DIPS_GRAY_ALU_WAVES", waves)
     x = np.arange(256, dtype=np.uint8)

@@ -393,6 +393,43 @@ def test_gray_alu_vec_identity():
         assert np.array_equal(8421504 * sum_d + sum_corr, v.ravel()[lanes].sum(axis=1))
 
 
+@pytest.mark.parametrize("tau", [0.0, 1 / 255, 2 / 255, 7.5 / 255, 8 / 255, 15.9 / 255, 0.1, 0.5, 0.999, 1.0])
+def test_gray_band_layout(tau):
+    """Layout 3 of the GRAY8 table (series_gray.hip kGrayBandOffset): the
+    entry of (a, b) at u16 index x * 256 + (a ^ sw(x)), x = a ^ b,
+    sw(x) = (x << 1) & 0x7E, is a bijection of the 65,536 pairs; the band word
+    (max of 256 - x over rows x holding a selected pair) gives
+    K = 256 * 2^m - 1, m = floor(log2(first such row)), and every index
+    <= K holds entry 0 -- so the kernel's clamp max(index, K) changes no
+    entry, for any tau.  Also: the clamp is the whole near-diagonal band the
+    bench's content lives in (|a - b| <= 7 at tau = 8/255 maps to K), and
+    the bank of an index (bits 1-6) mixes a and x."""
+    F32 = np.float32
+    a, b = np.meshgrid(np.arange(256), np.arange(256), indexing="ij")
+    di = np.abs((nr.U_LUT[a] - nr.U_LUT[b]).astype(F32))
+    sel = di > F32(tau)
+    x = a ^ b
+    pos = x * 256 + (a ^ ((x << 1) & 0x7E))
+    assert np.array_equal(np.sort(pos.ravel()), np.arange(65536))
+    entry = np.zeros(65536, dtype=np.int64)
+    entry[pos.ravel()] = np.where(sel, 1 + np.abs(a - b), 0).ravel()  # nonzero exactly when selected
+    rows = np.unique(x[sel])
+    w = int(256 - rows.min()) if rows.size else 0
+    first = 256 - min(w, 255)
+    m = first.bit_length() - 1
+    K = (256 << m) - 1
+    assert K <= 65535 and not entry[: K + 1].any()
+    # the kernel's view: max(index, K) reads the same entry as index
+    assert np.array_equal(entry[np.maximum(pos, K)], entry[pos])
+    # the band is as wide as tau allows: row `first` holds a selected pair
+    if first < 256:
+        assert entry[first * 256:(first + 1) * 256].any() and first < (2 << m)
+    if abs(tau - 8 / 255) < 1e-9:
+        assert K == 2047 and np.all(np.maximum(pos, K)[x < 8] == K)
+    bank = (pos >> 1) & 63
+    assert np.array_equal(bank, ((a >> 1) ^ x) & 63)
+
+
 @pytest.mark.parametrize("filt", [0, 1, 255])
 @pytest.mark.parametrize("colorize", [False, True])
 def test_epilogue_table_encoding(filt, colorize):

@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """gray_variant_ab.py -- in-process A/B of the GRAY8 table kernel's variants,
-read per call: vecs per lane (a number: DIPS_GRAY_LUT_U) or arithmetic vecs
-and waves per group ("a<NA>w<W>": DIPS_GRAY_ALU / DIPS_GRAY_ALU_WAVES); one
-batch of 4K gray8 frames, per-frame, tau 8/255; variants alternated over
+read per call: vecs per lane of the layout-2 table (a number: DIPS_GRAY_LUT_U),
+arithmetic vecs and waves per group ("a<NA>w<W>": DIPS_GRAY_ALU /
+DIPS_GRAY_ALU_WAVES) or the table layout at U = 4 ("L3", "L2": DIPS_GRAY_LUT);
+one batch of 4K gray8 frames, per-frame, tau 8/255; variants alternated over
 rounds, kernel time by hipEvents, series compared with the first variant's.
 Run on the GPU box: python tools/gray_variant_ab.py [rounds] [frames] [variants] [pf|overall] [map|nomap]
-(with the map, GBps counts the map's writes too).
+[synth|random] (with the map, GBps counts the map's writes too; "random":
+i.i.d. uniform frames instead of the bench's synthetic clip).
 """
 import json
 import os
@@ -23,6 +25,7 @@ def main():
     variants = (sys.argv[3] if len(sys.argv) > 3 else "4,2,3").split(",")
     mode = sys.argv[4] if len(sys.argv) > 4 else "pf"
     with_map = len(sys.argv) > 5 and sys.argv[5] == "map"
+    content = sys.argv[6] if len(sys.argv) > 6 else "synth"
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     W, H = 3840, 2160
@@ -30,16 +33,29 @@ def main():
                             time_kernel=True)
     frames = torch.empty((n, H, W), dtype=torch.uint8, device="cuda")
     dmap = torch.empty_like(frames) if with_map else None
-    op.synth_device(frames, W, H, 0xD1B5, 0)
+    if content == "random":
+        g = torch.Generator(device="cuda")
+        g.manual_seed(7)
+        for k in range(0, n, 500):
+            frames[k:k + 500].copy_(torch.randint(0, 256, frames[k:k + 500].shape, dtype=torch.uint8,
+                                                  device="cuda", generator=g))
+    else:
+        op.synth_device(frames, W, H, 0xD1B5, 0)
     ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
     ref = None
     for r in range(rounds):
         for v in variants:
-            if v.startswith("a"):
+            if v.startswith("L"):
+                os.environ["DIPS_GRAY_LUT"] = v[1:]
+                os.environ["DIPS_GRAY_ALU"] = "0"
+                os.environ["DIPS_GRAY_LUT_U"] = "4"
+            elif v.startswith("a"):
+                os.environ["DIPS_GRAY_LUT"] = "2"
                 na, w = v[1:].split("w")
                 os.environ["DIPS_GRAY_ALU"], os.environ["DIPS_GRAY_ALU_WAVES"] = na, w
                 os.environ["DIPS_GRAY_LUT_U"] = "4"
             else:
+                os.environ["DIPS_GRAY_LUT"] = "2"
                 os.environ["DIPS_GRAY_ALU"] = "0"
                 os.environ["DIPS_GRAY_LUT_U"] = v
             op.run_device(frames, ser, map_out=dmap)
@@ -53,7 +69,7 @@ def main():
             if ref is None:
                 ref = h
             gbs = n * W * H * (2 if with_map else 1) / (ms / 1e3) / 1e9
-            print(json.dumps({"round": r, "variant": v, "mode": mode, "map": with_map, "kernel_ms": round(ms, 4), "GBps": round(gbs, 1),
+            print(json.dumps({"round": r, "variant": v, "mode": mode, "map": with_map, "content": content, "kernel_ms": round(ms, 4), "GBps": round(gbs, 1),
                               "frac_of_8TBps": round(gbs / 8000, 4), "series_equal_first": bool(np.array_equal(h, ref))}),
                   flush=True)
     op.close()
