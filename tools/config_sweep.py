@@ -35,11 +35,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--only", default="", help="run the configs whose name contains this string")
-    ap.add_argument("--gray-kernel", choices=["lut16", "lut8", "f32"], default="lut16",
-                    help="GRAY8: series_gray_lut_kernel with the u16 table (default) or the two byte "
-                         "tables, or the f32 series_fast_kernel")
+    ap.add_argument("--gray-kernel", choices=["band", "lut16", "lut8", "f32"], default=None,
+                    help="GRAY8: series_gray_lut_kernel with the band-clamped u16 table (the library "
+                         "default), the (a, b) u16 table or the two byte tables, or the f32 "
+                         "series_fast_kernel; unset: the library's choice (DIPS_GRAY_LUT as set)")
     args = ap.parse_args()
-    os.environ["DIPS_GRAY_LUT"] = {"lut16": "2", "lut8": "1", "f32": "0"}[args.gray_kernel]
+    if args.gray_kernel:
+        os.environ["DIPS_GRAY_LUT"] = {"band": "3", "lut16": "2", "lut8": "1", "f32": "0"}[args.gray_kernel]
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     from oracle import oracle
@@ -67,7 +69,7 @@ def main():
         want, _, _ = oracle.series(host, mode=mode, tau=tau, nthreads=8)
         ok = bool(np.array_equal(series[:3].cpu().numpy().view(np.uint64), want))
         fb = W * H * C
-        print(json.dumps({"config": name, **({"gray_kernel": args.gray_kernel} if C == 1 else {}),
+        print(json.dumps({"config": name, **({"gray_kernel": args.gray_kernel or {"0": "f32", "1": "lut8", "2": "lut16"}.get(os.environ.get("DIPS_GRAY_LUT", "3"), "band")} if C == 1 else {}),
                           "frames_per_s": round(F / wall, 1),
                           "kernel_ms": round(kms, 4), "kernel_GBps": round(F * fb / (kms / 1e3) / 1e9, 1),
                           "frac_of_8TBps": round(F * fb / (kms / 1e3) / 8e12, 4),

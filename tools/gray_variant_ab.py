@@ -2,7 +2,8 @@
 """gray_variant_ab.py -- in-process A/B of the GRAY8 table kernel's variants,
 read per call: vecs per lane of the layout-2 table (a number: DIPS_GRAY_LUT_U),
 arithmetic vecs and waves per group ("a<NA>w<W>": DIPS_GRAY_ALU /
-DIPS_GRAY_ALU_WAVES) or the table layout at U = 4 ("L3", "L2": DIPS_GRAY_LUT);
+DIPS_GRAY_ALU_WAVES) or the table layout ("L3", "L2", "L3u3": DIPS_GRAY_LUT,
+U = 4 or the number after u);
 one batch of 4K gray8 frames, per-frame, tau 8/255; variants alternated over
 rounds, kernel time by hipEvents, series compared with the first variant's.
 Run on the GPU box: python tools/gray_variant_ab.py [rounds] [frames] [variants] [pf|overall] [map|nomap]
@@ -45,10 +46,11 @@ def main():
     ref = None
     for r in range(rounds):
         for v in variants:
-            if v.startswith("L"):
-                os.environ["DIPS_GRAY_LUT"] = v[1:]
+            if v.startswith("L"):  # L<layout>[u<U>]
+                lay, _, u = v[1:].partition("u")
+                os.environ["DIPS_GRAY_LUT"] = lay
                 os.environ["DIPS_GRAY_ALU"] = "0"
-                os.environ["DIPS_GRAY_LUT_U"] = "4"
+                os.environ["DIPS_GRAY_LUT_U"] = u or "4"
             elif v.startswith("a"):
                 os.environ["DIPS_GRAY_LUT"] = "2"
                 na, w = v[1:].split("w")
