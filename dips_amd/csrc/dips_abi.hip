@@ -184,7 +184,7 @@ struct FastGeom {
 };
 
 FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, int C, bool pf,
-                       bool map, bool align = false, bool isi = false) {
+                       bool map, bool align = false, int isi = 0) {
     FastGeom g;
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t fb = npx * (uint64_t)C;
@@ -221,8 +221,7 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
 
 // GRAY8 runs on the table kernel (series_gray.hip) unless DIPS_GRAY_LUT=0
 // (the f32 kernel series_fast_kernel; kept for A/B runs and as a cross-check).
-// table layout: 1 two byte tables, 2 one u16 table, 0 off (DIPS_GRAY_LUT)
-// GRAY8 kernel: 3 the u16 table keyed by (a ^ b, a) with the band clamp
+// Table layout: 3 the u16 table keyed by (a ^ b, a) with the band clamp
 // (default), 2 the u16 table keyed by (a, b), 1 two byte tables, 0 the f32
 // series_fast_kernel (DIPS_GRAY_LUT, read per call: A/B runs and tests)
 int gray_lut_layout() {
@@ -292,9 +291,15 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     const bool align = C == 3 && ((((uintptr_t)frames | (uintptr_t)fb | (uintptr_t)ref0) & 3u) != 0u) &&
                        !(align_env && align_env[0] == '0');
     // RGB8 / RGBA8 with tau >= 2^-5: the integer intensity sum (series_v2.hip
-    // ISI; DIPS_SERIES_ISI=0 keeps the f64 sum, A/B)
+    // ISI = 1, or 2 = SADI with DIPS_SERIES_ISI=2; DIPS_SERIES_ISI=0 keeps the
+    // f64 sum; A/B runs)
     const char* isi_env = std::getenv("DIPS_SERIES_ISI");
-    const bool isi = C != 1 && dips::series_v2_isi(h->p.tau) && !(isi_env && isi_env[0] == '0');
+    int isi = 0;
+    if (C != 1 && dips::series_v2_isi(h->p.tau)) {
+        isi = 1;
+        if (isi_env && isi_env[0] == '0') isi = 0;
+        if (isi_env && isi_env[0] == '2' && dips::series_v2_sadi(h->p.tau)) isi = 2;
+    }
     if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC))
         g = glut ? gray_lut_geometry(h, width, height, n_frames)
                  : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr, align, isi);
@@ -346,6 +351,7 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         a.n_tiles = (uint32_t)g.n_tiles;
         a.n_waves = (uint32_t)g.n_waves;
         a.thr = dips::series_threshold(C, h->p.tau, isi);
+        a.thr_int = isi == 2 ? dips::series_sadi_threshold(h->p.tau) : 0u;
         if (glut) {
             a.lut = h->gray_lut.p;
             const int alu = h->gray_lut_layout == 2 ? dips::gray_alu_vecs(h->p.tau) : 0;
@@ -371,7 +377,8 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     }
     if (g.ok)
         DIPS_HIP(h, dips::launch_series_reduce(h->partials.as<uint64_t>(), n_frames, (uint32_t)g.n_tiles,
-                                               C == 1 ? (glut ? 2 : 1) : 0, series, s));
+                                               C == 1 ? (glut ? 2 : 1) : (isi == 2 ? 3 : 0), series, s,
+                                               isi == 2 ? dips::series_sadi_threshold(h->p.tau) : 0u));
     return DIPS_OK;
 }
 

@@ -58,6 +58,7 @@ struct SeriesArgs {
     float thr;               // threshold in kernel units: series_threshold()
     const void* lut;         // GRAY8 table kernel: T_d / T_c bytes (series_gray.hip), 128 KiB
     uint32_t part_frames;    // frames per part of the part-major schedule (series_v2 SCHED = 1)
+    uint32_t thr_int;        // series_v2 SADI (ISI = 2): T = tau * 2^28 as an integer (series_sadi_threshold)
 };
 
 struct GenericArgs {
@@ -232,19 +233,27 @@ inline bool alt_fast_epilogue_ok(uint32_t filter, float k) {
 
 int pixels_per_vec(int channels);
 int fast_unroll(int channels);
+// isi (series_v2, RGB8 / RGBA8): 0 the exact f64 intensity sum, 1 the
+// integer sum with a threshold select (ISI), 2 the integer sum from
+// sum |x - T| and sum x (SADI); 1 and 2 need tau >= 2^-5
 const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align = false,
-                                   bool isi = false);
+                                   int isi = 0);
 const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align = false,
-                                 bool isi = false);
+                                 int isi = 0);
 // whether tau admits the integer intensity sum of series_v2 (tau >= 2^-5)
 bool series_v2_isi(float tau);
+// whether tau admits SADI (2^-5 <= tau < 1)
+bool series_v2_sadi(float tau);
+// SeriesArgs::thr_int of the SADI kernel: tau * 2^28, at most 2^28
+uint32_t series_sadi_threshold(float tau);
 // threshold argument (SeriesArgs::thr) of the kernel series_fast_kernel_ptr picks
-float series_threshold(int channels, float tau, bool isi = false);
+float series_threshold(int channels, float tau, int isi = 0);
 hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, bool per_frame, bool map,
-                              uint32_t blocks, hipStream_t s, bool align = false, bool isi = false);
-// record layout: 0 RGB(A), 1 gray (series_fast_kernel), 2 gray table kernel (series_gray_lut_kernel)
+                              uint32_t blocks, hipStream_t s, bool align = false, int isi = 0);
+// record layout: 0 RGB(A), 1 gray (series_fast_kernel), 2 gray table kernel (series_gray_lut_kernel),
+// 3 RGB(A) SADI (thr_int: its T)
 hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
-                                dips_series_entry* series, hipStream_t s);
+                                dips_series_entry* series, hipStream_t s, uint32_t thr_int = 0);
 // GRAY8 table kernel, table layout 1 (two byte tables), 2 (one u16 table) or
 // 3 (the u16 table keyed by (a ^ b, a), band clamp: the default)
 const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs = 0, uint32_t waves = 16);

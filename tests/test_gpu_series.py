@@ -526,3 +526,48 @@ def test_device_calls_ordered_with_torch_default_stream():
         assert int(ser[1, 0]) == W * H * 3 * 197 and int(ser[2, 0]) == 0
     finally:
         op.close()
+
+
+@pytest.mark.parametrize("isi", ["0", "1", "2"])
+@pytest.mark.parametrize("c", [3, 4])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_series_intensity_sum_forms_match_oracle(isi, c, mode, monkeypatch):
+    """The three intensity-sum forms of series_v2 (DIPS_SERIES_ISI: 0 the
+    exact f64 sum, 1 the integer sum with a threshold select, 2 SADI: sums of
+    |x - T| and x, SJ rounded per tile in series_reduce) against the oracle,
+    for tau at and above 2^-5 up to just below 1 (SADI's range) and 1.0
+    (SADI falls back to 1): synthetic and random clips, black / white frames
+    (every pixel dI = 1: the largest per-lane sums), identical frames, a
+    ragged shape and an offset (aligned-load) batch, with and without the
+    map."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    monkeypatch.setenv("DIPS_SERIES_ISI", isi)
+    bw = np.zeros((6, 32, 96, c), dtype=np.uint8)
+    bw[1::2] = 255
+    same = np.repeat(_frames(c, 96, 32, 1, 5, "random"), 4, axis=0)
+    clips = [_frames(c, 256, 64, 9, 31, "synth"), _frames(c, 256, 64, 9, 32, "random"), bw, same,
+             _frames(c, 1000, 37, 6, 33, "random")]
+    below_one = float(np.nextafter(np.float32(1), np.float32(0)))
+    for tau in (1 / 32, 8 / 255, 0.3, below_one, 1.0):
+        for chroma in (0, 2):
+            op = DiffSeriesOperator(PixelFormat(c), Mode(mode), tau, chroma)
+            try:
+                for fr in clips:
+                    out4, si, dmap = oracle.series(fr, mode=mode, chroma=chroma, tau=tau, want_map=True)
+                    got, gmap = op(fr, want_map=True)
+                    _check(got, out4, si, gmap, dmap)
+                    got, _ = op(fr)
+                    _check(got, out4, si)
+                if c == 3:  # frames off a 4-byte boundary: the aligned-load form
+                    import torch
+                    fr = clips[0]
+                    buf = torch.empty(fr.nbytes + 8, dtype=torch.uint8, device="cuda")
+                    dev = buf[1:1 + fr.nbytes].view(fr.shape)
+                    dev.copy_(torch.from_numpy(fr))
+                    ser = torch.zeros((fr.shape[0], 4), dtype=torch.int64, device="cuda")
+                    op.run_device(dev, ser)
+                    torch.cuda.synchronize()
+                    out4, _, _ = oracle.series(fr, mode=mode, chroma=chroma, tau=tau)
+                    assert np.array_equal(ser.cpu().numpy().view(np.uint64), out4), (isi, tau, chroma)
+            finally:
+                op.close()

@@ -297,6 +297,55 @@ def test_v2_sj_lane_sum_rounds_exactly():
     assert np.array_equal(np.trunc(sj).astype(np.int64), want)
 
 
+@pytest.mark.parametrize("tau", [0.03125, 8 / 255, 0.1, 0.5, 0.999, float(np.nextafter(np.float32(1), np.float32(0)))])
+def test_v2_sadi_sums(tau):
+    """series_v2 SADI (ISI = 2): per pixel x = trunc(|dI| * 2^28) (the
+    intensities x32, I * 2^28), T = min(tau * 2^28, 2^28); per lane of 16
+    pixels Sa = sum |x - T| (one u32), Sx_0 / Sx_1 = sum x over the two 8-pixel
+    halves; the record carries Q = (Sa + Sx - 16 T) / 2 and
+    u = (Sx_0 >> 8) + (Sx_1 >> 8); series_reduce adds 16 T count per frame and
+    rounds SJ = (sum u * 510 + 2^19) >> 20 per 1024-pixel tile.  Checked:
+    Q = sum_selected x - c T exactly and in [0, 2^32), the selected x exact
+    (x * 2^-28 = |dI|), every u32 sum in range, and the per-tile SJ equal to
+    sum |dJ| -- random tiles and tiles of the extreme pixel pairs (black
+    against white: x = 2^28; equal pixels: x = 0).  SADI is used for
+    2^-5 <= tau < 1 only: with tau = 1, T = 2^28 and 16 equal pixels would
+    make Sa = 2^32."""
+    rng = np.random.default_rng(23)
+    mx, mn = np.meshgrid(np.arange(256), np.arange(256), indexing="ij")
+    keep = mx >= mn
+    mx, mn = mx[keep], mn[keep]
+    i28 = ((nr.U_LUT[mx] + nr.U_LUT[mn]).astype(np.float32) * np.float32(2.0 ** 27)).astype(np.float32)
+    j = (mx + mn).astype(np.int64)
+    tau32 = np.float32(tau)
+    thr = np.float32(tau32 * np.float32(2.0 ** 28))
+    T = int(min(float(thr), 2.0 ** 28))
+    assert float(thr) == T and 2 ** 23 <= T < 2 ** 28
+    n_tiles, lanes, px = 300, 64, 16
+    p = rng.integers(0, i28.size, (n_tiles, lanes, px))
+    q = rng.integers(0, i28.size, (n_tiles, lanes, px))
+    ext = np.array([0, i28.size - 1, int(np.argmax(j)), int(np.argmin(j))])
+    for a_, b_ in ((ext[0], ext[1]), (ext[1], ext[0]), (ext[2], ext[3]), (ext[0], ext[0]), (ext[1], ext[1])):
+        p = np.concatenate([p, np.full((1, lanes, px), a_)])
+        q = np.concatenate([q, np.full((1, lanes, px), b_)])
+    d = np.abs((i28[p] - i28[q]).astype(np.float32))  # |dI| * 2^28, f32 (the kernel's d)
+    x = np.trunc(d.astype(np.float64)).astype(np.int64)
+    sel = d > thr
+    assert np.all(x[sel] == d[sel].astype(np.float64)) and x.max() <= 2 ** 28
+    sa = np.abs(x - T).sum(axis=2)
+    sx0, sx1 = x[..., :8].sum(axis=2), x[..., 8:].sum(axis=2)
+    assert sa.max() < 2 ** 32 and max(sx0.max(), sx1.max()) <= 2 ** 31
+    q2 = sa + sx0 + sx1 - 16 * T
+    assert np.all(q2 % 2 == 0) and q2.min() >= 0 and q2.max() < 2 ** 33
+    qv = q2 // 2
+    cnt = sel.sum(axis=2)
+    assert np.array_equal(qv, np.where(sel, x, 0).sum(axis=2) - cnt * T)
+    u = (sx0 >> 8) + (sx1 >> 8)
+    assert u.max() <= 2 ** 24 and u.sum(axis=1).max() <= 2 ** 30
+    sj_tile = (u.sum(axis=1) * 510 + (1 << 19)) >> 20
+    assert np.array_equal(sj_tile, np.abs(j[p] - j[q]).sum(axis=(1, 2)))
+
+
 def test_tau_boundary_fixtures_straddle_tau():
     """The *_tauedge fixtures hold pixels whose f32 |dI| is exactly f32(tau)
     and one ulp either side: moving tau down one ulp adds the 'equal' pixels
