@@ -225,26 +225,14 @@ hipError_t run_striped_frame(const uint8_t* frame, uint8_t* out, uint32_t height
 // kernel has finished.  Small pieces let several threads stage the first
 // stripe and copy out the last one, the two exposed ends of the call.  The
 // copy-out tasks come after every staging task and wait for their stripe's
-// launch, so one worker or many run the same schedule (direct_interleave:
-// ready copy-outs go before the remaining staging).  The caller makes sure no
-// earlier kernel still reads `pin_in` or writes `pin_out`.
+// launch, so one worker or many run the same schedule.  The caller makes
+// sure no earlier kernel still reads `pin_in` or writes `pin_out`.
 inline uint32_t direct_split() {
     if (const char* e = std::getenv("DIPS_DIRECT_SPLIT")) {
         const long v = std::strtol(e, nullptr, 10);
         if (v >= 1 && v <= 64) return (uint32_t)v;
     }
     return 8u;
-}
-
-// Order of the pool's work in run_striped_frame_direct: interleaved (the
-// default) -- a worker takes the next copy-out piece as soon as its stripe's
-// kernel has finished (hipEventQuery), else the next staging piece, so the
-// expansion of the first stripes' keys runs beside the packing of the last
-// ones; DIPS_DIRECT_ORDER=0 -- every staging piece first, then the copy-outs
-// in order (round 3 before this change).  Read on the calling thread.
-inline bool direct_interleave() {
-    const char* e = std::getenv("DIPS_DIRECT_ORDER");
-    return !(e && e[0] == '0');
 }
 
 // Rows of the first stripe: a quarter stripe, so that the first kernel (whose
@@ -284,7 +272,6 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
                                     int device, PieceEvents& ev, Launch&& launch, int key_bytes = 0,
                                     int in_bytes = 0, int ch = 0) {
     const bool nt = nt_copy();  // on the calling thread, never in the workers
-    const bool interleave = direct_interleave();
     const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
     const uint32_t first = std::min(height, direct_first_rows(rows));
     const uint32_t n_s = 1u + (height - first + rows - 1) / rows;
@@ -301,53 +288,13 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
     }
     std::mutex launch_mu;
     std::atomic<int> err{(int)hipSuccess};
-    std::atomic<size_t> next_stage{0}, next_out{0};  // interleaved order: the next unclaimed piece of each kind
     static const bool trace = std::getenv("DIPS_STRIPE_TRACE") != nullptr;
     using clk = std::chrono::steady_clock;
     const auto tbeg = clk::now();
     std::vector<double> ts(trace ? 2 * n_s + n_t : 0);
     auto since = [&]() { return std::chrono::duration<double, std::micro>(clk::now() - tbeg).count(); };
-    // One unit of work per call: FIFO -- unit i (staging pieces, then
-    // copy-outs); interleaved -- the next copy-out piece whose stripe's kernel
-    // has finished, else the next staging piece, else (every staging piece
-    // claimed) the next copy-out, waiting for it.  2 n_t calls consume the
-    // n_t units of each kind exactly once either way, and a copy-out only
-    // waits once every staging piece is claimed, so every stripe it can wait
-    // for gets launched.
-    auto claim = [&](size_t i, bool& is_out) -> size_t {
-        if (!interleave) {
-            is_out = i >= n_t;
-            return is_out ? i - n_t : i;
-        }
-        for (;;) {
-            size_t o = next_out.load(std::memory_order_acquire);
-            if (o < n_t) {
-                const uint32_t so = (uint32_t)(o / k);
-                const int st = ready[so].load(std::memory_order_acquire);
-                if (st < 0 || (st > 0 && hipEventQuery(ev.ev[so]) == hipSuccess)) {
-                    if (next_out.compare_exchange_weak(o, o + 1, std::memory_order_acq_rel)) {
-                        is_out = true;
-                        return o;
-                    }
-                    continue;
-                }
-            }
-            size_t sg = next_stage.load(std::memory_order_acquire);
-            if (sg < n_t) {
-                if (next_stage.compare_exchange_weak(sg, sg + 1, std::memory_order_acq_rel)) {
-                    is_out = false;
-                    return sg;
-                }
-                continue;
-            }
-            is_out = true;
-            return next_out.fetch_add(1, std::memory_order_acq_rel);
-        }
-    };
     CopyPool::global().run(2 * n_t, [&](size_t i) {
-        bool is_out = false;
-        const size_t pi = claim(i, is_out);
-        if (pi >= n_t) return;  // (not reached: one unit per call)
+        const size_t pi = i < n_t ? i : i - n_t;
         const uint32_t si = (uint32_t)(pi / k), j = (uint32_t)(pi % k);
         const uint32_t y0 = stripe_y0(si), y1 = si + 1 == n_s ? height : stripe_y0(si + 1);
         const size_t so = (size_t)y0 * row, slen = (size_t)(y1 - y0) * row;
@@ -355,7 +302,7 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
         const size_t p0 = std::min(slen, (slen * j / k) & ~(size_t)63);
         const size_t p1 = j + 1 == k ? slen : std::min(slen, (slen * (j + 1) / k) & ~(size_t)63);
         const size_t o = so + p0, len = p1 - p0;
-        if (!is_out) {
+        if (i < n_t) {
             if (frame) stage_piece(pin_in, frame, o, len, in_bytes, ch, nt);  // frame == nullptr: already staged
             if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != k) return;
             // the stripe's last piece: its kernel and event back to back on the stream
