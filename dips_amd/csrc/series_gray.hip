@@ -360,9 +360,6 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
     }
     __syncthreads();
     const uint8_t* lds = reinterpret_cast<const uint8_t*>(lds32);
-    // LAYOUT 4 reads the table only from inline assembly: tell the compiler
-    // it is read, or it drops the copy above and the allocation with it
-    if constexpr (LAYOUT == 4) asm volatile("" : : "v"(lds32) : "memory");
     static_assert(U * 64 * 16 <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)GW + (threadIdx.x >> 6));
