@@ -176,30 +176,22 @@ __device__ __forceinline__ void gstore_one(__amdgpu_buffer_rsrc_t rpart, uint32_
 // LAYOUT 4: layout 3's table and indices, each pixel pair's two entries
 // gathered straight into the halves of one register by ds_read_u16 and
 // ds_read_u16_d16_hi (hipcc does not form the d16 load, so the byte
-// addresses -- one SDWA word-select shift each -- and the loads are inline
-// assembly).  A d16_hi load merges with the register's low half as it is
-// when the load ISSUES (measured: issued behind the first load of the pair,
-// it kept the stale half), so a vec's eight low-half loads are waited for
-// before its eight d16_hi loads issue (gray_lgkm_wait), and those are waited
-// for before the SADs.  Saves the v_perm_b32 that merges the two entries,
-// one per pixel pair.  The table must sit at LDS address 0 (the kernel's
-// only LDS variable).
-__device__ __forceinline__ uint32_t gray_gather_lo(uint32_t i, uint32_t one) {
-    uint32_t r, a;
+// addresses -- one SDWA word-select shift each -- and both loads are inline
+// assembly; LDS returns a wave's reads in order, so the d16_hi half lands
+// after the full-register write of the first).  Saves the v_perm_b32 that
+// merges the two entries, one per pixel pair.  The table must sit at LDS
+// address 0 (the kernel's only LDS variable).  The reads of a vec's four
+// dwords are waited for together (gray_lgkm_wait).
+__device__ __forceinline__ uint32_t gray_gather_pair_d16(uint32_t i, uint32_t one) {
+    uint32_t r, a0, a1;
     asm volatile(
-        "v_lshlrev_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
-        "ds_read_u16 %0, %1"
-        : "=&v"(r), "=&v"(a)
+        "v_lshlrev_b32_sdwa %1, %4, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
+        "v_lshlrev_b32_sdwa %2, %4, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
+        "ds_read_u16 %0, %1\n\t"
+        "ds_read_u16_d16_hi %0, %2"
+        : "=&v"(r), "=&v"(a0), "=&v"(a1)
         : "v"(i), "v"(one));
     return r;
-}
-__device__ __forceinline__ void gray_gather_hi(uint32_t& r, uint32_t i, uint32_t one) {
-    uint32_t a;
-    asm volatile(
-        "v_lshlrev_b32_sdwa %1, %3, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
-        "ds_read_u16_d16_hi %0, %1"
-        : "+v"(r), "=&v"(a)
-        : "v"(i), "v"(one));
 }
 __device__ __forceinline__ void gray_lgkm_wait(uint32_t (&g)[8]) {
     asm volatile("s_waitcnt lgkmcnt(0)"
@@ -233,22 +225,18 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
     for (int u = 0; u < U; ++u) {
         uint32_t g4[8];  // LAYOUT 4: the entry pairs (0, 2), (1, 3) of the vec's dwords
         if constexpr (LAYOUT == 4) {
-            uint32_t ix[8];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t f = cur[u][k], r = rb[u][k];
                 const uint32_t x = f ^ r;
                 const uint32_t col = f ^ ((x << 1) & (gray_band_swizzle(0xFFu) * 0x01010101u));
-                ix[2 * k] = as_u32(
+                const uint32_t i02 = as_u32(
                     __builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x06020400u)), as_u16x2(kk)));
-                ix[2 * k + 1] = as_u32(
+                const uint32_t i13 = as_u32(
                     __builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x07030501u)), as_u16x2(kk)));
-                g4[2 * k] = gray_gather_lo(ix[2 * k], 1u);
-                g4[2 * k + 1] = gray_gather_lo(ix[2 * k + 1], 1u);
+                g4[2 * k] = gray_gather_pair_d16(i02, 1u);
+                g4[2 * k + 1] = gray_gather_pair_d16(i13, 1u);
             }
-            gray_lgkm_wait(g4);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) gray_gather_hi(g4[j], ix[j], 1u);
             gray_lgkm_wait(g4);
         }
 #pragma unroll
