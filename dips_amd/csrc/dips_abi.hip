@@ -229,7 +229,6 @@ int gray_lut_layout() {
         if (e[0] == '0') return 0;
         if (e[0] == '1') return 1;
         if (e[0] == '2') return 2;
-        if (e[0] == '4') return 4;  // layout 3 with d16 LDS gathers (series_gray.hip LAYOUT 4, A/B)
     }
     return 3;
 }
@@ -242,7 +241,7 @@ FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint
     if (nvec == 0 || npx >= (1ull << 31) || n_frames == 0) return g;
     const int layout = gray_lut_layout();
     const int alu = layout == 2 ? dips::gray_alu_vecs(h->p.tau) : 0;
-    const uint64_t U = (uint64_t)(layout == 4 ? 4 : layout >= 2 ? (alu > 0 ? 4 : dips::gray_lut_unroll()) : dips::kUnrollGrayLut);
+    const uint64_t U = (uint64_t)(layout >= 2 ? (alu > 0 ? 4 : dips::gray_lut_unroll()) : dips::kUnrollGrayLut);
     const uint64_t gw = dips::gray_lut_waves(layout, alu);
     g.vec_bytes = nvec * 16u;
     g.tail_px0 = nvec * 16u;

@@ -173,38 +173,13 @@ __device__ __forceinline__ void gstore_one(__amdgpu_buffer_rsrc_t rpart, uint32_
 // One frame of one tile against the reference bytes rb: the 4 per-lane
 // values {SAD, sum d, sum corr, 0} and the wave-wide count.
 // NA > 0 (layout 2): vecs U - NA .. U - 1 take the arithmetic path.
-// LAYOUT 4: layout 3's table and indices, each pixel pair's two entries
-// gathered straight into the halves of one register by ds_read_u16 and
-// ds_read_u16_d16_hi (hipcc does not form the d16 load, so the byte
-// addresses -- one SDWA word-select shift each -- and both loads are inline
-// assembly; LDS returns a wave's reads in order, so the d16_hi half lands
-// after the full-register write of the first).  Saves the v_perm_b32 that
-// merges the two entries, one per pixel pair.  The table must sit at LDS
-// address 0 (the kernel's only LDS variable).  The reads of a vec's four
-// dwords are waited for together (gray_lgkm_wait).
-__device__ __forceinline__ uint32_t gray_gather_pair_d16(uint32_t i, uint32_t one) {
-    uint32_t r, a0, a1;
-    asm volatile(
-        "v_lshlrev_b32_sdwa %1, %4, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0\n\t"
-        "v_lshlrev_b32_sdwa %2, %4, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1\n\t"
-        "ds_read_u16 %0, %1\n\t"
-        "ds_read_u16_d16_hi %0, %2"
-        : "=&v"(r), "=&v"(a0), "=&v"(a1)
-        : "v"(i), "v"(one));
-    return r;
-}
-__device__ __forceinline__ void gray_lgkm_wait(uint32_t (&g)[8]) {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), "+v"(g[6]), "+v"(g[7]));
-}
-
-// LAYOUT 3 / 4: kk = the band clamp K in both u16 halves.
+// LAYOUT 3: kk = the band clamp K in both u16 halves.
 template <int U, int NA, bool MAP, int LAYOUT>
 __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* lds, const uint32_t (&rb)[U][4],
                                            const uint32_t (&cur)[U][4], float thr28, uint32_t kk, uint32_t voff,
                                            uint32_t t, uint32_t* vals, uint32_t& cnt) {
     static_assert(NA == 0 || (LAYOUT == 2 && NA < U), "arithmetic vecs: layout 2, at least one table vec");
-    constexpr bool U16 = LAYOUT >= 2;  // one u16 entry per pixel (layouts 2, 3, 4)
+    constexpr bool U16 = LAYOUT >= 2;  // one u16 entry per pixel (layouts 2, 3)
     uint32_t sad = 0, acc = 0, accd = 0, accc = 0, c = 0;
     uint32_t map[U][4];
     uint32_t alu_s[NA > 0 ? 2 * NA : 1], alu_c = 0;
@@ -223,38 +198,12 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        uint32_t g4[8];  // LAYOUT 4: the entry pairs (0, 2), (1, 3) of the vec's dwords
-        if constexpr (LAYOUT == 4) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t f = cur[u][k], r = rb[u][k];
-                const uint32_t x = f ^ r;
-                const uint32_t col = f ^ ((x << 1) & (gray_band_swizzle(0xFFu) * 0x01010101u));
-                const uint32_t i02 = as_u32(
-                    __builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x06020400u)), as_u16x2(kk)));
-                const uint32_t i13 = as_u32(
-                    __builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x07030501u)), as_u16x2(kk)));
-                g4[2 * k] = gray_gather_pair_d16(i02, 1u);
-                g4[2 * k + 1] = gray_gather_pair_d16(i13, 1u);
-            }
-            gray_lgkm_wait(g4);
-        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t f = cur[u][k], r = rb[u][k];
             sad = __builtin_amdgcn_sad_u8(f, r, sad);
             if constexpr (MAP) map[u][k] = absdiff_bytes(f, r);
             if (u >= U - NA) continue;
-            if constexpr (LAYOUT == 4) {
-                const uint32_t r02 = g4[2 * k], r13 = g4[2 * k + 1];
-                accc = __builtin_amdgcn_sad_u8(r02, 0u, accc);
-                accc = __builtin_amdgcn_sad_u8(r13, 0u, accc);
-                accd = __builtin_amdgcn_sad_u16(r02, 0u, accd);
-                accd = __builtin_amdgcn_sad_u16(r13, 0u, accd);
-                acc = __builtin_amdgcn_sad_u16(r02, 0x00010001u, acc);
-                acc = __builtin_amdgcn_sad_u16(r13, 0x00010001u, acc);
-                continue;
-            }
             // table indices of pixels (0, 2) and (1, 3) as u16 pairs, per byte
             // of the dword at once: layouts 1 / 2 f_i * 256 + r_i (layout 2:
             // r_i ^ sw(f_i)); layout 3 x_i * 256 + (f_i ^ sw3(x_i)),
@@ -357,7 +306,7 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
     const uint32_t rec_off4 = (lane & 15u) == 0u ? (lane >> 4) * 4u : 0x80000000u;
     const float thr28 = a.thr * 268435456.0f;  // 2^28 tau (exact)
     uint32_t kk = 0u;
-    if constexpr (LAYOUT == 3 || LAYOUT == 4) {
+    if constexpr (LAYOUT == 3) {
         // the band clamp from the word after the table: rows x < 2^m hold no
         // selected pair, m = floor(log2(the first row that does)), K = 256 * 2^m - 1
         const uint32_t w = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(a.lut) + kGrayBandOffset);
@@ -506,7 +455,6 @@ const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int
             default: return gray_ptr<4, 3>(per_frame, map);
         }
     }
-    if (layout == 4) return (alu_vecs != 0 || waves != 16u) ? nullptr : gray_ptr<4, 4>(per_frame, map);
     if (layout != 2) return nullptr;
     if (waves != 12u && waves != 16u) return nullptr;
     if (alu_vecs == 0 && waves == 12u) return gray_lut_unroll() == 4 ? gray_ptr<4, 2, 0, 12>(per_frame, map) : nullptr;
@@ -520,7 +468,6 @@ const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int
 }
 
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
-    if (layout == 4) layout = 3;  // layout 4 reads layout 3's table
     if (layout == 3) {
         const hipError_t e = hipMemsetAsync(tab + kGrayBandOffset, 0, 4, s);
         if (e != hipSuccess) return e;

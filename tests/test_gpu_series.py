@@ -377,8 +377,7 @@ def test_unaligned_device_batches(c, mode, offsets, with_map):
 @pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.5, 1.0])
 def test_gray_kernels_agree(mode, tau, monkeypatch):
     """GRAY8 on the table kernel (u16 table keyed by (a ^ b, a) with the band
-    clamp, the default; DIPS_GRAY_LUT=3; =4 the same with d16 LDS gathers),
-    the u16 table keyed by (a, b) (=2),
+    clamp, the default; DIPS_GRAY_LUT=3), the u16 table keyed by (a, b) (=2),
     its two-byte-table layout (=1) and the f32 series_fast_kernel (=0), with
     and without the map, against the oracle -- random and synthetic frames,
     ragged shape included."""
@@ -386,7 +385,7 @@ def test_gray_kernels_agree(mode, tau, monkeypatch):
     for (w, h), kind in [((256, 64), "random"), ((640, 48), "synth"), ((37, 23), "random")]:
         frames = _frames(1, w, h, 9, 40 + w, kind)
         out4, si, dmap = oracle.series(frames, mode=mode, tau=tau, want_map=True)
-        for layout in ("3", "4", "2", "1", "0"):
+        for layout in ("3", "2", "1", "0"):
             monkeypatch.setenv("DIPS_GRAY_LUT", layout)
             op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
             try:
@@ -398,7 +397,7 @@ def test_gray_kernels_agree(mode, tau, monkeypatch):
             _check(got_nomap, out4, si)
 
 
-@pytest.mark.parametrize("layout", ["3", "4", "2"])
+@pytest.mark.parametrize("layout", ["3", "2"])
 @pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.1, 0.5, 1.0])
 def test_gray_table_every_byte_pair(tau, layout, monkeypatch):
     """Every (frame byte a, reference byte b) through the swizzled GRAY8
