@@ -571,3 +571,38 @@ def test_series_intensity_sum_forms_match_oracle(isi, c, mode, monkeypatch):
                     assert np.array_equal(ser.cpu().numpy().view(np.uint64), out4), (isi, tau, chroma)
             finally:
                 op.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_4k_forms_agree_and_match_oracle(mode, monkeypatch):
+    """At the bench's full frame size (4K), the alternative forms of the two
+    series kernels give the same series over a 48-frame batch (a
+    size-independent property): GRAY8 layout 3 (band clamp) = layout 2, and
+    the RGB8 intensity-sum forms ISI = 1 = 2 (SADI) = 0 (f64); the first 4
+    frames of each against the oracle."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    w, h, n, tau = 3840, 2160, 48, 8 / 255
+    for fmt, env, forms in ((PixelFormat.Gray8, "DIPS_GRAY_LUT", ("3", "2")),
+                            (PixelFormat.RGB8, "DIPS_SERIES_ISI", ("1", "2", "0"))):
+        c = int(fmt)
+        shape = (n, h, w) if c == 1 else (n, h, w, c)
+        op = DiffSeriesOperator(fmt, Mode(mode), tau, 0)
+        try:
+            dev = torch.empty(shape, dtype=torch.uint8, device="cuda")
+            op.synth_device(dev, w, h, 0xD1B5, 7)
+            got = {}
+            for form in forms:
+                monkeypatch.setenv(env, form)
+                ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+                op.run_device(dev, ser)
+                torch.cuda.synchronize()
+                got[form] = ser.cpu().numpy().view(np.uint64)
+            monkeypatch.delenv(env)
+            for form in forms[1:]:
+                assert np.array_equal(got[form], got[forms[0]]), (fmt, form)
+            head = dev[:4].cpu().numpy()
+            out4, _, _ = oracle.series(head, mode=mode, tau=tau, nthreads=8)
+            assert np.array_equal(got[forms[0]][:4], out4), fmt
+        finally:
+            op.close()
