@@ -1,0 +1,122 @@
+// alloc_policy_ab.hip -- the headline series kernel (4K RGB8, per-frame,
+// tau 8/255, integer SI) over frame buffers allocated with different memory
+// types (hipExtMallocWithFlags: default coarse-grained, fine-grained,
+// uncached, contiguous), in ONE process, alternated over rounds: does a
+// memory type that skips the caches read the frames for less energy, and so
+// faster under the package power limit?  Same frames in every buffer (one
+// synthesis, copied); the series of every run is compared with the first.
+// Output lines "run <round> <name> <t0> <t1> <median ms> <frac of 8 TB/s>
+// <frames>" for tools/walk_energy.py (--bin build/alloc_policy_ab), which
+// adds the SMU energy of each window.
+// Usage: alloc_policy_ab <frames> <seconds per run> <rounds>
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o build/alloc_policy_ab tools/alloc_policy_ab.hip
+#include "../dips_amd/csrc/series_kernels.hip"
+#include "../dips_amd/csrc/series_v2.hip"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace dips;
+
+static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct Kind {
+    const char* name;
+    unsigned flags;
+};
+
+int main(int argc, char** argv) {
+    const uint32_t W = 3840, H = 2160, C = 3;
+    const uint32_t F = argc > 1 ? (uint32_t)atoi(argv[1]) : 2000;
+    const double secs = argc > 2 ? atof(argv[2]) : 3.0;
+    const int rounds = argc > 3 ? atoi(argv[3]) : 2;
+    const uint64_t fb = (uint64_t)W * H * C, total = fb * F;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) return 1;
+    const std::vector<Kind> kinds = {{"default", hipDeviceMallocDefault},
+                                     {"finegrained", hipDeviceMallocFinegrained},
+                                     {"uncached", hipDeviceMallocUncached},
+                                     {"contiguous", hipDeviceMallocContiguous}};
+    std::vector<uint8_t*> bufs;
+    std::vector<size_t> ok;
+    for (size_t i = 0; i < kinds.size(); ++i) {
+        void* p = nullptr;
+        if (hipExtMallocWithFlags(&p, total, kinds[i].flags) != hipSuccess || !p) {
+            fprintf(stderr, "%s: allocation failed, skipped\n", kinds[i].name);
+            (void)hipGetLastError();
+            bufs.push_back(nullptr);
+            continue;
+        }
+        bufs.push_back(static_cast<uint8_t*>(p));
+        ok.push_back(i);
+    }
+    if (ok.empty() || bufs[ok[0]] == nullptr) return 1;
+    SynthArgs sa{};
+    sa.dst = bufs[ok[0]]; sa.total_bytes = total; sa.frame_bytes = fb; sa.seed = 0xD1B5; sa.t0 = 0;
+    sa.channels = C; sa.width = W; sa.height = H; sa.radius = H / 8;
+    if (launch_synth(sa, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return 1;
+    for (size_t j = 1; j < ok.size(); ++j)
+        if (hipMemcpy(bufs[ok[j]], bufs[ok[0]], total, hipMemcpyDeviceToDevice) != hipSuccess) return 1;
+    const void* k = series_v2_kernel_ptr(3, 0, true, false, false, 1);
+    int occ = 0;
+    if (!k || hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, 256, 0) != hipSuccess || occ < 1) return 1;
+    const uint64_t nvec = fb / 12, tiles = (nvec + 64ull * kUnrollV2 - 1) / (64ull * kUnrollV2);
+    uint64_t* partials = nullptr;
+    dips_series_entry* series = nullptr;
+    SeriesArgs a{};
+    a.frame_bytes = (uint32_t)fb; a.vec_bytes = (uint32_t)fb; a.n_frames = F;
+    a.n_tiles = (uint32_t)tiles; a.items = tiles * F;
+    a.n_waves = (uint32_t)std::min<uint64_t>(a.items, (uint64_t)occ * cus * 4);
+    a.thr = series_threshold(3, 8.0f / 255.0f, 1);
+    if (hipMalloc(&partials, a.items * 16 + 4096) != hipSuccess) return 1;
+    if (hipMalloc(&series, sizeof(dips_series_entry) * F) != hipSuccess) return 1;
+    a.partials = partials;
+    const uint32_t blocks = (a.n_waves + 3) / 4;
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 1;
+    std::vector<dips_series_entry> ref(F), h(F);
+    bool have_ref = false;
+    for (int r = 0; r < rounds; ++r) {
+        for (size_t vi = 0; vi < ok.size(); ++vi) {
+            const size_t i = ok[(r % 2 == 0) ? vi : ok.size() - 1 - vi];
+            SeriesArgs args = a;
+            args.frames = bufs[i];
+            args.ref0 = bufs[i];
+            std::vector<float> ms;
+            const double t0 = now();
+            while (now() - t0 < secs) {
+                (void)hipMemsetAsync(series, 0, sizeof(dips_series_entry) * F, 0);
+                if (hipEventRecord(e0, 0) != hipSuccess) return 1;
+                void* params[] = {&args};
+                if (hipLaunchKernel(k, dim3(blocks), dim3(256), params, 0, 0) != hipSuccess) return 1;
+                if (hipEventRecord(e1, 0) != hipSuccess) return 1;
+                if (launch_series_reduce(partials, F, a.n_tiles, 0, series, 0) != hipSuccess) return 1;
+                if (hipDeviceSynchronize() != hipSuccess) return 1;
+                float t = 0;
+                (void)hipEventElapsedTime(&t, e0, e1);
+                ms.push_back(t);
+            }
+            const double t1 = now();
+            if (hipMemcpy(h.data(), series, sizeof(dips_series_entry) * F, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+            if (!have_ref) {
+                ref = h;
+                have_ref = true;
+            }
+            const bool same = std::equal(h.begin(), h.end(), ref.begin(), [](const dips_series_entry& x,
+                                                                           const dips_series_entry& y) {
+                return x.sad == y.sad && x.sj == y.sj && x.count == y.count && x.si_fixed == y.si_fixed;
+            });
+            std::sort(ms.begin(), ms.end());
+            const double med = ms[ms.size() / 2];
+            printf("run\t%d\t%s%s\t%.6f\t%.6f\t%.4f\t%.4f\t%u\n", r, kinds[i].name, same ? "" : " DIFF", t0, t1, med,
+                   (double)total / (med / 1e3) / 8e12, F);
+            fflush(stdout);
+        }
+    }
+    return 0;
+}
