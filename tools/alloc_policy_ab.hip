@@ -8,7 +8,9 @@
 // Output lines "run <round> <name> <t0> <t1> <median ms> <frac of 8 TB/s>
 // <frames>" for tools/walk_energy.py (--bin build/alloc_policy_ab), which
 // adds the SMU energy of each window.
-// Usage: alloc_policy_ab <frames> <seconds per run> <rounds>
+// Usage: alloc_policy_ab <frames> <seconds per run> <rounds> [kinds, e.g.
+// default,finegrained,default,finegrained: repeated kinds separate the memory
+// type from where a buffer happens to land]
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o build/alloc_policy_ab tools/alloc_policy_ab.hip
 #include "../dips_amd/csrc/series_kernels.hip"
 #include "../dips_amd/csrc/series_v2.hip"
@@ -17,6 +19,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 using namespace dips;
@@ -38,10 +41,22 @@ int main(int argc, char** argv) {
     const uint64_t fb = (uint64_t)W * H * C, total = fb * F;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess) return 1;
-    const std::vector<Kind> kinds = {{"default", hipDeviceMallocDefault},
-                                     {"finegrained", hipDeviceMallocFinegrained},
-                                     {"uncached", hipDeviceMallocUncached},
-                                     {"contiguous", hipDeviceMallocContiguous}};
+    const std::vector<Kind> all = {{"default", hipDeviceMallocDefault},
+                                   {"finegrained", hipDeviceMallocFinegrained},
+                                   {"uncached", hipDeviceMallocUncached},
+                                   {"contiguous", hipDeviceMallocContiguous}};
+    std::vector<Kind> kinds;
+    {
+        const std::string list = argc > 4 ? argv[4] : "default,finegrained,uncached,contiguous";
+        size_t pos = 0;
+        while (pos <= list.size()) {
+            const size_t e = std::min(list.find(',', pos), list.size());
+            const std::string name = list.substr(pos, e - pos);
+            for (const Kind& kd : all)
+                if (name == kd.name) kinds.push_back(kd);
+            pos = e + 1;
+        }
+    }
     std::vector<uint8_t*> bufs;
     std::vector<size_t> ok;
     for (size_t i = 0; i < kinds.size(); ++i) {
@@ -113,7 +128,7 @@ int main(int argc, char** argv) {
             });
             std::sort(ms.begin(), ms.end());
             const double med = ms[ms.size() / 2];
-            printf("run\t%d\t%s%s\t%.6f\t%.6f\t%.4f\t%.4f\t%u\n", r, kinds[i].name, same ? "" : " DIFF", t0, t1, med,
+            printf("run\t%d\t%s#%zu%s\t%.6f\t%.6f\t%.4f\t%.4f\t%u\n", r, kinds[i].name, i, same ? "" : " DIFF", t0, t1, med,
                    (double)total / (med / 1e3) / 8e12, F);
             fflush(stdout);
         }
