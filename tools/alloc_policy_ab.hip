@@ -10,7 +10,8 @@
 // adds the SMU energy of each window.
 // Usage: alloc_policy_ab <frames> <seconds per run> <rounds> [kinds, e.g.
 // default,finegrained,default,finegrained: repeated kinds separate the memory
-// type from where a buffer happens to land]
+// type from where a buffer happens to land; "padN" allocates N GiB that is
+// not measured, before the next buffer)]
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o build/alloc_policy_ab tools/alloc_policy_ab.hip
 #include "../dips_amd/csrc/series_kernels.hip"
 #include "../dips_amd/csrc/series_v2.hip"
@@ -19,6 +20,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -54,6 +56,7 @@ int main(int argc, char** argv) {
             const std::string name = list.substr(pos, e - pos);
             for (const Kind& kd : all)
                 if (name == kd.name) kinds.push_back(kd);
+            if (name.rfind("pad", 0) == 0) kinds.push_back({strdup(name.c_str()), 0x80000000u});
             pos = e + 1;
         }
     }
@@ -61,6 +64,13 @@ int main(int argc, char** argv) {
     std::vector<size_t> ok;
     for (size_t i = 0; i < kinds.size(); ++i) {
         void* p = nullptr;
+        if (kinds[i].flags == 0x80000000u) {  // pad: N GiB, not measured
+            const size_t n = (size_t)atoi(kinds[i].name + 3) << 30;
+            if (hipMalloc(&p, n) != hipSuccess) return 1;
+            fprintf(stderr, "%s at %p\n", kinds[i].name, p);
+            bufs.push_back(nullptr);
+            continue;
+        }
         if (hipExtMallocWithFlags(&p, total, kinds[i].flags) != hipSuccess || !p) {
             fprintf(stderr, "%s: allocation failed, skipped\n", kinds[i].name);
             (void)hipGetLastError();
@@ -69,6 +79,7 @@ int main(int argc, char** argv) {
         }
         bufs.push_back(static_cast<uint8_t*>(p));
         ok.push_back(i);
+        fprintf(stderr, "%s#%zu at %p\n", kinds[i].name, i, p);
     }
     if (ok.empty() || bufs[ok[0]] == nullptr) return 1;
     SynthArgs sa{};
