@@ -11,7 +11,8 @@
 // Usage: alloc_policy_ab <frames> <seconds per run> <rounds> [kinds, e.g.
 // default,finegrained,default,finegrained: repeated kinds separate the memory
 // type from where a buffer happens to land; "padN" allocates N GiB that is
-// not measured, before the next buffer)]
+// not measured, before the next buffer)] [L,L,...: also the part-major
+// schedule (series_v2_body SCHED = 1) with parts of L frames, per buffer]
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o build/alloc_policy_ab tools/alloc_policy_ab.hip
 #include "../dips_amd/csrc/series_kernels.hip"
 #include "../dips_amd/csrc/series_v2.hip"
@@ -28,6 +29,10 @@ using namespace dips;
 
 static double now() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+__global__ __launch_bounds__(256, (v2_min_waves<3, kUnrollV2, true, false, false, 1>())) void parts_isi(SeriesArgs a) {
+    series_v2_body<3, 0, kUnrollV2, true, false, kAuxNT, kAuxNT, 1, false, 1>(a);
 }
 
 struct Kind {
@@ -88,9 +93,16 @@ int main(int argc, char** argv) {
     if (launch_synth(sa, 0) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return 1;
     for (size_t j = 1; j < ok.size(); ++j)
         if (hipMemcpy(bufs[ok[j]], bufs[ok[0]], total, hipMemcpyDeviceToDevice) != hipSuccess) return 1;
-    const void* k = series_v2_kernel_ptr(3, 0, true, false, false, 1);
+    std::vector<uint32_t> Ls = {0};  // 0: the shipped schedule
+    if (argc > 5)
+        for (char* q = argv[5]; *q;) {
+            Ls.push_back((uint32_t)strtoul(q, &q, 10));
+            if (*q == ',') ++q;
+        }
+    const void* k0 = series_v2_kernel_ptr(3, 0, true, false, false, 1);
+
     int occ = 0;
-    if (!k || hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, 256, 0) != hipSuccess || occ < 1) return 1;
+    if (!k0 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k0, 256, 0) != hipSuccess || occ < 1) return 1;
     const uint64_t nvec = fb / 12, tiles = (nvec + 64ull * kUnrollV2 - 1) / (64ull * kUnrollV2);
     uint64_t* partials = nullptr;
     dips_series_entry* series = nullptr;
@@ -108,11 +120,15 @@ int main(int argc, char** argv) {
     std::vector<dips_series_entry> ref(F), h(F);
     bool have_ref = false;
     for (int r = 0; r < rounds; ++r) {
-        for (size_t vi = 0; vi < ok.size(); ++vi) {
-            const size_t i = ok[(r % 2 == 0) ? vi : ok.size() - 1 - vi];
+        for (size_t vj = 0; vj < ok.size() * Ls.size(); ++vj) {
+            const size_t vv = (r % 2 == 0) ? vj : ok.size() * Ls.size() - 1 - vj;
+            const size_t i = ok[vv / Ls.size()];
+            const uint32_t L = Ls[vv % Ls.size()];
+            const void* k = L == 0 ? k0 : (const void*)&parts_isi;
             SeriesArgs args = a;
             args.frames = bufs[i];
             args.ref0 = bufs[i];
+            args.part_frames = L;
             std::vector<float> ms;
             const double t0 = now();
             while (now() - t0 < secs) {
@@ -139,7 +155,8 @@ int main(int argc, char** argv) {
             });
             std::sort(ms.begin(), ms.end());
             const double med = ms[ms.size() / 2];
-            printf("run\t%d\t%s#%zu%s\t%.6f\t%.6f\t%.4f\t%.4f\t%u\n", r, kinds[i].name, i, same ? "" : " DIFF", t0, t1, med,
+            printf("run\t%d\t%s#%zu/%s%u%s\t%.6f\t%.6f\t%.4f\t%.4f\t%u\n", r, kinds[i].name, i, L ? "P" : "S", L,
+                   same ? "" : " DIFF", t0, t1, med,
                    (double)total / (med / 1e3) / 8e12, F);
             fflush(stdout);
         }
