@@ -13,6 +13,7 @@
 // type from where a buffer happens to land; "padN" allocates N GiB that is
 // not measured, before the next buffer)] [L,L,...: also the part-major
 // schedule (series_v2_body SCHED = 1) with parts of L frames, per buffer]
+// [waves of the part-major runs: e.g. 4050 = 32,400 items of L = 1250 / 8]
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o build/alloc_policy_ab tools/alloc_policy_ab.hip
 #include "../dips_amd/csrc/series_kernels.hip"
 #include "../dips_amd/csrc/series_v2.hip"
@@ -114,7 +115,7 @@ int main(int argc, char** argv) {
     if (hipMalloc(&partials, a.items * 16 + 4096) != hipSuccess) return 1;
     if (hipMalloc(&series, sizeof(dips_series_entry) * F) != hipSuccess) return 1;
     a.partials = partials;
-    const uint32_t blocks = (a.n_waves + 3) / 4;
+
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return 1;
     std::vector<dips_series_entry> ref(F), h(F);
@@ -124,11 +125,14 @@ int main(int argc, char** argv) {
             const size_t vv = (r % 2 == 0) ? vj : ok.size() * Ls.size() - 1 - vj;
             const size_t i = ok[vv / Ls.size()];
             const uint32_t L = Ls[vv % Ls.size()];
+            (void)0;
             const void* k = L == 0 ? k0 : (const void*)&parts_isi;
             SeriesArgs args = a;
             args.frames = bufs[i];
             args.ref0 = bufs[i];
             args.part_frames = L;
+            if (L != 0 && argc > 6) args.n_waves = (uint32_t)atoi(argv[6]);
+            const uint32_t blocks = (args.n_waves + 3) / 4;
             std::vector<float> ms;
             const double t0 = now();
             while (now() - t0 < secs) {
