@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """isi_ab.py -- the RGB8 series kernel's intensity-sum forms, named in argv[5]
-(default "isi,f64"; "sadi" = DIPS_SERIES_ISI=2): the integer intensity sum
+(default "isi,f64"; "sadi" = DIPS_SERIES_ISI=2; "contig" / "parts" =
+DIPS_SERIES_PARTS=0 / 1, the schedule): the integer intensity sum
 (series_v2.hip ISI, the default for tau >= 2^-5) against the f64 sum
 (DIPS_SERIES_ISI=0), alternated in ONE process over ONE resident buffer of
 the headline workload (5000 4K RGB8 frames, 'per-frame', tau 8/255): kernel
@@ -31,7 +32,8 @@ def main():
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     mode = Mode.PerFrame if (len(sys.argv) <= 4 or sys.argv[4] == "per-frame") else Mode.Overall
     names = (sys.argv[5] if len(sys.argv) > 5 else "isi,f64").split(",")
-    env_of = {"f64": "0", "isi": "1", "sadi": "2"}
+    env_of = {"f64": ("DIPS_SERIES_ISI", "0"), "isi": ("DIPS_SERIES_ISI", "1"), "sadi": ("DIPS_SERIES_ISI", "2"),
+              "contig": ("DIPS_SERIES_PARTS", "0"), "parts": ("DIPS_SERIES_PARTS", "1")}
     frames = torch.empty((F, H, W, 3), dtype=torch.uint8, device="cuda")
     op = DiffSeriesOperator(PixelFormat.RGB8, mode, 8 / 255, time_kernel=True)
     op.synth_device(frames, W, H, 0xD1B5, 0)
@@ -49,8 +51,10 @@ def main():
     res = {}
     for rnd in range(rounds):
         order = [(k, env_of[k]) for k in names]
-        for name, env in (order if rnd % 2 == 0 else order[::-1]):
-            os.environ["DIPS_SERIES_ISI"] = env
+        for name, (var, env) in (order if rnd % 2 == 0 else order[::-1]):
+            os.environ.pop("DIPS_SERIES_ISI", None)
+            os.environ.pop("DIPS_SERIES_PARTS", None)
+            os.environ[var] = env
             r = None if mode == Mode.PerFrame else ref
             op.run_device(frames, series[name], ref=r)  # warm
             torch.cuda.synchronize()
@@ -79,6 +83,7 @@ def main():
             res.setdefault(name, []).append(rec)
             print(json.dumps(rec), flush=True)
     os.environ.pop("DIPS_SERIES_ISI", None)
+    os.environ.pop("DIPS_SERIES_PARTS", None)
     same = all(bool(torch.equal(series[names[0]], series[k])) for k in names[1:])
     summ = {"summary": True, "mode": "per-frame" if mode == Mode.PerFrame else "overall", "series_equal": same}
     for k, v in res.items():
