@@ -303,6 +303,8 @@ FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint
     }
     const uint64_t resident = per_simd * 4u * (uint64_t)h->cu_count;
     g.n_waves = g.items < resident ? g.items : resident;
+    // 'per-frame' batches: the part-major schedule, as for RGB8 (part_geometry)
+    if (h->p.mode == DIPS_MODE_PER_FRAME) part_geometry(g, n_frames, resident);
     g.blocks = (g.n_waves + gw - 1) / gw;
     g.ok = g.n_tiles < (1ull << 32) && g.blocks < (1ull << 31);
     return g;
@@ -400,7 +402,7 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         a.n_waves = (uint32_t)g.n_waves;
         a.thr = dips::series_threshold(C, h->p.tau, isi);
         a.thr_int = isi == 2 ? dips::series_sadi_threshold(h->p.tau) : 0u;
-        a.part_frames = glut ? 0u : g.part_frames;
+        a.part_frames = g.part_frames;  // 0: contiguous ranges (part_geometry)
         if (glut) {
             a.lut = h->gray_lut.p;
             const int alu = h->gray_lut_layout == 2 ? dips::gray_alu_vecs(h->p.tau) : 0;

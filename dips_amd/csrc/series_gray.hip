@@ -34,6 +34,7 @@
 #include "series_common.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dips {
 
@@ -315,15 +316,32 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
         kk = kc | (kc << 16);
     }
 
+    // one contiguous (tile, frame) range per wave, or (a.part_frames = L > 0)
+    // the part-major schedule of series_v2.hip: items (part, tile) dealt with
+    // stride n_waves, concurrent waves on adjacent tiles of the same frames
     uint64_t i = (uint64_t)wave * a.items / a.n_waves;
     const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
-    while (i < iend) {
-        const uint32_t tile = (uint32_t)(i / a.n_frames);
-        const uint32_t t0 = (uint32_t)(i - (uint64_t)tile * a.n_frames);
-        const uint64_t remaining = iend - i;
-        const uint32_t tend =
-            (uint32_t)((uint64_t)a.n_frames < t0 + remaining ? (uint64_t)a.n_frames : t0 + remaining);
-        i += tend - t0;
+    const bool parts = PF && a.part_frames != 0u;  // wave-uniform; per-frame batches only
+    const uint32_t plen = parts ? a.part_frames : 1u;
+    const uint64_t pitems = parts ? (uint64_t)((a.n_frames + plen - 1) / plen) * a.n_tiles : 0u;
+    uint64_t it = wave;
+    while (true) {
+        uint32_t tile, t0, tend;
+        if (!parts) {
+            if (i >= iend) break;
+            tile = (uint32_t)(i / a.n_frames);
+            t0 = (uint32_t)(i - (uint64_t)tile * a.n_frames);
+            const uint64_t remaining = iend - i;
+            tend = (uint32_t)((uint64_t)a.n_frames < t0 + remaining ? (uint64_t)a.n_frames : t0 + remaining);
+            i += tend - t0;
+        } else {
+            if (it >= pitems) break;
+            const uint32_t part = (uint32_t)(it / a.n_tiles);
+            tile = (uint32_t)(it - (uint64_t)part * a.n_tiles);
+            t0 = part * plen;
+            tend = min(a.n_frames, t0 + plen);
+            it += a.n_waves;
+        }
         const uint32_t n = tend - t0;
         const uint32_t tlast = tend - 1;
         const uint32_t voff = (tile * U * 64u + lane) * 16u;
@@ -383,8 +401,11 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
                 gstore_pair(rpart, t0 + k + 2 * h, rec_off8, lane, y, c0, c1);
             }
         }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
+        // tail: up to 3 frames (written out: with the part-major schedule
+        // hipcc no longer unrolls a loop here, and a rolled one would index
+        // the register ring at run time)
+        auto tail = [&](auto jc) {
+            constexpr int j = decltype(jc)::value;
             if (k + (uint32_t)j < n) {
                 uint32_t v[4], c;
                 const uint32_t tf = t0 + k + (uint32_t)j;
@@ -395,7 +416,10 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
                 const uint32_t y = wave_sum4_lanes(v);
                 gstore_one(rpart, tf, rec_off4, lane, y, c);
             }
-        }
+        };
+        tail(std::integral_constant<int, 0>{});
+        tail(std::integral_constant<int, 1>{});
+        tail(std::integral_constant<int, 2>{});
     }
 }
 

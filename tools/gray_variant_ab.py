@@ -3,7 +3,8 @@
 read per call: vecs per lane of the layout-2 table (a number: DIPS_GRAY_LUT_U),
 arithmetic vecs and waves per group ("a<NA>w<W>": DIPS_GRAY_ALU /
 DIPS_GRAY_ALU_WAVES) or the table layout ("L3", "L2", "L3u3": DIPS_GRAY_LUT,
-U = 4 or the number after u);
+U = 4 or the number after u; a trailing "c": DIPS_SERIES_PARTS=0, the
+contiguous ranges instead of the part-major schedule);
 one batch of 4K gray8 frames, per-frame, tau 8/255; variants alternated over
 rounds, kernel time by hipEvents, series compared with the first variant's.
 Run on the GPU box: python tools/gray_variant_ab.py [rounds] [frames] [variants] [pf|overall] [map|nomap]
@@ -46,6 +47,11 @@ def main():
     ref = None
     for r in range(rounds):
         for v in variants:
+            name = v
+            os.environ.pop("DIPS_SERIES_PARTS", None)
+            if v.endswith("c"):  # ...c: contiguous ranges instead of the part-major schedule
+                os.environ["DIPS_SERIES_PARTS"] = "0"
+                v = v[:-1]
             if v.startswith("L"):  # L<layout>[u<U>]
                 lay, _, u = v[1:].partition("u")
                 os.environ["DIPS_GRAY_LUT"] = lay
@@ -71,7 +77,7 @@ def main():
             if ref is None:
                 ref = h
             gbs = n * W * H * (2 if with_map else 1) / (ms / 1e3) / 1e9
-            print(json.dumps({"round": r, "variant": v, "mode": mode, "map": with_map, "content": content, "kernel_ms": round(ms, 4), "GBps": round(gbs, 1),
+            print(json.dumps({"round": r, "variant": name, "mode": mode, "map": with_map, "content": content, "kernel_ms": round(ms, 4), "GBps": round(gbs, 1),
                               "frac_of_8TBps": round(gbs / 8000, 4), "series_equal_first": bool(np.array_equal(h, ref))}),
                   flush=True)
     op.close()
