@@ -606,3 +606,48 @@ def test_4k_forms_agree_and_match_oracle(mode, monkeypatch):
             assert np.array_equal(got[forms[0]][:4], out4), fmt
         finally:
             op.close()
+
+
+@pytest.mark.parametrize("fmt_name,w,h,n", [("RGB8", 1920, 1080, 523), ("RGBA8", 1920, 1080, 525),
+                                             ("Gray8", 2048, 1536, 1000)])
+def test_part_major_schedule_matches_contiguous_and_oracle(fmt_name, w, h, n, monkeypatch):
+    """'Per-frame' batches of >= 256 frames run the part-major schedule
+    (dips_abi.hip part_geometry; series_v2.hip / series_gray.hip item loop).
+    These shapes take it on a 256-CU MI355X: 1080p RGB8 4 parts of 131
+    frames (the last 130), RGBA8 4 parts of 132 (the last 129), 2048x1536
+    gray8 7 parts of 143 (the last 142), so items start mid-batch, segments
+    end in 0- to 3-frame tails and the last part is short.  The series (and the |F - R| map for RGB8)
+    must equal the contiguous schedule's (DIPS_SERIES_PARTS=0) bit for bit,
+    and every frame must match the oracle."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    fmt = getattr(PixelFormat, fmt_name)
+    c, tau = int(fmt), 8 / 255
+    shape = (n, h, w) if c == 1 else (n, h, w, c)
+    want_map = c == 3
+    op = DiffSeriesOperator(fmt, Mode.PerFrame, tau, 0)
+    try:
+        dev = torch.empty(shape, dtype=torch.uint8, device="cuda")
+        op.synth_device(dev, w, h, 0xA11CE, 3)
+        got, maps = {}, {}
+        for parts in ("1", "0"):
+            monkeypatch.setenv("DIPS_SERIES_PARTS", parts)
+            ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+            dmap = torch.empty_like(dev) if want_map else None
+            op.run_device(dev, ser, map_out=dmap)
+            torch.cuda.synchronize()
+            got[parts] = ser.cpu().numpy().view(np.uint64)
+            if want_map:
+                maps[parts] = dmap
+        monkeypatch.delenv("DIPS_SERIES_PARTS")
+        assert np.array_equal(got["1"], got["0"])
+        if want_map:
+            assert torch.equal(maps["1"], maps["0"])
+        frames = dev.cpu().numpy()
+        out4, _, omap = oracle.series(frames, mode=1, tau=tau, want_map=want_map, nthreads=16)
+        bad = np.nonzero(~np.all(got["1"] == out4, axis=1))[0]
+        assert bad.size == 0, f"frames differing from the oracle: {bad[:10]}"
+        if want_map:
+            assert np.array_equal(maps["1"].cpu().numpy(), omap)
+    finally:
+        op.close()
