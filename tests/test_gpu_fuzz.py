@@ -205,3 +205,67 @@ def test_random_alt_runs_match_oracle():
             r.close()
         got = np.concatenate(outs)
         assert np.array_equal(got, want), (what, np.argwhere(got != want)[:4])
+
+
+COMPAT_CASES = 60
+COMPAT_OPS = 40
+
+
+def test_random_compute_state_properties_match_oracle():
+    """dips-compat ComputeState (dips/src/gpu/mod.rs:170-397, lib.rs:233-246)
+    on drawn properties -- colour, window 1-6, sigmoid scalar, filter, chroma
+    -- and frame shapes, each case a short random sequence of add_texture /
+    dispatch / frame_callback / frame_callback_batch / start_texture against
+    the oracle's ComputeState, every output bit-exact.  (The interleaving
+    surface with streams and resume is test_gpu_sequence.py's, on fixed
+    properties.)"""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
+
+    rng = np.random.default_rng(SEED + 2)
+    for case in range(COMPAT_CASES):
+        colorize = bool(rng.random() < 0.5)
+        window = int(rng.choice([1, 1, 2, 3, 4, 5, 6]))
+        scalar = _alt_scalar(rng)
+        filt = int(rng.choice([0, 1, 255]))
+        chroma = int(rng.integers(0, 4))
+        w, h = int(rng.integers(1, 90)), int(rng.integers(1, 50))
+        what = dict(case=case, colorize=colorize, window=window, scalar=scalar, filt=filt, chroma=chroma, w=w, h=h)
+        gpu = ComputeState(colorize, window, scalar, DiPsFilter(filt), ChromaFilter(chroma))
+        ora = oracle.ComputeState(colorize, window, scalar, filt, chroma)
+        levels = rng.integers(0, 256, int(rng.integers(2, 7)), dtype=np.uint8) if rng.random() < 0.3 else None
+
+        def frame():
+            if levels is not None:  # few distinct bytes: ties in the temporal and spatial medians
+                return levels[rng.integers(0, levels.size, (h, w, 4))]
+            return rng.integers(0, 256, (h, w, 4), dtype=np.uint8)
+
+        try:
+            for i in range(COMPAT_OPS):
+                op = rng.choice(["add", "dispatch", "callback", "batch", "start"], p=[0.3, 0.25, 0.2, 0.15, 0.1])
+                where = (what, i, op)
+                if op == "add":
+                    f = frame()
+                    gpu.add_texture(w, h, f)
+                    ora.add_texture(w, h, f)
+                elif op == "dispatch":
+                    a, b = gpu.dispatch(), ora.dispatch()
+                    assert (a is None) == (b is None), where
+                    if b is not None:
+                        assert np.array_equal(a, b), (where, np.argwhere(a != b)[:4])
+                elif op == "callback":
+                    f = frame()
+                    a = frame_callback(w, h, f, gpu)
+                    b = oracle.frame_callback(w, h, f, ora)
+                    assert np.array_equal(a, b), (where, np.argwhere(a != b)[:4])
+                elif op == "batch":
+                    fr = np.stack([frame() for _ in range(int(rng.integers(1, 6)))])
+                    a = gpu.frame_callback_batch(w, h, fr)
+                    b = np.stack([oracle.frame_callback(w, h, f, ora) for f in fr])
+                    assert np.array_equal(a, b), (where, np.argwhere(a != b)[:4])
+                else:
+                    a, b = gpu.start_texture(), ora.start_texture()
+                    assert (a is None) == (b is None), where
+                    if b is not None:
+                        assert np.array_equal(a, b), where
+        finally:
+            gpu.close()
