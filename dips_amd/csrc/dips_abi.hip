@@ -334,11 +334,12 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
 
     FastGeom g;
     const bool glut = C == 1 && gray_lut_enabled();
-    // RGB8 frames off a 4-byte boundary (an odd frame stride or an offset
-    // pointer) run the aligned-load form of the kernel (series_v2.hip ALIGN)
-    // (DIPS_SERIES_ALIGN=0: the byte-unaligned 12-B loads instead, A/B)
+    // RGB8 / RGBA8 frames off a 4-byte boundary (an odd frame stride or an
+    // offset pointer) run the aligned-load form of the kernel (series_v2.hip
+    // ALIGN) (DIPS_SERIES_ALIGN=0: the byte-unaligned 12-/16-B loads instead,
+    // A/B)
     const char* align_env = std::getenv("DIPS_SERIES_ALIGN");
-    const bool align = C == 3 && ((((uintptr_t)frames | (uintptr_t)fb | (uintptr_t)ref0) & 3u) != 0u) &&
+    const bool align = (C == 3 || C == 4) && ((((uintptr_t)frames | (uintptr_t)fb | (uintptr_t)ref0) & 3u) != 0u) &&
                        !(align_env && align_env[0] == '0');
     // RGB8 / RGBA8 with tau >= 2^-5: the integer intensity sum (series_v2.hip
     // ISI = 1, or 2 = SADI with DIPS_SERIES_ISI=2; DIPS_SERIES_ISI=0 keeps the

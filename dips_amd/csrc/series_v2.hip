@@ -82,7 +82,7 @@ __device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t c) 
 // (updated to this frame's state in per-frame mode) and the reference bytes
 // `rb`; produce the 4 per-lane values {SAD, SJ, H, L} and the wave-wide count.
 // rb / cur rows hold LR / LC dwords, the first Fmt<C>::NDW of which are the
-// vec's bytes (LC = 4 for RGB8 in the aligned-load form, see load_frame).
+// vec's bytes (LC = NDW + 1 in the aligned-load form, see load_at).
 template <int C, int CH, int U, bool PF, bool MAP, int SAUX = kAuxNT, int LR = Fmt<C>::NDW, int LC = Fmt<C>::NDW,
           int ISI = 0>
 __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], const uint32_t (&rb)[U][LR],
@@ -205,7 +205,7 @@ __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t
 // VGPRs; 4 and 5 waves per SIMD run the ISI kernel at the same speed).
 template <int C, int U, bool PF, bool MAP, bool ALIGN = false, int ISI = 0>
 constexpr int v2_min_waves() {
-    return ALIGN ? (MAP ? 1 : 4)
+    return ALIGN ? (MAP ? 1 : (C == 4 ? 3 : 4))  // RGBA8: 5 dwords per vec spill at 128 VGPRs
                  : ((C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : (ISI == 2 ? 4 : 5))) : 1);
 }
 
@@ -217,10 +217,14 @@ constexpr int v2_min_waves() {
 // Byte-unaligned 12-B buffer loads return the same bytes but cost extra
 // cache-line requests (62-63 % of 8 TB/s against 71.7 % aligned,
 // profiles/r02_fallback_rate_after.jsonl, r02_unaligned_probe.txt).
-__device__ __forceinline__ void funnel3(uint32_t (&v)[4], uint32_t sh) {
-    v[0] = __builtin_amdgcn_alignbyte(v[1], v[0], sh);
-    v[1] = __builtin_amdgcn_alignbyte(v[2], v[1], sh);
-    v[2] = __builtin_amdgcn_alignbyte(v[3], v[2], sh);
+// RGBA8 frames are off a 4-byte boundary only through an offset pointer
+// (their stride is a multiple of 4); their 16-B vec comes out of an aligned
+// dwordx4 plus the next dword (20 bytes, 4 funnel shifts).
+template <int N, int L>
+__device__ __forceinline__ void funnel(uint32_t (&v)[L], uint32_t sh) {
+    static_assert(L > N, "a funnel needs the dword after the vec");
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = __builtin_amdgcn_alignbyte(v[k + 1], v[k], sh);
 }
 
 // The kernel body; AUX / SAUX are the cache-policy bits of the frame loads /
@@ -239,8 +243,8 @@ template <int C, int CH, int U, bool PF, bool MAP, int AUX, int SAUX, int SCHED 
 __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
     constexpr int CW = ISI == 2 ? 0 : 1;  // record word of the count
     using F = Fmt<C>;
-    static_assert(!ALIGN || C == 3, "the aligned-load form is the RGB8 one");
-    constexpr int LW = ALIGN ? 4 : F::NDW;  // dwords loaded per vec
+    static_assert(!ALIGN || C == 3 || C == 4, "the aligned-load form is the RGB8 / RGBA8 one");
+    constexpr int LW = ALIGN ? F::NDW + 1 : F::NDW;  // dwords loaded per vec
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -295,6 +299,8 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
                     dst[u][1] = x.y;
                     dst[u][2] = x.z;
                     dst[u][3] = x.w;
+                    if constexpr (C == 4)
+                        dst[u][4] = __builtin_amdgcn_raw_buffer_load_b32(r, voff + (uint32_t)(u * 64 * F::VB + 16), 0, AUX);
                 }
             } else {
                 const __amdgpu_buffer_rsrc_t r = make_rsrc(p, vb);
@@ -333,7 +339,7 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
             if constexpr (ALIGN) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    funnel3(buf[j][u], sh[j]);
+                    funnel<F::NDW>(buf[j][u], sh[j]);
                     buf[j][u][0] &= keep[u];
                 }
             }
@@ -356,7 +362,7 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if constexpr (ALIGN) {
-                    funnel3(dref[u], rsh);
+                    funnel<F::NDW>(dref[u], rsh);
                     dref[u][0] &= keep[u];
                 }
                 uint32_t dv[F::NDW];
@@ -423,7 +429,7 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP, ALIGN, ISI>())) v
 // ---------------------------------------------------------------------------
 template <int C, int CH, bool PF, bool MAP, bool ALIGN, int ISI>
 static const void* v2_ptr() {
-    return reinterpret_cast<const void*>(&series_v2_kernel<C, CH, kUnrollV2, PF, MAP, ALIGN && C == 3, ISI>);
+    return reinterpret_cast<const void*>(&series_v2_kernel<C, CH, kUnrollV2, PF, MAP, ALIGN && (C == 3 || C == 4), ISI>);
 }
 
 template <int C, bool ALIGN, int ISI>
@@ -452,8 +458,11 @@ const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool 
                 return align ? pick_v2<3, true, 1>(chroma, per_frame, map) : pick_v2<3, false, 1>(chroma, per_frame, map);
             return align ? pick_v2<3, true, 0>(chroma, per_frame, map) : pick_v2<3, false, 0>(chroma, per_frame, map);
         case 4:
-            if (isi == 2) return pick_v2<4, false, 2>(chroma, per_frame, map);
-            return isi == 1 ? pick_v2<4, false, 1>(chroma, per_frame, map) : pick_v2<4, false, 0>(chroma, per_frame, map);
+            if (isi == 2)
+                return align ? pick_v2<4, true, 2>(chroma, per_frame, map) : pick_v2<4, false, 2>(chroma, per_frame, map);
+            if (isi == 1)
+                return align ? pick_v2<4, true, 1>(chroma, per_frame, map) : pick_v2<4, false, 1>(chroma, per_frame, map);
+            return align ? pick_v2<4, true, 0>(chroma, per_frame, map) : pick_v2<4, false, 0>(chroma, per_frame, map);
         default: return nullptr;
     }
 }

@@ -336,9 +336,10 @@ def test_unaligned_device_batches(c, mode, offsets, with_map):
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     fo, ro, mo = offsets
-    # (RGB8 frames off a 4-byte boundary -- an offset batch, or a stride
-    # W*H*3 that is not a multiple of 4 such as (62, 33)'s 6138 -- run the
-    # aligned-load kernel, series_v2.hip ALIGN)
+    # (RGB8 / RGBA8 frames off a 4-byte boundary -- an offset batch, or an
+    # RGB8 stride W*H*3 that is not a multiple of 4 such as (62, 33)'s 6138
+    # -- run the aligned-load kernel, series_v2.hip ALIGN; the reference at
+    # its own offset gets its own funnel shift)
     for (w, h) in [(64, 48), (62, 33)] + RAGGED_SHAPES:
         for tau, chroma in [(0.0, 0), (8 / 255, 0 if c == 1 else 2)]:
             n = 9
@@ -558,17 +559,17 @@ def test_series_intensity_sum_forms_match_oracle(isi, c, mode, monkeypatch):
                     _check(got, out4, si, gmap, dmap)
                     got, _ = op(fr)
                     _check(got, out4, si)
-                if c == 3:  # frames off a 4-byte boundary: the aligned-load form
-                    import torch
-                    fr = clips[0]
+                # frames off a 4-byte boundary: the aligned-load form
+                import torch
+                for fr, off in ((clips[0], 1 if c == 3 else 3), (clips[2], 2)):
                     buf = torch.empty(fr.nbytes + 8, dtype=torch.uint8, device="cuda")
-                    dev = buf[1:1 + fr.nbytes].view(fr.shape)
+                    dev = buf[off:off + fr.nbytes].view(fr.shape)
                     dev.copy_(torch.from_numpy(fr))
                     ser = torch.zeros((fr.shape[0], 4), dtype=torch.int64, device="cuda")
                     op.run_device(dev, ser)
                     torch.cuda.synchronize()
                     out4, _, _ = oracle.series(fr, mode=mode, chroma=chroma, tau=tau)
-                    assert np.array_equal(ser.cpu().numpy().view(np.uint64), out4), (isi, tau, chroma)
+                    assert np.array_equal(ser.cpu().numpy().view(np.uint64), out4), (isi, tau, chroma, off)
             finally:
                 op.close()
 

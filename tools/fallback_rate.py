@@ -49,8 +49,8 @@ def main():
     cases = []
     for name, W, H, C, off, generic in CASES:
         cases.append((name, W, H, C, off, generic, None))
-        if C == 3 and not generic and ((W * H * C) % 4 or off % 4):
-            # the same unaligned batch with the byte-unaligned 12-B loads (A/B)
+        if C in (3, 4) and not generic and ((W * H * C) % 4 or off % 4):
+            # the same unaligned batch with the byte-unaligned 12-/16-B loads (A/B)
             cases.append((name + " [DIPS_SERIES_ALIGN=0]", W, H, C, off, generic, "0"))
     for name, W, H, C, off, generic, align_env in cases:
         if align_env is None:
