@@ -35,9 +35,10 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import subprocess
 import sys
 import time
+import traceback
+from datetime import timedelta
 
 import numpy as np
 
@@ -80,18 +81,36 @@ def parse():
     ap.add_argument("--no-per-frame-call", action="store_true", help="skip the per_frame_call leg")
     ap.add_argument("--per-frame-calls", type=int, default=200,
                     help="timed dips_frame_callback calls of the per_frame_call leg (4K RGBA8)")
+    ap.add_argument("--dump-series", default=None,
+                    help="rank 0 saves the gathered series of the timed step (uint64 [N*F, 4]) to this .npy, and "
+                         "each configs leg's beside it as <stem>_<leg>.npy (tests compare them with the oracle)")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds a collective may wait before the process group fails (init_process_group timeout)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="HBM traffic per launch measured by profiles/collect_pmc.sh")
     return ap.parse_args()
 
 
+def _series_isi(tau: float) -> int:
+    """The intensity-sum form run_series_device (dips_abi.hip) picks: 0 (f64
+    sum) below tau = 2^-5 or with DIPS_SERIES_ISI=0, 2 (SADI) with
+    DIPS_SERIES_ISI=2 and tau < 1, else 1 (the integer sum)."""
+    if not tau >= 0.03125:
+        return 0
+    env = os.environ.get("DIPS_SERIES_ISI", "1")[:1]
+    if env == "0":
+        return 0
+    if env == "2" and tau < 1.0:
+        return 2
+    return 1
+
+
 def _v2_kernel_name(per_frame: bool, tau: float, with_map: bool = False) -> str:
     """The series_v2_kernel instantiation the library runs for an aligned RGB8
-    batch (series_v2.hip: <C, CH, U, PF, MAP, ALIGN, ISI>; ISI for tau >= 2^-5
-    unless DIPS_SERIES_ISI=0)."""
-    isi = tau >= 0.03125 and os.environ.get("DIPS_SERIES_ISI", "1")[:1] != "0"
+    batch (series_v2.hip: <C, CH, U, PF, MAP, ALIGN, ISI>), spelled as
+    rocprofv3 prints it (ISI is an int template argument)."""
     b = lambda v: "true" if v else "false"  # noqa: E731
-    return f"series_v2_kernel<3,0,4,{b(per_frame)},{b(with_map)},false,{b(isi)}>"
+    return f"series_v2_kernel<3, 0, 4, {b(per_frame)}, {b(with_map)}, false, {_series_isi(tau)}>"
 
 
 def log(msg):
@@ -368,7 +387,8 @@ def _max_over_ranks(torch, dist, world, dev, values):
     return [float(v) for v in t]
 
 
-def _config_leg(torch, dist, buf, *, name, W, H, F, mode, tau, steps, world, rank, local, dev, check=True):
+def _config_leg(torch, dist, buf, *, name, W, H, F, mode, tau, steps, world, rank, local, dev, check=True,
+                dump=None):
     """One more BASELINE.json config on the same ranks and the same resident
     buffer (regenerated in place, so HBM holds one batch at a time): 'overall'
     mode, the reference broadcast once (RCCL), each step the series kernel
@@ -438,6 +458,8 @@ def _config_leg(torch, dist, buf, *, name, W, H, F, mode, tau, steps, world, ran
                                               per_frame=(mode == Mode.PerFrame), local_series=series, ref=ref,
                                               gathered=final, device=dev)
             chk.pop("global_frames", None)
+        if dump and rank == 0 and final is not None:
+            np.save(dump, final.cpu().numpy().view(np.uint64))
         algo = F * fb
         ach = algo / (kms / 1e3) / 1e9
         return {"workload": name, "frames_per_gpu": F, "width": W, "height": H,
@@ -490,7 +512,7 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
     # loop (a compare between calls measured 0.85-0.9x, tools/pfc_variants.py)
     outs = np.empty_like(host)
     outs.fill(0)
-    times = []
+    times, phases = [], []
     try:
         for t in range(n):
             t0 = time.perf_counter()
@@ -499,12 +521,28 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
             dt = time.perf_counter() - t0
             if t >= warm:
                 times.append(dt)
+                phases.append(cs.callback_phases())  # outside the timed call
     finally:
         cs.close()
     equal = bool(np.array_equal(outs, want))
     del outs
     fb = W * H * 4
     tot = float(np.sum(times))
+    ph = [p for p in phases if p]
+    med = lambda k: round(float(np.median([p[k] for p in ph])) / 1e3, 4) if ph else None  # noqa: E731
+    breakdown = {
+        "phases_ms_median": {
+            "sync": med("sync_us"), "staged": med("staged_us"), "launched": med("launched_us"),
+            "kernels_done": med("kernels_us"), "wall_in_library": med("wall_us")},
+        "cpu_ms_per_call_median": {"pack": med("pack_cpu_us"), "expand": med("expand_cpu_us"),
+                                   "wait_for_kernels": med("wait_cpu_us")},
+        "pool_threads": int(ph[0]["threads"]) if ph else None,
+        "stripes": int(ph[0]["stripes"]) if ph else None,
+        "host": _host_cpu(),
+        "note": "phase times from the call's start (dips_callback_phases): staged = last input piece packed "
+                "into pinned memory, launched = last stripe kernel launched, kernels_done = last stripe kernel "
+                "seen complete, wall_in_library = return; cpu sums over the copy pool's tasks",
+    } if ph else {"phases": "not recorded (call did not take the zero-copy path)"}
     rec = {"frames_per_s": round(n_timed / tot, 1), "calls": n_timed,
            "ms_per_call_median": round(float(np.median(times)) * 1e3, 4),
            "ms_per_call_p90": round(float(np.percentile(times, 90)) * 1e3, 4),
@@ -520,12 +558,36 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
                    "compat_main_host_packed_kernel on it (PCIe reads of the packed stripe, 1-B gray keys "
                    "written back over PCIe); the pool expands the keys into the RGBA8 output as each stripe's "
                    "event fires (dips_abi.hip frame_callback_striped, copy_pool.h pack_frame / expand_keys)",
-           "pcie_bytes_each_way_per_frame": {"host_to_device": W * H * 2, "device_to_host": W * H}}
+           "pcie_bytes_each_way_per_frame": {"host_to_device": W * H * 2, "device_to_host": W * H},
+           "breakdown": breakdown}
     return rec, (host[:warm].copy(), want[:warm].copy())
 
 
+# identity of this rank for failure reports: rank, local device, PCI bus id
+_WHO = {"rank": os.environ.get("RANK", "0"), "local": os.environ.get("LOCAL_RANK", "0"), "bus": None}
+
+
 def main():
+    """Run the bench; any exception on any rank ends THIS process with a
+    non-zero status after naming the rank and its device's PCI bus id (a rank
+    left waiting in a collective fails at the process group's timeout,
+    --dist-timeout, instead of hanging until the driver's limit)."""
     args = parse()
+    try:
+        _main(args)
+    except SystemExit:
+        raise
+    except BaseException:
+        log(f"FAILED on rank {_WHO['rank']} (local device {_WHO['local']}, PCI {_WHO['bus']}):\n"
+            f"{traceback.format_exc()}")
+        sys.stdout.flush()
+        sys.stderr.flush()
+        # no destructors: a process group or a HIP context in a failed state
+        # can block in its teardown
+        os._exit(1)
+
+
+def _main(args):
     import torch
     import torch.distributed as dist
 
@@ -544,6 +606,12 @@ def main():
         local = 0
     corrupt_halo = os.environ.get("DIPS_BENCH_CORRUPT_HALO") == "1"  # the self-check must catch it (tests)
     torch.cuda.set_device(local)  # one rank per GPU (RCCL rejects two ranks on one device)
+    _WHO["local"] = local
+    try:
+        pr = torch.cuda.get_device_properties(local)
+        _WHO["bus"] = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+    except Exception:  # the report only
+        pass
     if world > 1:
         # leave one wave slot per SIMD to RCCL's send/recv kernels (the halo
         # exchange runs beside the persistent series kernel); 4 and 5 waves
@@ -551,10 +619,16 @@ def main():
         os.environ.setdefault("DIPS_SERIES_WAVES_PER_SIMD", "4")
     dev = torch.device("cuda", local)
     if world > 1:
+        # a bounded wait: a rank stuck in a collective (a peer that died, a
+        # lost RCCL connection) fails after --dist-timeout seconds
+        tmo = timedelta(seconds=args.dist_timeout)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
+        log(f"rank {rank}/{world}: device {local} PCI {_WHO['bus']}, backend {backend}")
+    if os.environ.get("DIPS_BENCH_FAIL_RANK") == str(rank):  # the failure report path (tests)
+        raise RuntimeError("DIPS_BENCH_FAIL_RANK: injected failure")
 
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat, shard
 
@@ -650,6 +724,8 @@ def main():
     if rank == 0:
         final_np = final.cpu().numpy().view(np.uint64)
         assert final_np.shape == (world * F, 4)
+        if args.dump_series:
+            np.save(args.dump_series, final_np)
         if args.check and world * F * fb > (64 << 30):
             log("--check skipped: the N*F frames would not fit beside the resident batch (small sizes only)")
         elif args.check:
@@ -726,7 +802,9 @@ def main():
                     raise ValueError("fewer than 2 frames per GPU at this size")
                 legs[key] = _config_leg(torch, dist, buf, name=name, W=lw, H=lh, F=lf, mode=Mode.Overall,
                                         tau=args.tau, steps=args.leg_steps, world=world, rank=rank, local=local,
-                                        dev=dev, check=not args.no_check)
+                                        dev=dev, check=not args.no_check,
+                                        dump=(os.path.splitext(args.dump_series)[0] + f"_{key}.npy"
+                                              if args.dump_series else None))
                 log(f"{key}: {legs[key]['frames_per_s']} frames/s, frac {legs[key]['frac']}, "
                     f"check {legs[key]['check']}")
             except Exception as e:  # report, never hide
@@ -797,8 +875,8 @@ def main():
                     "series_shape": {
                         "achieved": round(F * fb / (walk_ms / 1e3) / 1e9, 1),
                         "frac": round(achieved / (F * fb / (walk_ms / 1e3) / 1e9), 4),
-                        "kernel": "read_walk_kernel: the series kernel's tile walk and vecs over the same frames, "
-                                  "no compute",
+                        "kernel": "read_walk_kernel: the series kernel's tile walk, schedule (part-major for "
+                                  "'per-frame' batches) and vecs over the same frames, no compute",
                     },
                 },
                 "algorithmic_bytes_per_launch": algo_bytes,

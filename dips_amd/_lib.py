@@ -143,6 +143,7 @@ def load() -> ctypes.CDLL:
             "dips_add_texture": ([_vp, u32, u32, _u8p, ctypes.c_size_t], st),
             "dips_dispatch": ([_vp, _u8p, ctypes.c_size_t], st),
             "dips_frame_callback": ([_vp, u32, u32, _u8p, ctypes.c_size_t, _u8p, ctypes.c_size_t], st),
+            "dips_callback_phases": ([_vp, P(ctypes.c_double), u32, P(u32)], st),
             "dips_start_texture": ([_vp, _u8p, ctypes.c_size_t], st),
             "dips_compat_resume": ([_vp, u32, u32, _u8p, _u8p, u64], st),
             "dips_frame_callback_batch": ([_vp, u32, u32, _u8p, u32, _u8p], st),

@@ -292,6 +292,20 @@ class ComputeState:
             hd.check(hd._lib.dips_kernel_time_reset(hd.ptr))
         return ms.value, cnt.value
 
+    CALLBACK_PHASES = ("sync_us", "staged_us", "launched_us", "kernels_us", "wall_us", "pack_cpu_us",
+                       "expand_cpu_us", "wait_cpu_us", "threads", "stripes")
+
+    def callback_phases(self) -> Optional[dict]:
+        """Where the last zero-copy frame_callback spent its time
+        (dips_callback_phases; None before the first such call)."""
+        v = (ctypes.c_double * len(self.CALLBACK_PHASES))()
+        n = ctypes.c_uint32()
+        st = self._hd._lib.dips_callback_phases(self._hd.ptr, v, len(v), ctypes.byref(n))
+        if st == _lib.DIPS_ERR_STATE:
+            return None
+        self._hd.check(st)
+        return dict(zip(self.CALLBACK_PHASES, list(v)[: n.value]))
+
     def start_texture(self) -> Optional[np.ndarray]:
         out = np.empty((self._h, self._w, 4), dtype=np.uint8)
         r = self._hd.check(self._hd._lib.dips_start_texture(self._hd.ptr, out.ctypes.data, out.nbytes))

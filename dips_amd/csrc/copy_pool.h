@@ -13,6 +13,8 @@
 #pragma once
 
 #include <immintrin.h>
+#include <pthread.h>
+#include <sched.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -22,7 +24,9 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <functional>
+#include <string>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -46,6 +50,38 @@ class CopyPool {
     CopyPool& operator=(const CopyPool&) = delete;
 
     unsigned threads() const { return (unsigned)th_.size() + 1u; }
+
+    // Pin the workers to the CPUs of NUMA node `node` that this process may
+    // use (the calling thread is left alone).  Returns the CPU count pinned
+    // to, 0 if the node's CPU list is unreadable or disjoint from the
+    // process's affinity (nothing changed then).
+    unsigned pin_workers_to_node(int node) {
+        std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+        std::string list;
+        if (node < 0 || !(f >> list)) return 0;
+        cpu_set_t allowed, set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return 0;
+        unsigned n = 0;
+        size_t pos = 0;
+        while (pos < list.size()) {
+            const size_t comma = list.find(',', pos);
+            const std::string r = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
+            const size_t dash = r.find('-');
+            const long a = std::strtol(r.c_str(), nullptr, 10);
+            const long b = dash == std::string::npos ? a : std::strtol(r.c_str() + dash + 1, nullptr, 10);
+            for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+                if (c >= 0 && CPU_ISSET(c, &allowed)) {
+                    CPU_SET(c, &set);
+                    ++n;
+                }
+            if (comma == std::string::npos) break;
+            pos = comma + 1;
+        }
+        if (n == 0) return 0;
+        for (auto& t : th_) pthread_setaffinity_np(t.native_handle(), sizeof set, &set);
+        return n;
+    }
 
     // fn(i) for every i in [0, n), spread over the workers and the caller.
     void run(size_t n, const std::function<void(size_t)>& fn) {

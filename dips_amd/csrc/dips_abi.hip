@@ -12,7 +12,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
+#include <fstream>
 #include <map>
 #include <mutex>
 #include <new>
@@ -82,6 +84,8 @@ struct dips_handle {
     dips_host::PieceEvents pieces;  // per-piece completion of the per-frame readback
     dips_host::PieceEvents up_pieces;  // per-stripe upload completion (striped frame_callback)
     HostPinned io_out;                 // readback staging of the striped frame_callback
+    dips_host::CallPhases cb_phases;   // where the last zero-copy frame_callback's time went
+    bool cb_phases_valid = false;
     // deferred add_texture (steady state, W = 1, host frame): add_texture
     // stages the frame into `io` and launches, stripe by stripe, the
     // compute_main of the dispatch that normally follows (zero-copy, output
@@ -322,6 +326,19 @@ dips_status ensure_gray_lut(dips_handle* h, hipStream_t s) {
     return DIPS_OK;
 }
 
+// The intensity-sum form of the RGB8 / RGBA8 series kernel for the handle's
+// tau (series_v2.hip ISI): 1 (the integer sum) for tau >= 2^-5, or 2 (SADI)
+// with DIPS_SERIES_ISI=2 and tau < 1; 0 (the exact f64 sum) below 2^-5 or
+// with DIPS_SERIES_ISI=0 (A/B runs).  Read per call.
+int series_isi_form(const dips_handle* h) {
+    const int C = (int)h->p.format;
+    if (C == 1 || !dips::series_v2_isi(h->p.tau)) return 0;
+    const char* isi_env = std::getenv("DIPS_SERIES_ISI");
+    if (isi_env && isi_env[0] == '0') return 0;
+    if (isi_env && isi_env[0] == '2' && dips::series_v2_sadi(h->p.tau)) return 2;
+    return 1;
+}
+
 // Run the series on device pointers, asynchronously on `s`.
 dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
                               uint32_t n_frames, const uint8_t* ref0, dips_series_entry* series, uint8_t* map,
@@ -344,13 +361,7 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     // RGB8 / RGBA8 with tau >= 2^-5: the integer intensity sum (series_v2.hip
     // ISI = 1, or 2 = SADI with DIPS_SERIES_ISI=2; DIPS_SERIES_ISI=0 keeps the
     // f64 sum; A/B runs)
-    const char* isi_env = std::getenv("DIPS_SERIES_ISI");
-    int isi = 0;
-    if (C != 1 && dips::series_v2_isi(h->p.tau)) {
-        isi = 1;
-        if (isi_env && isi_env[0] == '0') isi = 0;
-        if (isi_env && isi_env[0] == '2' && dips::series_v2_sadi(h->p.tau)) isi = 2;
-    }
+    const int isi = series_isi_form(h);
     if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC))
         g = glut ? gray_lut_geometry(h, width, height, n_frames)
                  : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr, align, isi);
@@ -462,6 +473,26 @@ dips_status dips_params_default(dips_params* p) {
     return DIPS_OK;
 }
 
+// DIPS_COPY_AFFINITY=1: pin the copy pool's workers to the CPUs of the NUMA
+// node the device hangs off (sysfs numa_node of its PCI function), once per
+// process, at the first handle (A/B runs: tools/pfc_threads_ab.py).
+void maybe_pin_copy_pool(int device) {
+    static std::once_flag once;
+    const char* e = std::getenv("DIPS_COPY_AFFINITY");
+    if (!e || e[0] != '1') return;
+    std::call_once(once, [device]() {
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) != hipSuccess) return;
+        for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+        std::ifstream f(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
+        int node = -1;
+        if (!(f >> node) || node < 0) return;
+        const unsigned n = dips_host::CopyPool::global().pin_workers_to_node(node);
+        if (std::getenv("DIPS_STRIPE_TRACE"))
+            std::fprintf(stderr, "copy pool pinned to NUMA node %d of %s: %u CPUs\n", node, bus, n);
+    });
+}
+
 dips_status dips_create(const dips_params* params, int device, dips_handle** out) {
     if (!out) return DIPS_ERR_INVALID;
     *out = nullptr;
@@ -501,6 +532,7 @@ dips_status dips_create(const dips_params* params, int device, dips_handle** out
         return DIPS_ERR_HIP;
     }
     h->stream = h->own_stream;
+    maybe_pin_copy_pool(device);
     *out = h;
     return DIPS_OK;
 }
@@ -1016,6 +1048,10 @@ dips_status batch_steady(dips_handle* h, const uint8_t* bf, uint8_t* bo, uint32_
 // stripe s comes back while stripes s+1.. still go up (both PCIe directions
 // at once).  Same outputs and ring state as add_texture + dispatch.
 int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
+    const auto t_call = std::chrono::steady_clock::now();
+    auto us_since_call = [&]() {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_call).count();
+    };
     dips_status st = flush_pending(h);  // a deferred frame into its slot first
     if (st != DIPS_OK) return st;
     const uint32_t W = h->width, H = h->height;
@@ -1064,6 +1100,9 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
         // stripe's kernel has finished when the call returns
         const char* one_env = std::getenv("DIPS_DIRECT_STREAMS");  // "1": every stripe on the compute stream (A/B)
         const hipStream_t cs[2] = {h->stream, (one_env && one_env[0] == '1') ? h->stream : h->copy_stream};
+        dips_host::CallPhases ph;
+        ph.sync_us = us_since_call();
+        h->cb_phases_valid = false;
         DIPS_HIP(h, dips_host::run_striped_frame_direct(frame, out, H, row, h->io.bytes(), h->io_out.bytes(), cs,
                                                         h->device, h->pieces,
                                                         [&](uint32_t y0, uint32_t y1, hipStream_t s) {
@@ -1071,7 +1110,11 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
                                                             a.y1 = y1;
                                                             return dips::launch_compat_main_host(a, s);
                                                         },
-                                                        (int)a.out_key, (int)a.in_key, (int)a.chroma - 1));
+                                                        (int)a.out_key, (int)a.in_key, (int)a.chroma - 1, &ph,
+                                                        t_call));
+        ph.wall_us = us_since_call();
+        h->cb_phases = ph;
+        h->cb_phases_valid = true;
         return 1;
     }
     DIPS_HIP(h, dips_host::run_striped_frame(frame, out, H, row, h->io.bytes(), h->io_out.bytes(), slot,
@@ -1403,7 +1446,10 @@ dips_status dips_read_ceiling_walk(dips_handle* h, const uint8_t* dev_frames, ui
     if (!dev_frames || !ms) return fail(h, DIPS_ERR_INVALID, "read_ceiling_walk: null argument");
     const int C = (int)h->p.format;
     if (C != 3 && C != 4) return fail(h, DIPS_ERR_INVALID, "read_ceiling_walk: RGB8 / RGBA8 only");
-    FastGeom g = fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false);
+    // the geometry and schedule an aligned batch of this shape runs with
+    // (part-major for 'per-frame' batches of >= 256 frames)
+    FastGeom g = fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false, false,
+                               series_isi_form(h));
     if (!g.ok) return fail(h, DIPS_ERR_INVALID, "read_ceiling_walk: shape not eligible for the series kernel");
     DIPS_HIP(h, h->probe_out.ensure(256));
     dips::SeriesArgs a{};
@@ -1414,6 +1460,7 @@ dips_status dips_read_ceiling_walk(dips_handle* h, const uint8_t* dev_frames, ui
     a.n_frames = n_frames;
     a.n_tiles = (uint32_t)g.n_tiles;
     a.n_waves = (uint32_t)g.n_waves;
+    a.part_frames = g.part_frames;
     hipEvent_t e0 = take_event(h), e1 = take_event(h);
     if (!e0 || !e1) return fail(h, DIPS_ERR_HIP, "hipEventCreate failed");
     DIPS_HIP(h, hipEventRecord(e0, h->stream));
@@ -1428,14 +1475,28 @@ dips_status dips_read_ceiling_walk(dips_handle* h, const uint8_t* dev_frames, ui
     return DIPS_OK;
 }
 
+dips_status dips_callback_phases(const dips_handle* h, double* us, uint32_t cap, uint32_t* n) {
+    if (!h || (!us && cap)) return DIPS_ERR_INVALID;
+    if (!h->cb_phases_valid) return DIPS_ERR_STATE;
+    const dips_host::CallPhases& p = h->cb_phases;
+    const double v[DIPS_CALLBACK_PHASES] = {p.sync_us,     p.staged_us,     p.launched_us, p.kernels_us, p.wall_us,
+                                            p.pack_cpu_us, p.expand_cpu_us, p.wait_cpu_us, p.threads,    p.stripes};
+    for (uint32_t i = 0; i < cap && i < DIPS_CALLBACK_PHASES; ++i) us[i] = v[i];
+    if (n) *n = DIPS_CALLBACK_PHASES;
+    return DIPS_OK;
+}
+
 dips_status dips_series_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames,
                                  uint64_t* waves, uint64_t* tiles, uint64_t* partial_bytes) {
     dips_status st = bind(h);
     if (st != DIPS_OK) return st;
     const int C = (int)h->p.format;
+    // the kernel an aligned batch of this shape runs (its occupancy sets the
+    // wave slots)
     FastGeom g = C == 1 && gray_lut_enabled()
                      ? gray_lut_geometry(h, width, height, n_frames)
-                     : fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false);
+                     : fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false, false,
+                                     series_isi_form(h));
     if (waves) *waves = g.ok ? g.n_waves : 0;
     if (tiles) *tiles = g.ok ? g.n_tiles : 0;
     if (partial_bytes) *partial_bytes = g.ok ? g.n_tiles * 16u : 0;

@@ -258,6 +258,22 @@ inline void stage_piece(uint8_t* pin_in, const uint8_t* frame, size_t o, size_t 
         host_copy(pin_in + o, frame + o, len, nt);
 }
 
+// Where one per-frame call's time went (run_striped_frame_direct; the
+// bench's per_frame_call record, dips_callback_phases).  Times in us from
+// `t0` (the caller's start of the call); CPU sums over the pool's tasks.
+struct CallPhases {
+    double sync_us = 0;      // the start-of-call stream synchronisations (caller)
+    double staged_us = 0;    // the last input piece staged (packed) into pinned memory
+    double launched_us = 0;  // the last stripe's kernel launched
+    double kernels_us = 0;   // the last stripe's kernel seen complete by a copy-out task
+    double wall_us = 0;      // the call returned (caller)
+    double pack_cpu_us = 0;  // sum over staging tasks
+    double expand_cpu_us = 0;  // sum over copy-out tasks, excluding their waits
+    double wait_cpu_us = 0;  // sum over copy-out tasks of the wait for their stripe's kernel
+    double threads = 0;      // pool threads (workers + the caller)
+    double stripes = 0;
+};
+
 inline void copy_out_piece(uint8_t* out, const uint8_t* pin_out, size_t o, size_t len, int key_bytes, bool nt) {
     if (!len) return;
     if (key_bytes)
@@ -270,7 +286,8 @@ template <typename Launch>
 hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t height, size_t row,
                                     uint8_t* pin_in, const uint8_t* pin_out, const hipStream_t (&compute)[2],
                                     int device, PieceEvents& ev, Launch&& launch, int key_bytes = 0,
-                                    int in_bytes = 0, int ch = 0) {
+                                    int in_bytes = 0, int ch = 0, CallPhases* ph = nullptr,
+                                    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now()) {
     const bool nt = nt_copy();  // on the calling thread, never in the workers
     const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
     const uint32_t first = std::min(height, direct_first_rows(rows));
@@ -293,6 +310,17 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
     const auto tbeg = clk::now();
     std::vector<double> ts(trace ? 2 * n_s + n_t : 0);
     auto since = [&]() { return std::chrono::duration<double, std::micro>(clk::now() - tbeg).count(); };
+    // phase record: latest-event times as integer ns since t0 (atomic max),
+    // CPU sums in ns
+    std::atomic<int64_t> p_staged{0}, p_launched{0}, p_kernels{0}, p_pack{0}, p_expand{0}, p_wait{0};
+    auto ns_since_t0 = [&]() {
+        return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t0).count();
+    };
+    auto amax = [](std::atomic<int64_t>& a, int64_t v) {
+        int64_t cur = a.load(std::memory_order_relaxed);
+        while (v > cur && !a.compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
+        }
+    };
     CopyPool::global().run(2 * n_t, [&](size_t i) {
         const size_t pi = i < n_t ? i : i - n_t;
         const uint32_t si = (uint32_t)(pi / k), j = (uint32_t)(pi % k);
@@ -303,7 +331,13 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
         const size_t p1 = j + 1 == k ? slen : std::min(slen, (slen * (j + 1) / k) & ~(size_t)63);
         const size_t o = so + p0, len = p1 - p0;
         if (i < n_t) {
+            const int64_t a0 = ph ? ns_since_t0() : 0;
             if (frame) stage_piece(pin_in, frame, o, len, in_bytes, ch, nt);  // frame == nullptr: already staged
+            if (ph) {
+                const int64_t a1 = ns_since_t0();
+                p_pack.fetch_add(a1 - a0, std::memory_order_relaxed);
+                amax(p_staged, a1);
+            }
             if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != k) return;
             // the stripe's last piece: its kernel and event back to back on the stream
             if (trace) ts[2 * si] = since();
@@ -317,9 +351,11 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
             }
             if (r != hipSuccess) err.store((int)r);
             if (trace) ts[2 * si + 1] = since();
+            if (ph) amax(p_launched, ns_since_t0());
             ready[si].store(r == hipSuccess ? 1 : -1, std::memory_order_release);
             return;
         }
+        const int64_t w0 = ph ? ns_since_t0() : 0;
         int st;
         while ((st = ready[si].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
         if (st < 0) return;
@@ -328,7 +364,13 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
             err.store((int)r);
             return;
         }
+        const int64_t w1 = ph ? ns_since_t0() : 0;
         copy_out_piece(out, pin_out, o, len, key_bytes, nt);
+        if (ph) {
+            p_wait.fetch_add(w1 - w0, std::memory_order_relaxed);
+            p_expand.fetch_add(ns_since_t0() - w1, std::memory_order_relaxed);
+            amax(p_kernels, w1);
+        }
         if (trace) ts[2 * n_s + pi] = since();
     });
     if (trace) {
@@ -339,6 +381,16 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
             std::fprintf(stderr, " [%.0f %.0f %.0f]", ts[2 * si], ts[2 * si + 1], done);
         }
         std::fprintf(stderr, " end %.0f\n", since());
+    }
+    if (ph) {
+        ph->staged_us = p_staged.load() * 1e-3;
+        ph->launched_us = p_launched.load() * 1e-3;
+        ph->kernels_us = p_kernels.load() * 1e-3;
+        ph->pack_cpu_us = p_pack.load() * 1e-3;
+        ph->expand_cpu_us = p_expand.load() * 1e-3;
+        ph->wait_cpu_us = p_wait.load() * 1e-3;
+        ph->threads = (double)CopyPool::global().threads();
+        ph->stripes = (double)n_s;
     }
     return (hipError_t)err.load();
 }

@@ -407,9 +407,11 @@ __global__ __launch_bounds__(256) void read_ceiling_kernel(const u32x4* __restri
 }
 
 // Read-only walk with the series kernels' access shape: the persistent
-// (tile, frame) item schedule of series_v2_kernel, a wave's 64 lanes x U
-// vecs of VB bytes per frame, two frames of loads in flight, no compute.
-// Its rate is the ceiling of that shape (profiles/r02_read_walk_probe.jsonl).
+// (tile, frame) item schedule of series_v2_kernel -- one contiguous range per
+// wave, or with a.part_frames = L > 0 the part-major schedule (items (part,
+// tile) with stride n_waves, as series_v2_body) -- a wave's 64 lanes x U vecs
+// of VB bytes per frame, two frames of loads in flight, no compute.  Its rate
+// is the ceiling of that shape (profiles/r02_read_walk_probe.jsonl).
 template <int VB, int U>
 __global__ __launch_bounds__(256) void read_walk_kernel(SeriesArgs a, uint32_t* __restrict__ out) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -417,13 +419,28 @@ __global__ __launch_bounds__(256) void read_walk_kernel(SeriesArgs a, uint32_t* 
     if (wave >= a.n_waves) return;
     uint64_t i = (uint64_t)wave * a.items / a.n_waves;
     const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
+    const bool parts = a.part_frames != 0u;
+    const uint32_t plen = parts ? a.part_frames : 1u;
+    const uint64_t pitems = parts ? (uint64_t)((a.n_frames + plen - 1) / plen) * a.n_tiles : 0u;
+    uint64_t it = wave;
     uint32_t acc = 0;
-    while (i < iend) {
-        const uint32_t tile = (uint32_t)(i / a.n_frames);
-        uint32_t t = (uint32_t)(i - (uint64_t)tile * a.n_frames);
-        const uint64_t rem = iend - i;
-        const uint32_t tend = (uint32_t)((uint64_t)a.n_frames < t + rem ? (uint64_t)a.n_frames : t + rem);
-        i += tend - t;
+    while (true) {
+        uint32_t tile, t, tend;
+        if (!parts) {
+            if (i >= iend) break;
+            tile = (uint32_t)(i / a.n_frames);
+            t = (uint32_t)(i - (uint64_t)tile * a.n_frames);
+            const uint64_t rem = iend - i;
+            tend = (uint32_t)((uint64_t)a.n_frames < t + rem ? (uint64_t)a.n_frames : t + rem);
+            i += tend - t;
+        } else {
+            if (it >= pitems) break;
+            const uint32_t part = (uint32_t)(it / a.n_tiles);
+            tile = (uint32_t)(it - (uint64_t)part * a.n_tiles);
+            t = part * plen;
+            tend = min(a.n_frames, t + plen);
+            it += a.n_waves;
+        }
         const uint32_t voff = (tile * (uint32_t)U * 64u + lane) * (uint32_t)VB;
         for (; t < tend; t += 2) {
             const uint32_t t1 = t + 1 < tend ? t + 1 : t;

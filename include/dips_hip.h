@@ -178,6 +178,25 @@ int dips_frame_callback(dips_handle *h, uint32_t width, uint32_t height,
 dips_status dips_frame_callback_batch(dips_handle *h, uint32_t width, uint32_t height, const uint8_t *frames,
                                       uint32_t n_frames, uint8_t *out);
 
+/* Where the last dips_frame_callback call that took the zero-copy striped
+ * path (steady state, window 1, host pointers) spent its time -- the
+ * per-phase record of the per-frame call pattern (dips/src/frame_extractor.rs:
+ * 206-276 -> lib.rs:233-246 -> gpu/mod.rs:170-397, whose per-frame cost is
+ * what this path replaces).  Writes up to `cap` values to `us`, *n = the
+ * number available (DIPS_CALLBACK_PHASES), in this order:
+ *   0 sync     us from the call's start to the end of its stream syncs
+ *   1 staged   .. to the last input piece packed into pinned memory
+ *   2 launched .. to the last stripe's kernel launch
+ *   3 kernels  .. to the last stripe's kernel seen complete
+ *   4 wall     .. to the call's return
+ *   5 pack_cpu, 6 expand_cpu, 7 wait_cpu: thread-time sums (us) of the copy
+ *     pool's staging tasks, output tasks and their waits for the kernels
+ *   8 threads  copy-pool threads (workers + the calling thread)
+ *   9 stripes  row stripes the frame was cut into
+ * DIPS_ERR_STATE if no such call has completed on `h`. */
+#define DIPS_CALLBACK_PHASES 10u
+dips_status dips_callback_phases(const dips_handle *h, double *us, uint32_t cap, uint32_t *n);
+
 /* Copy the start texture (RGBA8 gray, pre_compute_shader.wgsl:92-132) built
  * at the 4th frame.  Returns 1 if available, 0 if not yet built. */
 int dips_start_texture(dips_handle *h, uint8_t *out_rgba, size_t cap);
@@ -250,8 +269,9 @@ dips_status dips_read_ceiling(dips_handle *h, const uint8_t *dev_bytes, uint64_t
 
 /* The same with the RGB8 / RGBA8 series kernel's own access shape: its
  * persistent (tile, frame) schedule over n_frames DEVICE frames of
- * width x height (the handle's format and mode), 12- / 16-byte vecs, two
- * frames of loads in flight, no compute; *ms = the hipEvent duration. */
+ * width x height (the handle's format and mode; the part-major schedule where
+ * the series kernel runs it), 12- / 16-byte vecs, two frames of loads in
+ * flight, no compute; *ms = the hipEvent duration. */
 dips_status dips_read_ceiling_walk(dips_handle *h, const uint8_t *dev_frames, uint32_t width, uint32_t height,
                                    uint32_t n_frames, double *ms);
 

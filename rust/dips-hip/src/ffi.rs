@@ -36,6 +36,7 @@ pub const DIPS_MODE_PER_FRAME: u32 = 1;
 pub const DIPS_FLAG_DEVICE_PTRS: u32 = 0x1;
 pub const DIPS_FLAG_TIME_KERNEL: u32 = 0x2;
 pub const DIPS_FLAG_FORCE_GENERIC: u32 = 0x4;
+pub const DIPS_CALLBACK_PHASES: u32 = 10;
 
 /// `dips_params`: ComputeState::new's arguments (dips/src/gpu/mod.rs:59-65,
 /// DiPsProperties dips/src/lib.rs:63-86) + the batch series configuration.
@@ -130,6 +131,7 @@ extern "C" {
                                out: *mut u8, cap: usize) -> c_int;
     pub fn dips_frame_callback_batch(h: *mut DipsHandle, width: u32, height: u32, frames: *const u8,
                                      n_frames: u32, out: *mut u8) -> DipsStatus;
+    pub fn dips_callback_phases(h: *const DipsHandle, us: *mut f64, cap: u32, n: *mut u32) -> DipsStatus;
     pub fn dips_start_texture(h: *mut DipsHandle, out_rgba: *mut u8, cap: usize) -> c_int;
     pub fn dips_compat_resume(h: *mut DipsHandle, width: u32, height: u32, start_rgba: *const u8,
                               halo: *const u8, t0: u64) -> DipsStatus;

@@ -210,7 +210,7 @@ impl ComputeState {
         if fb == 0 || frames.len() % fb != 0 || out.len() < frames.len() {
             return Err(DipsError { status: ffi::DIPS_ERR_INVALID, message: "frames/out not n RGBA8 frames".into() });
         }
-        let n = (frames.len() / fb) as u32;
+        let n = frame_count(frames.len() / fb)?;
         // SAFETY: sizes checked above.
         let st = unsafe {
             ffi::dips_frame_callback_batch(self.h.as_ptr(), width, height, frames.as_ptr(), n, out.as_mut_ptr())
@@ -219,6 +219,17 @@ impl ComputeState {
         self.width = width;
         self.height = height;
         Ok(())
+    }
+
+    /// Where the last zero-copy `frame_callback` spent its time
+    /// (dips_callback_phases: sync, staged, launched, kernels, wall, pack /
+    /// expand / wait CPU sums in microseconds, pool threads, stripes).
+    pub fn callback_phases(&self) -> Option<[f64; ffi::DIPS_CALLBACK_PHASES as usize]> {
+        let mut v = [0f64; ffi::DIPS_CALLBACK_PHASES as usize];
+        let mut n = 0u32;
+        // SAFETY: v has cap entries.
+        let st = unsafe { ffi::dips_callback_phases(self.h.as_ptr(), v.as_mut_ptr(), v.len() as u32, &mut n) };
+        if st == ffi::DIPS_OK { Some(v) } else { None }
     }
 
     /// The start texture S (pre_compute_shader.wgsl:92-132), once built.
@@ -322,12 +333,26 @@ impl DiffSeries {
         Ok(Self { h: create(&p, device)?, format })
     }
 
+    fn frame_bytes(&self, width: u32, height: u32) -> usize {
+        width as usize * height as usize * self.format.channels()
+    }
+
     fn frames_of(&self, width: u32, height: u32, frames: &[u8]) -> Result<u32, DipsError> {
-        let fb = width as usize * height as usize * self.format.channels();
+        let fb = self.frame_bytes(width, height);
         if fb == 0 || frames.len() % fb != 0 {
             return Err(DipsError { status: ffi::DIPS_ERR_INVALID, message: "frames: n whole frames".into() });
         }
-        Ok((frames.len() / fb) as u32)
+        frame_count(frames.len() / fb)
+    }
+
+    /// The C ABI takes no length for the reference and reads one whole frame
+    /// from it: anything but exactly one frame is refused here.
+    fn reference_ptr(&self, width: u32, height: u32, reference: Option<&[u8]>) -> Result<*const u8, DipsError> {
+        match reference {
+            None => Ok(ptr::null()),
+            Some(r) if r.len() == self.frame_bytes(width, height) => Ok(r.as_ptr()),
+            Some(_) => Err(DipsError { status: ffi::DIPS_ERR_INVALID, message: "reference: one whole frame".into() }),
+        }
     }
 
     /// Series of host frames (staged through HBM); `reference` = None uses
@@ -336,6 +361,7 @@ impl DiffSeries {
     pub fn run(&mut self, width: u32, height: u32, frames: &[u8], reference: Option<&[u8]>,
                absdiff_map: Option<&mut [u8]>) -> Result<Vec<ffi::DipsSeriesEntry>, DipsError> {
         let n = self.frames_of(width, height, frames)?;
+        let ref_ptr = self.reference_ptr(width, height, reference)?;
         let mut series = vec![ffi::DipsSeriesEntry::default(); n as usize];
         let map_ptr = match absdiff_map {
             Some(m) if m.len() >= frames.len() => m.as_mut_ptr(),
@@ -344,8 +370,8 @@ impl DiffSeries {
         };
         // SAFETY: sizes checked; every buffer is caller-owned for the call.
         let st = unsafe {
-            ffi::dips_diff_series(self.h.as_ptr(), width, height, frames.as_ptr(), n,
-                                  reference.map_or(ptr::null(), |r| r.as_ptr()), series.as_mut_ptr(), map_ptr)
+            ffi::dips_diff_series(self.h.as_ptr(), width, height, frames.as_ptr(), n, ref_ptr, series.as_mut_ptr(),
+                                  map_ptr)
         };
         check(st, self.h.as_ptr())?;
         Ok(series)
@@ -356,12 +382,12 @@ impl DiffSeries {
     pub fn run_streamed(&mut self, width: u32, height: u32, frames: &[u8], reference: Option<&[u8]>,
                         chunk_frames: u32) -> Result<Vec<ffi::DipsSeriesEntry>, DipsError> {
         let n = self.frames_of(width, height, frames)?;
+        let ref_ptr = self.reference_ptr(width, height, reference)?;
         let mut series = vec![ffi::DipsSeriesEntry::default(); n as usize];
         // SAFETY: as in `run`.
         let st = unsafe {
-            ffi::dips_diff_series_streamed(self.h.as_ptr(), width, height, frames.as_ptr(), n,
-                                           reference.map_or(ptr::null(), |r| r.as_ptr()), series.as_mut_ptr(),
-                                           chunk_frames)
+            ffi::dips_diff_series_streamed(self.h.as_ptr(), width, height, frames.as_ptr(), n, ref_ptr,
+                                           series.as_mut_ptr(), chunk_frames)
         };
         check(st, self.h.as_ptr())?;
         Ok(series)
@@ -448,11 +474,14 @@ impl DiPsCompute {
         if self.bytes == 0 || frames.len() % self.bytes != 0 || out.len() < frames.len() {
             return Err(DipsError { status: ffi::DIPS_ERR_INVALID, message: "frames/out not n frames".into() });
         }
+        let n = frame_count(frames.len() / self.bytes)?;
+        let n_markers = u32::try_from(refresh_markers.len())
+            .map_err(|_| DipsError { status: ffi::DIPS_ERR_INVALID, message: "too many refresh markers".into() })?;
         // SAFETY: sizes checked above.
         let st = unsafe {
-            ffi::dips_alt_run(self.h.as_ptr(), frames.as_ptr(), (frames.len() / self.bytes) as u32,
+            ffi::dips_alt_run(self.h.as_ptr(), frames.as_ptr(), n,
                               if refresh_markers.is_empty() { ptr::null() } else { refresh_markers.as_ptr() },
-                              refresh_markers.len() as u32, out.as_mut_ptr())
+                              n_markers, out.as_mut_ptr())
         };
         check_alt(st, self.h.as_ptr())?;
         Ok(())
@@ -464,6 +493,12 @@ impl Drop for DiPsCompute {
         // SAFETY: the handle is live and dropped once.
         unsafe { ffi::dips_alt_destroy(self.h.as_ptr()) }
     }
+}
+
+/// A frame count as the ABI's u32 (a batch of 2^32 or more frames is refused,
+/// not truncated).
+fn frame_count(n: usize) -> Result<u32, DipsError> {
+    u32::try_from(n).map_err(|_| DipsError { status: ffi::DIPS_ERR_INVALID, message: "too many frames".into() })
 }
 
 /// The ABI version the library was built with (ffi::DIPS_ABI_VERSION expected).

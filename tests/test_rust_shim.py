@@ -76,6 +76,7 @@ def header_structs():
 
 def header_functions():
     src = _strip_c_comments(open(HEADER).read())
+    src = re.sub(r"^\s*#.*$", " ", src, flags=re.M)  # preprocessor lines (#define ...)
     src = re.sub(r"\s+", " ", src)
     out = {}
     for m in re.finditer(r"([A-Za-z_][A-Za-z_0-9 ]*?)\s*(\*?)\s*\b(dips_\w+)\(([^)]*)\);", src):

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""pfc_threads_ab.py -- the per_frame_call leg (4K RGBA8 dips_frame_callback
+from pageable host memory, DiPsProperties defaults) under copy-pool variants:
+the pool's thread count (DIPS_COPY_THREADS, read once per process) and its
+NUMA pinning (DIPS_COPY_AFFINITY=1: workers on the GPU's node).  Each variant
+runs in its own process, the variants alternated over --rounds rounds; every
+run prints one JSON line with frames/s and the per-phase medians of
+dips_callback_phases.  Outputs are checked against the device batch path.
+
+  python tools/pfc_threads_ab.py [--rounds 2] [--calls 200] [--variants 8:0,16:0,8:1,16:1]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def worker(calls: int, warm: int = 8):
+    import torch
+    from dips_amd import ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, PixelFormat
+    W, H = 3840, 2160
+    n = warm + calls
+    gen = DiffSeriesOperator(PixelFormat.RGBA8)
+    dev = torch.empty((n, H, W, 4), dtype=torch.uint8, device="cuda")
+    gen.synth_device(dev, W, H, 0xD1B5 ^ 0x4A, 0)
+    gen.close()
+    host = dev.cpu().numpy()
+    b = ComputeState(False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
+    od = torch.empty_like(dev)
+    b.frame_callback_batch_device(dev, od)
+    torch.cuda.synchronize()
+    want = od.cpu().numpy()
+    b.close()
+    del dev, od
+    torch.cuda.empty_cache()
+    outs = np.empty_like(host)
+    outs.fill(0)
+    cs = ComputeState(False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
+    lib, hd = cs._hd._lib, cs._hd
+    times, ph = [], []
+    for t in range(n):
+        t0 = time.perf_counter()
+        hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
+                                         outs[t].ctypes.data, outs[t].nbytes))
+        dt = time.perf_counter() - t0
+        if t >= warm:
+            times.append(dt)
+            ph.append(cs.callback_phases())
+    cs.close()
+    med = {k: round(float(np.median([p[k] for p in ph])) / 1e3, 4) for k in ph[0]
+           if k not in ("threads", "stripes")}
+    return {"frames_per_s": round(calls / sum(times), 1), "median_ms": round(float(np.median(times)) * 1e3, 4),
+            "p90_ms": round(float(np.percentile(times, 90)) * 1e3, 4), "phases_ms_median": med,
+            "threads": int(ph[0]["threads"]), "stripes": int(ph[0]["stripes"]),
+            "equal": bool(np.array_equal(outs, want))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worker", action="store_true")
+    ap.add_argument("--calls", type=int, default=200)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--variants", default="8:0,12:0,16:0,8:1,16:1",
+                    help="comma list of threads:affinity")
+    args = ap.parse_args()
+    if args.worker:
+        print(json.dumps(worker(args.calls)), flush=True)
+        return
+    for r in range(args.rounds):
+        for v in args.variants.split(","):
+            th, aff = v.split(":")
+            env = dict(os.environ, DIPS_COPY_THREADS=th, DIPS_COPY_AFFINITY=aff)
+            p = subprocess.run([sys.executable, os.path.abspath(__file__), "--worker", "--calls", str(args.calls)],
+                               env=env, capture_output=True, text=True, timeout=300)
+            line = [l for l in p.stdout.splitlines() if l.startswith("{")]
+            rec = json.loads(line[-1]) if line else {"failed": p.stderr[-800:]}
+            rec.update({"round": r, "DIPS_COPY_THREADS": int(th), "DIPS_COPY_AFFINITY": int(aff)})
+            print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
