@@ -205,7 +205,7 @@ __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t
 // VGPRs; 4 and 5 waves per SIMD run the ISI kernel at the same speed).
 template <int C, int U, bool PF, bool MAP, bool ALIGN = false, int ISI = 0>
 constexpr int v2_min_waves() {
-    return ALIGN ? (MAP ? 1 : (C == 4 ? 3 : 4))  // RGBA8: 5 dwords per vec spill at 128 VGPRs
+    return ALIGN ? (MAP ? 1 : 4)
                  : ((C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : (ISI == 2 ? 4 : 5))) : 1);
 }
 
@@ -218,8 +218,15 @@ constexpr int v2_min_waves() {
 // cache-line requests (62-63 % of 8 TB/s against 71.7 % aligned,
 // profiles/r02_fallback_rate_after.jsonl, r02_unaligned_probe.txt).
 // RGBA8 frames are off a 4-byte boundary only through an offset pointer
-// (their stride is a multiple of 4); their 16-B vec comes out of an aligned
-// dwordx4 plus the next dword (20 bytes, 4 funnel shifts).
+// (their stride is a multiple of 4); their 16-B vec comes out of the lane's
+// aligned dwordx4 and the FIRST dword of the next lane's (the vecs of a tile
+// are contiguous): one DPP wave_shl:1 move per vec brings it over, lane 63
+// takes it from lane 0 of the next vec (v_readlane / v_writelane) or, for
+// the tile's last vec, from one wave-uniform dword loaded beside the frame.
+// So the ring holds 4 dwords per vec (as aligned frames) and a frame costs
+// U + 1 loads per lane-slot instead of 2U (the previous form loaded the
+// fifth dword per lane: 65.3 % of 8 TB/s at +2 bytes against 75.1 %
+// aligned, profiles/r03/fallback_rate_align.jsonl).
 template <int N, int L>
 __device__ __forceinline__ void funnel(uint32_t (&v)[L], uint32_t sh) {
     static_assert(L > N, "a funnel needs the dword after the vec");
@@ -244,7 +251,8 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
     constexpr int CW = ISI == 2 ? 0 : 1;  // record word of the count
     using F = Fmt<C>;
     static_assert(!ALIGN || C == 3 || C == 4, "the aligned-load form is the RGB8 / RGBA8 one");
-    constexpr int LW = ALIGN ? F::NDW + 1 : F::NDW;  // dwords loaded per vec
+    constexpr bool A4 = ALIGN && C == 4;  // RGBA8: the fifth dword from the next lane
+    constexpr int LW = (ALIGN && C == 3) ? F::NDW + 1 : F::NDW;  // dwords loaded per vec
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
@@ -287,7 +295,9 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
         // ALIGN: a descriptor at the dword below p (range rounded up to whole
         // dwords: the dword holding the last byte never crosses a page), one
         // dwordx4 per vec, *sh = p's byte offset in that dword
-        auto load_at = [&](const uint8_t* p, uint32_t (&dst)[U][LW], uint32_t* sh) {
+        // A4: *tl = the dword right after the tile (wave-uniform offset)
+        const uint32_t tile_end = (tile + 1u) * U * 64u * (uint32_t)F::VB;
+        auto load_at = [&](const uint8_t* p, uint32_t (&dst)[U][LW], uint32_t* sh, uint32_t* tl) {
             if constexpr (ALIGN) {
                 const uint32_t d = (uint32_t)(uintptr_t)p & 3u;
                 *sh = d;
@@ -299,9 +309,8 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
                     dst[u][1] = x.y;
                     dst[u][2] = x.z;
                     dst[u][3] = x.w;
-                    if constexpr (C == 4)
-                        dst[u][4] = __builtin_amdgcn_raw_buffer_load_b32(r, voff + (uint32_t)(u * 64 * F::VB + 16), 0, AUX);
                 }
+                if constexpr (A4) *tl = __builtin_amdgcn_raw_buffer_load_b32(r, tile_end, 0, AUX);
             } else {
                 const __amdgpu_buffer_rsrc_t r = make_rsrc(p, vb);
 #pragma unroll
@@ -309,13 +318,14 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
             }
         };
         uint32_t sh[4] = {0u, 0u, 0u, 0u};  // ALIGN: byte offset of each ring slot's frame
-        auto load_frame = [&](uint32_t tf, uint32_t (&dst)[U][LW], uint32_t* shp) {
+        uint32_t tl[4] = {0u, 0u, 0u, 0u};  // A4: the dword after the tile, per ring slot
+        auto load_frame = [&](uint32_t tf, uint32_t (&dst)[U][LW], uint32_t* shp, uint32_t* tlp) {
 #ifdef DIPS_PROBE_SAMEFRAME
             // probe build only (tools/probe.hip): every load re-reads the
             // segment's first frame -- the kernel's compute-only time
             tf = t0;
 #endif
-            load_at(a.frames + (uint64_t)min(tf, tlast) * fb, dst, shp);
+            load_at(a.frames + (uint64_t)min(tf, tlast) * fb, dst, shp, tlp);
         };
 
         // ring: PF -- frame k of the segment in slot (k+1)&3, its reference
@@ -335,36 +345,51 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
         uint32_t keep[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) keep[u] = voff + (uint32_t)(u * 64 * F::VB) < vb ? 0xFFFFFFFFu : 0u;
-        auto settle = [&](int j) {
+        // the vec bytes out of the aligned words of one ring slot (or the
+        // reference), in increasing u: A4 takes vec u's fifth dword from
+        // vec u's next lane (lane 63: vec u + 1's lane 0, still unshifted, or
+        // the tile's trailing dword) before shifting vec u
+        const bool lane63 = lane == 63u;
+        auto realign = [&](uint32_t (&v)[U][LW], uint32_t shv, uint32_t tlv) {
             if constexpr (ALIGN) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    funnel<F::NDW>(buf[j][u], sh[j]);
-                    buf[j][u][0] &= keep[u];
+                    if constexpr (A4) {
+                        uint32_t nx = DIPS_DPP(v[u][0], 0x130);  // wave_shl:1 -- lane i gets lane i + 1
+                        const uint32_t l63 = u + 1 < U ? (uint32_t)__builtin_amdgcn_readlane((int)v[u + 1][0], 0)
+                                                       : __builtin_amdgcn_readfirstlane(tlv);
+                        nx = lane63 ? l63 : nx;
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) v[u][k] = __builtin_amdgcn_alignbyte(v[u][k + 1], v[u][k], shv);
+                        v[u][3] = __builtin_amdgcn_alignbyte(nx, v[u][3], shv);
+                    } else {
+                        funnel<F::NDW>(v[u], shv);
+                    }
+                    v[u][0] &= keep[u];
                 }
             }
+        };
+        auto settle = [&](int j) {
+            if constexpr (ALIGN) realign(buf[j], sh[j], tl[j]);
         };
         {
             const uint8_t* rp = PF ? (t0 == 0 ? a.ref0 : a.frames + (uint64_t)(t0 - 1) * fb) : a.ref0;
             uint32_t (&dref)[U][LW] = PF ? buf[0] : rb;
-            uint32_t rsh = 0;
-            load_at(rp, dref, &rsh);
+            uint32_t rsh = 0, rtl = 0;
+            load_at(rp, dref, &rsh, &rtl);
             if constexpr (PF) {
-                load_frame(t0, buf[1], &sh[1]);
-                load_frame(t0 + 1, buf[2], &sh[2]);
-                load_frame(t0 + 2, buf[3], &sh[3]);
+                load_frame(t0, buf[1], &sh[1], &tl[1]);
+                load_frame(t0 + 1, buf[2], &sh[2], &tl[2]);
+                load_frame(t0 + 2, buf[3], &sh[3], &tl[3]);
             } else {
-                load_frame(t0, buf[0], &sh[0]);
-                load_frame(t0 + 1, buf[1], &sh[1]);
-                load_frame(t0 + 2, buf[2], &sh[2]);
-                load_frame(t0 + 3, buf[3], &sh[3]);
+                load_frame(t0, buf[0], &sh[0], &tl[0]);
+                load_frame(t0 + 1, buf[1], &sh[1], &tl[1]);
+                load_frame(t0 + 2, buf[2], &sh[2], &tl[2]);
+                load_frame(t0 + 3, buf[3], &sh[3], &tl[3]);
             }
+            if constexpr (ALIGN) realign(dref, rsh, rtl);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                if constexpr (ALIGN) {
-                    funnel<F::NDW>(dref[u], rsh);
-                    dref[u][0] &= keep[u];
-                }
                 uint32_t dv[F::NDW];
 #pragma unroll
                 for (int k2 = 0; k2 < F::NDW; ++k2) dv[k2] = dref[u][k2];
@@ -386,13 +411,13 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
                         frame_v2<C, CH, U, PF, MAP, SAUX, LW, LW, ISI>(a, st, buf[j], buf[(j + 1) & 3], voff, tf,
                                                                   v + 4 * q, q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
-                        load_frame(tf + 3, buf[j], &sh[j]);
+                        load_frame(tf + 3, buf[j], &sh[j], &tl[j]);
                     } else {
                         settle(j);
                         frame_v2<C, CH, U, PF, MAP, SAUX, LW, LW, ISI>(a, st, rb, buf[j], voff, tf, v + 4 * q,
                                                                   q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
-                        load_frame(tf + 4, buf[j], &sh[j]);
+                        load_frame(tf + 4, buf[j], &sh[j], &tl[j]);
                     }
                 }
                 const uint32_t y = wave_sum8_lanes(v, lane);
