@@ -264,17 +264,22 @@ __attribute__((target("avx2"))) inline void expand_keys_avx2(uint8_t* dst, const
     if (nt) _mm_sfence();
 }
 
-inline void expand_keys(uint8_t* dst, const uint8_t* keys, size_t npx, int key_bytes, bool nt) {
-    static const bool avx2 = __builtin_cpu_supports("avx2");
-    if (avx2) {
-        expand_keys_avx2(dst, keys, npx, key_bytes, nt);
-        return;
-    }
+// The same without AVX2 (and the reference the CPU test checks the AVX2
+// form against, tests/test_copy_pool_cpu.py).
+inline void expand_keys_scalar(uint8_t* dst, const uint8_t* keys, size_t npx, int key_bytes) {
     for (size_t i = 0; i < npx; ++i) {
         const uint32_t r = keys[key_bytes * i], g = key_bytes == 1 ? r : keys[2 * i + 1];
         const uint32_t t = r | (g << 8) | ((r < g ? r : g) << 16) | 0xFF000000u;
         std::memcpy(dst + 4 * i, &t, 4);
     }
+}
+
+inline void expand_keys(uint8_t* dst, const uint8_t* keys, size_t npx, int key_bytes, bool nt) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2)
+        expand_keys_avx2(dst, keys, npx, key_bytes, nt);
+    else
+        expand_keys_scalar(dst, keys, npx, key_bytes);
 }
 
 // The per-frame zero-copy input in the form the kernel needs (compat_main_
@@ -326,12 +331,8 @@ __attribute__((target("avx2"))) inline void pack_frame_avx2(uint8_t* dst, const 
     if (nt) _mm_sfence();
 }
 
-inline void pack_frame(uint8_t* dst, const uint8_t* src, size_t npx, int in_bytes, int ch, bool nt) {
-    static const bool avx2 = __builtin_cpu_supports("avx2");
-    if (avx2) {
-        pack_frame_avx2(dst, src, npx, in_bytes, ch, nt);
-        return;
-    }
+// The same without AVX2 (and the CPU test's reference for the AVX2 form).
+inline void pack_frame_scalar(uint8_t* dst, const uint8_t* src, size_t npx, int in_bytes, int ch) {
     for (size_t i = 0; i < npx; ++i) {
         const uint8_t r = src[4 * i], g = src[4 * i + 1], b = src[4 * i + 2];
         if (in_bytes == 2) {
@@ -341,6 +342,14 @@ inline void pack_frame(uint8_t* dst, const uint8_t* src, size_t npx, int in_byte
             dst[i] = src[4 * i + ch];
         }
     }
+}
+
+inline void pack_frame(uint8_t* dst, const uint8_t* src, size_t npx, int in_bytes, int ch, bool nt) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2)
+        pack_frame_avx2(dst, src, npx, in_bytes, ch, nt);
+    else
+        pack_frame_scalar(dst, src, npx, in_bytes, ch);
 }
 
 // Host copy in ~4 MiB pieces over the pool.

@@ -81,8 +81,10 @@ struct HostPinned {
     }
     void release() {
         if (map) {
-            (void)hipHostUnregister(p);
-            munmap(map, map_len);
+            // unmap only what the runtime let go of: if the unregister fails
+            // the pages may still be mapped for the device, so the range is
+            // leaked rather than returned to the OS under a live mapping
+            if (hipHostUnregister(p) == hipSuccess) munmap(map, map_len);
             map = nullptr;
             map_len = 0;
         } else if (p) {
