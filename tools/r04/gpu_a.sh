@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r04a
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_series.py \
-  tests/test_gpu_fuzz.py -k "unaligned or intensity_sum_forms or fuzz or random" > $O/pytest_align.txt 2>&1; rc=$?
+  tests/test_gpu_fuzz.py tests/test_gpu_compact_io.py -k "unaligned or intensity_sum_forms or fuzz or random or zero_copy" > $O/pytest_align.txt 2>&1; rc=$?
 tail -5 $O/pytest_align.txt; [ $rc -ne 0 ] && { tail -80 $O/pytest_align.txt; exit $rc; }
 timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread \
   tests/test_gpu_timed_config.py tests/test_gpu_bench_rehearsal.py > $O/pytest_new.txt 2>&1; rc=$?
