@@ -33,6 +33,7 @@ constexpr uint32_t kGrayAluWaves = DIPS_GRAY_ALU_WAVES;
 constexpr uint32_t kGrayLutWaves = 16;  // its waves per workgroup (one 1024-thread group per CU)
 constexpr size_t kGrayLutBytes = 131072;  // its T_d / T_c tables
 constexpr size_t kGrayLutAllocBytes = kGrayLutBytes + 256;  // + layout 3's band word (series_gray.hip)
+// layout 4 (auto) keeps layout 3's table + band word and layout 2's after it
 // Prefetch depth: frames of loads each wave keeps in flight.
 #ifndef DIPS_DEPTH_RGB
 #define DIPS_DEPTH_RGB 2
@@ -59,6 +60,8 @@ struct SeriesArgs {
     const void* lut;         // GRAY8 table kernel: T_d / T_c bytes (series_gray.hip), 128 KiB
     uint32_t part_frames;    // frames per part of the part-major schedule (series_v2 SCHED = 1)
     uint32_t thr_int;        // series_v2 SADI (ISI = 2): T = tau * 2^28 as an integer (series_sadi_threshold)
+    const uint32_t* probe;   // GRAY8 table kernel, layout 4: the sampled band count (gray_band_probe_kernel)
+    uint32_t probe_min;      //   layout 3 when *probe >= probe_min, else layout 2
 };
 
 struct GenericArgs {
@@ -260,6 +263,12 @@ const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int
 int gray_alu_vecs(float tau);          // arithmetic vecs of this call's table kernel (0 for tau < 2^-5)
 uint32_t gray_lut_waves(int layout, int alu_vecs);  // waves per group of the table kernel
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s);
+// layout 4 (auto): vecs of the band probe (16 px each, strided over the frame)
+constexpr uint32_t kGrayProbeVecs = 16384;
+// the band occupancy sample of frame f against r into *out; returns the
+// pixels sampled (0: none)
+uint32_t launch_gray_band_probe(const uint8_t* f, const uint8_t* r, uint32_t vec_bytes, const uint8_t* lut3,
+                                 uint32_t* out, hipStream_t s, hipError_t* err);
 hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
                                   hipStream_t s, int alu_vecs = 0);
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);

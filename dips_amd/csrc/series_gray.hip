@@ -288,16 +288,10 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
     }
 }
 
-template <int U, bool PF, bool MAP, int LAYOUT, int NA = 0, int GW = kGrayWaves>
-__global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) {
-    __shared__ uint32_t lds32[32768];  // T_d at byte 0, T_c at byte kGrayLutTcOffset
-    {
-        const u32x4* src = reinterpret_cast<const u32x4*>(a.lut);
-        u32x4* dst = reinterpret_cast<u32x4*>(lds32);
-        for (uint32_t i = threadIdx.x; i < 8192u; i += 64u * GW) dst[i] = src[i];
-    }
-    __syncthreads();
-    const uint8_t* lds = reinterpret_cast<const uint8_t*>(lds32);
+// The item walk of the table kernel over its table in LDS (`lds`; `lut` =
+// the table's global copy, whose band word layout 3 reads).
+template <int U, bool PF, bool MAP, int LAYOUT, int NA, int GW>
+__device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* lds, const uint8_t* lut) {
     static_assert(U * 64 * 16 <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)GW + (threadIdx.x >> 6));
@@ -310,7 +304,7 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
     if constexpr (LAYOUT == 3) {
         // the band clamp from the word after the table: rows x < 2^m hold no
         // selected pair, m = floor(log2(the first row that does)), K = 256 * 2^m - 1
-        const uint32_t w = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(a.lut) + kGrayBandOffset);
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(lut + kGrayBandOffset);
         const uint32_t first = 256u - min(w, 255u);  // 1 .. 256 (row 0, a == b, is never selected)
         const uint32_t kc = (256u << (31u - __builtin_clz(first))) - 1u;
         kk = kc | (kc << 16);
@@ -423,6 +417,67 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
     }
 }
 
+// LAYOUT 4 (auto, the default): layout 3 when the batch's sampled band
+// occupancy reaches a.probe_min (*a.probe, gray_band_probe_kernel), else
+// layout 2 -- the table of the chosen layout is the one copied into LDS
+// (a.lut: layout 3's table + band word, then layout 2's at
+// kGrayLutAllocBytes).  Layout 3's broadcast pays on consecutive frames of
+// video (most pixels in the band); on content whose pixels all change it
+// is ~3 % slower than layout 2 (its extra VALU), so the choice follows the
+// content (tools/content_rate.py).
+template <int U, bool PF, bool MAP, int LAYOUT, int NA = 0, int GW = kGrayWaves>
+__global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) {
+    __shared__ uint32_t lds32[32768];  // T_d at byte 0, T_c at byte kGrayLutTcOffset
+    bool use3 = LAYOUT == 3;
+    if constexpr (LAYOUT == 4) use3 = __builtin_amdgcn_readfirstlane(*a.probe) >= a.probe_min;
+    const uint8_t* lut = static_cast<const uint8_t*>(a.lut) + ((LAYOUT == 4 && !use3) ? kGrayLutAllocBytes : 0u);
+    {
+        const u32x4* src = reinterpret_cast<const u32x4*>(lut);
+        u32x4* dst = reinterpret_cast<u32x4*>(lds32);
+        for (uint32_t i = threadIdx.x; i < 8192u; i += 64u * GW) dst[i] = src[i];
+    }
+    __syncthreads();
+    const uint8_t* lds = reinterpret_cast<const uint8_t*>(lds32);
+    if constexpr (LAYOUT == 4) {
+        if (use3)
+            gray_walk<U, PF, MAP, 3, NA, GW>(a, lds, lut);
+        else
+            gray_walk<U, PF, MAP, 2, NA, GW>(a, lds, lut);
+    } else {
+        gray_walk<U, PF, MAP, LAYOUT, NA, GW>(a, lds, lut);
+    }
+}
+
+// Band occupancy of a sample of the batch (LAYOUT 4's choice): over n_vec
+// 16-pixel vecs taken with stride `stride` from frame f and its reference r,
+// the number of pixels whose table row x = a ^ b lies below layout 3's band
+// clamp (x < 2^m, from the band word after layout 3's table) -- the pixels
+// whose lookup becomes a broadcast.  Added to *out (zeroed by the caller).
+__global__ __launch_bounds__(256) void gray_band_probe_kernel(const uint8_t* f, const uint8_t* r, uint32_t vb,
+                                                              uint32_t n_vec, uint32_t stride,
+                                                              const uint8_t* lut3, uint32_t* out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(lut3 + kGrayBandOffset);
+    const uint32_t first = 256u - min(w, 255u);
+    const uint32_t lim = 1u << (31u - __builtin_clz(first));  // 2^m
+    uint32_t c = 0;
+    if (i < n_vec) {
+        const __amdgpu_buffer_rsrc_t rf = make_rsrc(f, vb), rr = make_rsrc(r, vb);
+        const uint32_t off = i * stride * 16u;
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rf, off, 0, kAuxNT);
+        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kAuxNT);
+        const uint32_t d[4] = {x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) c += ((d[k] >> (8 * b)) & 0xFFu) < lim ? 1u : 0u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+    const uint32_t tot = __builtin_amdgcn_readfirstlane(c);
+    if ((threadIdx.x & 63u) == 0u && tot) atomicAdd(out, tot);
+}
+
 }  // namespace
 
 template <int U, int L, int NA = 0, int GW = kGrayWaves>
@@ -471,6 +526,7 @@ int gray_lut_unroll() {
 
 const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs, uint32_t waves) {
     if (layout == 1) return gray_ptr<kUnrollGrayLut, 1>(per_frame, map);
+    if (layout == 4) return (alu_vecs != 0 || waves != 16u) ? nullptr : gray_ptr<4, 4>(per_frame, map);
     if (layout == 3) {
         if (alu_vecs != 0 || waves != 16u) return nullptr;
         switch (gray_lut_unroll()) {
@@ -492,12 +548,30 @@ const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int
 }
 
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
+    if (layout == 4) {  // auto: layout 3 (+ band word), then layout 2 after it
+        const hipError_t e = launch_gray_lut(tab, tau, 3, s);
+        return e != hipSuccess ? e : launch_gray_lut(tab + kGrayLutAllocBytes, tau, 2, s);
+    }
     if (layout == 3) {
         const hipError_t e = hipMemsetAsync(tab + kGrayBandOffset, 0, 4, s);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(gray_lut_kernel, dim3(256), dim3(256), 0, s, tab, tau, (uint32_t)layout);
     return hipGetLastError();
+}
+
+uint32_t launch_gray_band_probe(const uint8_t* f, const uint8_t* r, uint32_t vec_bytes, const uint8_t* lut3,
+                                 uint32_t* out, hipStream_t s, hipError_t* err) {
+    const uint32_t nvec = vec_bytes / 16u;
+    const uint32_t n = nvec < kGrayProbeVecs ? nvec : kGrayProbeVecs;
+    *err = hipSuccess;
+    if (n == 0) return 0;
+    *err = hipMemsetAsync(out, 0, 4, s);
+    if (*err != hipSuccess) return 0;
+    hipLaunchKernelGGL(gray_band_probe_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, f, r, vec_bytes, n,
+                       nvec / n, lut3, out);
+    *err = hipGetLastError();
+    return n * 16u;
 }
 
 hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,

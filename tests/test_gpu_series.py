@@ -652,3 +652,34 @@ def test_part_major_schedule_matches_contiguous_and_oracle(fmt_name, w, h, n, mo
             assert np.array_equal(maps["1"].cpu().numpy(), omap)
     finally:
         op.close()
+
+
+@pytest.mark.parametrize("frac", ["0", "2", None])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gray_auto_layout_branches_match_oracle(frac, mode, monkeypatch):
+    """GRAY8 table layout 4 (the default): one kernel that takes layout 3
+    (band clamp) or layout 2 per launch from the band occupancy of a sampled
+    frame pair.  DIPS_GRAY_AUTO_FRAC=0 forces the layout-3 branch, 2 the
+    layout-2 branch, unset the content's own choice -- every branch against
+    the oracle on synthetic, random, identical and ragged clips, tau 0 / 8/255
+    / 0.5, with and without the map, one-frame batches included."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    if frac is None:
+        monkeypatch.delenv("DIPS_GRAY_AUTO_FRAC", raising=False)
+    else:
+        monkeypatch.setenv("DIPS_GRAY_AUTO_FRAC", frac)
+    monkeypatch.delenv("DIPS_GRAY_LUT", raising=False)
+    same = np.repeat(_frames(1, 256, 64, 1, 9, "random"), 5, axis=0)
+    clips = [_frames(1, 256, 64, 9, 41, "synth"), _frames(1, 256, 64, 9, 42, "random"), same,
+             _frames(1, 1000, 37, 6, 43, "random"), _frames(1, 512, 32, 1, 44, "synth")]
+    for tau in (0.0, 8 / 255, 0.5):
+        op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau, 0)
+        try:
+            for fr in clips:
+                out4, si, dmap = oracle.series(fr, mode=mode, tau=tau, want_map=True)
+                got, gmap = op(fr, want_map=True)
+                _check(got, out4, si, gmap, dmap)
+                got, _ = op(fr)
+                _check(got, out4, si)
+        finally:
+            op.close()
