@@ -247,6 +247,17 @@ def _host_cpu() -> dict:
     return {"model": model, "nproc": os.cpu_count(), "usable_cpus": usable, "cgroup_cpu_quota": quota}
 
 
+def _cgroup_cpu_stat() -> dict:
+    """The cgroup's CPU accounting (cgroup v2 cpu.stat: usage_usec,
+    nr_throttled, throttled_usec), {} where unreadable: a delta over a leg
+    gives the CPUs it kept busy and the time the CPU quota throttled it."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (line.split() for line in f if len(line.split()) == 2)}
+    except (OSError, ValueError):
+        return {}
+
+
 def _lib_sha256() -> str:
     """sha256 of the loaded HIP library: profiles/pmc_traffic.json is used
     for roofline.traffic only when it was collected with this very build."""
@@ -513,8 +524,11 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
     outs = np.empty_like(host)
     outs.fill(0)
     times, phases = [], []
+    cg0, tw0 = {}, 0.0
     try:
         for t in range(n):
+            if t == warm:
+                cg0, tw0 = _cgroup_cpu_stat(), time.perf_counter()
             t0 = time.perf_counter()
             hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
                                              outs[t].ctypes.data, outs[t].nbytes))
@@ -524,6 +538,7 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
                 phases.append(cs.callback_phases())  # outside the timed call
     finally:
         cs.close()
+    cg1, tw1 = _cgroup_cpu_stat(), time.perf_counter()
     equal = bool(np.array_equal(outs, want))
     del outs
     fb = W * H * 4
@@ -537,6 +552,12 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
         "cpu_ms_per_call_median": {"pack": med("pack_cpu_us"), "expand": med("expand_cpu_us"),
                                    "wait_for_kernels": med("wait_cpu_us")},
         "pool_threads": int(ph[0]["threads"]) if ph else None,
+        "cgroup_cpu": ({"cpus_busy_avg": round((cg1["usage_usec"] - cg0["usage_usec"]) / 1e6 / (tw1 - tw0), 2),
+                        "throttled_ms": round((cg1.get("throttled_usec", 0) - cg0.get("throttled_usec", 0)) / 1e3, 2),
+                        "nr_throttled": cg1.get("nr_throttled", 0) - cg0.get("nr_throttled", 0),
+                        "source": "/sys/fs/cgroup/cpu.stat over the timed calls (the whole process: copy pool + "
+                                  "the calling thread + any other thread)"}
+                       if cg0 and cg1 and "usage_usec" in cg0 else None),
         "stripes": int(ph[0]["stripes"]) if ph else None,
         "host": _host_cpu(),
         "note": "phase times from the call's start (dips_callback_phases): staged = last input piece packed "

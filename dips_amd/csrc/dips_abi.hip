@@ -105,6 +105,7 @@ struct dips_handle {
     DevBuf gray_lut;          // T_d / T_c tables of series_gray_lut_kernel (128 KiB) for gray_lut_tau
                               // (layout 4: layout 3's and layout 2's, kGrayLutAllocBytes apart)
     DevBuf gray_probe;        // layout 4: the sampled band count of the current launch
+    DevBuf pk_in, pk_out;     // DIPS_CALLBACK_DIRECT=2: packed input / keys of the per-frame call in HBM
     bool gray_lut_valid = false;
     float gray_lut_tau = 0.0f;
     int gray_lut_layout = 0;
@@ -603,6 +604,8 @@ void dips_destroy(dips_handle* h) {
     h->raw.release();
     h->filtered.release();
     h->cb_lut.release();
+    h->pk_in.release();
+    h->pk_out.release();
     h->gray_probe.release();
     h->gray_lut.release();
     h->start.release();
@@ -1121,6 +1124,36 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
     // host memory and writes its output there, the pool copies stripes in and
     // out
     const char* direct_env = std::getenv("DIPS_CALLBACK_DIRECT");
+    // DIPS_CALLBACK_DIRECT=2: the compact forms through the copy engines
+    // (run_striped_frame_dma_keys; A/B against the zero-copy form)
+    if (direct_env && direct_env[0] == '2') {
+        a.out_key = (uint32_t)compact_out_keys(h);
+        a.in_key = a.out_key ? (uint32_t)compact_in_bytes(h, (int)a.out_key) : 0u;
+        if (a.out_key != 0u && a.in_key != 0u) {
+            const size_t npx = (size_t)W * H;
+            DIPS_HIP(h, h->pk_in.ensure(npx * a.in_key));
+            DIPS_HIP(h, h->pk_out.ensure(npx * a.out_key));
+            a.raw = h->pk_in.as<uint8_t>();
+            a.out = h->pk_out.as<uint8_t>();
+            a.host_pairs = 0u;
+            dips_host::CallPhases ph;
+            ph.sync_us = us_since_call();
+            h->cb_phases_valid = false;
+            DIPS_HIP(h, dips_host::run_striped_frame_dma_keys(
+                            frame, out, H, row, h->io.bytes(), h->io_out.bytes(), h->pk_in.as<uint8_t>(),
+                            h->pk_out.as<uint8_t>(), h->copy_stream, h->stream, h->device, h->up_pieces, h->pieces,
+                            [&](uint32_t y0, uint32_t y1, hipStream_t s) {
+                                a.y0 = y0;
+                                a.y1 = y1;
+                                return dips::launch_compat_main_host(a, s);
+                            },
+                            (int)a.out_key, (int)a.in_key, (int)a.chroma - 1, &ph, t_call));
+            ph.wall_us = us_since_call();
+            h->cb_phases = ph;
+            h->cb_phases_valid = true;
+            return 1;
+        }
+    }
     if (!direct_env || direct_env[0] != '0') {
         void *din = nullptr, *dout = nullptr;
         DIPS_HIP(h, hipHostGetDevicePointer(&din, h->io.p, 0));

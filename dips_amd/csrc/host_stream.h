@@ -395,6 +395,121 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
     return (hipError_t)err.load();
 }
 
+// The per-frame call through the DMA engines with the compact forms: the
+// pool packs each piece of a stripe into `pin_in` (pack_frame: IN bytes per
+// pixel), the thread that stages a stripe's last piece enqueues its H2D copy
+// into `dev_in` on `up` and, on `compute` behind that copy, the stripe's
+// kernel (launch(y0, y1, compute): dev_in -> dev_out keys in HBM) and the D2H
+// copy of its keys into `pin_out`; the copy-out tasks expand each stripe's
+// keys into `out` once its event fires.  Against the zero-copy form the
+// PCIe transfers are done by the copy engines at their full rate (the
+// kernels' system-scope loads of pinned memory reached ~31 GB/s) and the
+// kernels touch only HBM.  Same pieces, phases and error handling as
+// run_striped_frame_direct; the caller makes sure both streams are idle and
+// the four buffers free.
+template <typename Launch>
+hipError_t run_striped_frame_dma_keys(const uint8_t* frame, uint8_t* out, uint32_t height, size_t row,
+                                      uint8_t* pin_in, const uint8_t* pin_out, uint8_t* dev_in, uint8_t* dev_out,
+                                      hipStream_t up, hipStream_t compute, int device, PieceEvents& up_ev,
+                                      PieceEvents& ev, Launch&& launch, int key_bytes, int in_bytes, int ch,
+                                      CallPhases* ph = nullptr,
+                                      std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now()) {
+    const bool nt = nt_copy();  // on the calling thread, never in the workers
+    const uint32_t rows = (uint32_t)std::max<size_t>(1, piece_bytes() / row);
+    const uint32_t first = std::min(height, direct_first_rows(rows));
+    const uint32_t n_s = 1u + (height - first + rows - 1) / rows;
+    auto stripe_y0 = [&](uint32_t si) { return si == 0 ? 0u : std::min(height, first + (si - 1) * rows); };
+    const uint32_t k = direct_split();
+    const size_t n_t = (size_t)n_s * k;
+    hipError_t e = ev.ensure(n_s);
+    if (e == hipSuccess) e = up_ev.ensure(n_s);
+    if (e != hipSuccess) return e;
+    std::unique_ptr<std::atomic<int>[]> ready(new std::atomic<int>[n_s]);
+    std::unique_ptr<std::atomic<uint32_t>[]> staged(new std::atomic<uint32_t>[n_s]);
+    for (uint32_t i = 0; i < n_s; ++i) {
+        ready[i].store(0, std::memory_order_relaxed);
+        staged[i].store(0, std::memory_order_relaxed);
+    }
+    std::mutex launch_mu;
+    std::atomic<int> err{(int)hipSuccess};
+    using clk = std::chrono::steady_clock;
+    std::atomic<int64_t> p_staged{0}, p_launched{0}, p_kernels{0}, p_pack{0}, p_expand{0}, p_wait{0};
+    auto ns_since_t0 = [&]() {
+        return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t0).count();
+    };
+    auto amax = [](std::atomic<int64_t>& a, int64_t v) {
+        int64_t cur = a.load(std::memory_order_relaxed);
+        while (v > cur && !a.compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
+        }
+    };
+    const size_t ib = (size_t)in_bytes, kb = (size_t)key_bytes;
+    CopyPool::global().run(2 * n_t, [&](size_t i) {
+        const size_t pi = i < n_t ? i : i - n_t;
+        const uint32_t si = (uint32_t)(pi / k), j = (uint32_t)(pi % k);
+        const uint32_t y0 = stripe_y0(si), y1 = si + 1 == n_s ? height : stripe_y0(si + 1);
+        const size_t so = (size_t)y0 * row, slen = (size_t)(y1 - y0) * row;
+        const size_t p0 = std::min(slen, (slen * j / k) & ~(size_t)63);
+        const size_t p1 = j + 1 == k ? slen : std::min(slen, (slen * (j + 1) / k) & ~(size_t)63);
+        const size_t o = so + p0, len = p1 - p0;
+        if (i < n_t) {
+            const int64_t a0 = ph ? ns_since_t0() : 0;
+            stage_piece(pin_in, frame, o, len, in_bytes, ch, nt);
+            if (ph) {
+                const int64_t a1 = ns_since_t0();
+                p_pack.fetch_add(a1 - a0, std::memory_order_relaxed);
+                amax(p_staged, a1);
+            }
+            if (staged[si].fetch_add(1, std::memory_order_acq_rel) + 1 != k) return;
+            hipError_t r;
+            {
+                std::lock_guard<std::mutex> lk(launch_mu);
+                const size_t io = so / 4u * ib, il = slen / 4u * ib;
+                const size_t oo = so / 4u * kb, ol = slen / 4u * kb;
+                r = hipSetDevice(device);
+                if (r == hipSuccess) r = hipMemcpyAsync(dev_in + io, pin_in + io, il, hipMemcpyHostToDevice, up);
+                if (r == hipSuccess) r = hipEventRecord(up_ev.ev[si], up);
+                if (r == hipSuccess) r = hipStreamWaitEvent(compute, up_ev.ev[si], 0);
+                if (r == hipSuccess) r = launch(y0, y1, compute);
+                if (r == hipSuccess)
+                    r = hipMemcpyAsync(const_cast<uint8_t*>(pin_out) + oo, dev_out + oo, ol, hipMemcpyDeviceToHost,
+                                       compute);
+                if (r == hipSuccess) r = hipEventRecord(ev.ev[si], compute);
+            }
+            if (r != hipSuccess) err.store((int)r);
+            if (ph) amax(p_launched, ns_since_t0());
+            ready[si].store(r == hipSuccess ? 1 : -1, std::memory_order_release);
+            return;
+        }
+        const int64_t w0 = ph ? ns_since_t0() : 0;
+        int st;
+        while ((st = ready[si].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        if (st < 0) return;
+        const hipError_t r = hipEventSynchronize(ev.ev[si]);
+        if (r != hipSuccess) {
+            err.store((int)r);
+            return;
+        }
+        const int64_t w1 = ph ? ns_since_t0() : 0;
+        copy_out_piece(out, pin_out, o, len, key_bytes, nt);
+        if (ph) {
+            p_wait.fetch_add(w1 - w0, std::memory_order_relaxed);
+            p_expand.fetch_add(ns_since_t0() - w1, std::memory_order_relaxed);
+            amax(p_kernels, w1);
+        }
+    });
+    if (ph) {
+        ph->staged_us = p_staged.load() * 1e-3;
+        ph->launched_us = p_launched.load() * 1e-3;
+        ph->kernels_us = p_kernels.load() * 1e-3;
+        ph->pack_cpu_us = p_pack.load() * 1e-3;
+        ph->expand_cpu_us = p_expand.load() * 1e-3;
+        ph->wait_cpu_us = p_wait.load() * 1e-3;
+        ph->threads = (double)CopyPool::global().threads();
+        ph->stripes = (double)n_s;
+    }
+    return (hipError_t)err.load();
+}
+
 // Stripe / piece geometry of the zero-copy frame pipeline (as in
 // run_striped_frame_direct), fixed at staging time so that a later collect
 // uses the same cut.

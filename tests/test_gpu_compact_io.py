@@ -33,9 +33,10 @@ def _frames(n, seed):
     return f
 
 
-def _run(monkeypatch, props, out_form, in_form, px, huge=False):
+def _run(monkeypatch, props, out_form, in_form, px, huge=False, direct="1"):
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
     colorize, sens, filt, chroma = props
+    monkeypatch.setenv("DIPS_CALLBACK_DIRECT", direct)
     monkeypatch.setenv("DIPS_COMPACT_OUT", out_form)
     monkeypatch.setenv("DIPS_COMPACT_IN", in_form)
     monkeypatch.setenv("DIPS_HOST_PX", px)
@@ -68,3 +69,11 @@ def test_zero_copy_io_forms_match_oracle(monkeypatch, props, out_form, in_form, 
 def test_zero_copy_on_huge_page_pinned_buffers(monkeypatch):
     _run(monkeypatch, (True, 5.0, 0, 0), "1", "1", "1", huge=True)
     _run(monkeypatch, (False, 5.0, 255, 2), "0", "0", "2", huge=True)
+
+
+@pytest.mark.parametrize("props", PROPS)
+def test_copy_engine_keys_path_matches_oracle(monkeypatch, props):
+    """DIPS_CALLBACK_DIRECT=2: the packed input and the keys travel by the
+    copy engines (host_stream.h run_striped_frame_dma_keys), the kernel runs
+    on HBM copies -- same outputs as the oracle."""
+    _run(monkeypatch, props, "1", "1", "1", direct="2")

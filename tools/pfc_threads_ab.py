@@ -47,7 +47,17 @@ def worker(calls: int, warm: int = 8):
     cs = ComputeState(False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_)
     lib, hd = cs._hd._lib, cs._hd
     times, ph = [], []
+
+    def cpu_stat():
+        try:
+            with open("/sys/fs/cgroup/cpu.stat") as f:
+                return {k: int(v) for k, v in (l.split() for l in f if len(l.split()) == 2)}
+        except (OSError, ValueError):
+            return {}
+    c0 = t00 = None
     for t in range(n):
+        if t == warm:
+            c0, t00 = cpu_stat(), time.perf_counter()
         t0 = time.perf_counter()
         hd.check(lib.dips_frame_callback(hd.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
                                          outs[t].ctypes.data, outs[t].nbytes))
@@ -55,13 +65,17 @@ def worker(calls: int, warm: int = 8):
         if t >= warm:
             times.append(dt)
             ph.append(cs.callback_phases())
+    c1, t11 = cpu_stat(), time.perf_counter()
     cs.close()
+    cg = ({"cpus_busy_avg": round((c1["usage_usec"] - c0["usage_usec"]) / 1e6 / (t11 - t00), 2),
+           "throttled_ms": round((c1.get("throttled_usec", 0) - c0.get("throttled_usec", 0)) / 1e3, 2)}
+          if c0 and c1 and "usage_usec" in c0 else None)
     med = {k: round(float(np.median([p[k] for p in ph])) / 1e3, 4) for k in ph[0]
            if k not in ("threads", "stripes")}
     return {"frames_per_s": round(calls / sum(times), 1), "median_ms": round(float(np.median(times)) * 1e3, 4),
             "p90_ms": round(float(np.percentile(times, 90)) * 1e3, 4), "phases_ms_median": med,
             "threads": int(ph[0]["threads"]), "stripes": int(ph[0]["stripes"]),
-            "equal": bool(np.array_equal(outs, want))}
+            "equal": bool(np.array_equal(outs, want)), "cgroup_cpu": cg}
 
 
 def main():
@@ -69,21 +83,23 @@ def main():
     ap.add_argument("--worker", action="store_true")
     ap.add_argument("--calls", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--variants", default="8:0,12:0,16:0,8:1,16:1",
-                    help="comma list of threads:affinity")
+    ap.add_argument("--variants", default="8:0:1,12:0:1,16:0:1,8:1:1,16:1:1",
+                    help="comma list of threads:affinity[:DIPS_CALLBACK_DIRECT]")
     args = ap.parse_args()
     if args.worker:
         print(json.dumps(worker(args.calls)), flush=True)
         return
     for r in range(args.rounds):
         for v in args.variants.split(","):
-            th, aff = v.split(":")
-            env = dict(os.environ, DIPS_COPY_THREADS=th, DIPS_COPY_AFFINITY=aff)
+            th, aff, *rest = v.split(":")
+            direct = rest[0] if rest else "1"
+            env = dict(os.environ, DIPS_COPY_THREADS=th, DIPS_COPY_AFFINITY=aff, DIPS_CALLBACK_DIRECT=direct)
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--worker", "--calls", str(args.calls)],
                                env=env, capture_output=True, text=True, timeout=300)
             line = [l for l in p.stdout.splitlines() if l.startswith("{")]
             rec = json.loads(line[-1]) if line else {"failed": p.stderr[-800:]}
-            rec.update({"round": r, "DIPS_COPY_THREADS": int(th), "DIPS_COPY_AFFINITY": int(aff)})
+            rec.update({"round": r, "DIPS_COPY_THREADS": int(th), "DIPS_COPY_AFFINITY": int(aff),
+                        "DIPS_CALLBACK_DIRECT": int(direct)})
             print(json.dumps(rec), flush=True)
 
 
