@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -96,13 +97,23 @@ inline hipError_t upload_via(void* dev, const uint8_t* host, size_t bytes, uint8
     return (hipError_t)err.load();
 }
 
+// The per-frame pipelines' waiting threads sleep instead of spinning
+// (DIPS_CB_BLOCKING=1: blocking-sync stripe events and a condition variable
+// for the stripe launches; A/B runs, tools/pfc_threads_ab.py).  Read when an
+// event set is created and per call.
+inline bool cb_blocking() {
+    const char* e = std::getenv("DIPS_CB_BLOCKING");
+    return e && e[0] == '1';
+}
+
 // Events marking the completion of each piece of a download.
 struct PieceEvents {
     std::vector<hipEvent_t> ev;
     hipError_t ensure(size_t n) {
+        const unsigned flags = hipEventDisableTiming | (cb_blocking() ? hipEventBlockingSync : 0u);
         while (ev.size() < n) {
             hipEvent_t e = nullptr;
-            const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+            const hipError_t r = hipEventCreateWithFlags(&e, flags);
             if (r != hipSuccess) return r;
             ev.push_back(e);
         }
@@ -303,7 +314,9 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
         ready[i].store(0, std::memory_order_relaxed);
         staged[i].store(0, std::memory_order_relaxed);
     }
-    std::mutex launch_mu;
+    std::mutex launch_mu, ready_mu;
+    std::condition_variable ready_cv;
+    const bool blocking = cb_blocking();
     std::atomic<int> err{(int)hipSuccess};
     static const bool trace = std::getenv("DIPS_STRIPE_TRACE") != nullptr;
     using clk = std::chrono::steady_clock;
@@ -353,11 +366,21 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
             if (trace) ts[2 * si + 1] = since();
             if (ph) amax(p_launched, ns_since_t0());
             ready[si].store(r == hipSuccess ? 1 : -1, std::memory_order_release);
+            if (blocking) {
+                std::lock_guard<std::mutex> lk(ready_mu);
+                ready_cv.notify_all();
+            }
             return;
         }
         const int64_t w0 = ph ? ns_since_t0() : 0;
         int st;
-        while ((st = ready[si].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        if (blocking) {
+            std::unique_lock<std::mutex> lk(ready_mu);
+            ready_cv.wait(lk, [&]() { return ready[si].load(std::memory_order_acquire) != 0; });
+            st = ready[si].load(std::memory_order_acquire);
+        } else {
+            while ((st = ready[si].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        }
         if (st < 0) return;
         const hipError_t r = hipEventSynchronize(ev.ev[si]);
         if (r != hipSuccess) {
@@ -430,7 +453,9 @@ hipError_t run_striped_frame_dma_keys(const uint8_t* frame, uint8_t* out, uint32
         ready[i].store(0, std::memory_order_relaxed);
         staged[i].store(0, std::memory_order_relaxed);
     }
-    std::mutex launch_mu;
+    std::mutex launch_mu, ready_mu;
+    std::condition_variable ready_cv;
+    const bool blocking = cb_blocking();
     std::atomic<int> err{(int)hipSuccess};
     using clk = std::chrono::steady_clock;
     std::atomic<int64_t> p_staged{0}, p_launched{0}, p_kernels{0}, p_pack{0}, p_expand{0}, p_wait{0};
@@ -478,11 +503,21 @@ hipError_t run_striped_frame_dma_keys(const uint8_t* frame, uint8_t* out, uint32
             if (r != hipSuccess) err.store((int)r);
             if (ph) amax(p_launched, ns_since_t0());
             ready[si].store(r == hipSuccess ? 1 : -1, std::memory_order_release);
+            if (blocking) {
+                std::lock_guard<std::mutex> lk(ready_mu);
+                ready_cv.notify_all();
+            }
             return;
         }
         const int64_t w0 = ph ? ns_since_t0() : 0;
         int st;
-        while ((st = ready[si].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        if (blocking) {
+            std::unique_lock<std::mutex> lk(ready_mu);
+            ready_cv.wait(lk, [&]() { return ready[si].load(std::memory_order_acquire) != 0; });
+            st = ready[si].load(std::memory_order_acquire);
+        } else {
+            while ((st = ready[si].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+        }
         if (st < 0) return;
         const hipError_t r = hipEventSynchronize(ev.ev[si]);
         if (r != hipSuccess) {

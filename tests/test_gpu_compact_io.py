@@ -77,3 +77,12 @@ def test_copy_engine_keys_path_matches_oracle(monkeypatch, props):
     copy engines (host_stream.h run_striped_frame_dma_keys), the kernel runs
     on HBM copies -- same outputs as the oracle."""
     _run(monkeypatch, props, "1", "1", "1", direct="2")
+
+
+@pytest.mark.parametrize("direct", ["1", "2"])
+def test_sleeping_waits_match_oracle(monkeypatch, direct):
+    """DIPS_CB_BLOCKING=1 (blocking-sync stripe events, condition-variable
+    waits) on both per-frame pipelines: same outputs."""
+    monkeypatch.setenv("DIPS_CB_BLOCKING", "1")
+    _run(monkeypatch, (True, 5.0, 0, 0), "1", "1", "1", direct=direct)
+    _run(monkeypatch, (False, 5.0, 255, 3), "1", "1", "1", direct=direct)

@@ -84,7 +84,7 @@ def main():
     ap.add_argument("--calls", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--variants", default="8:0:1,12:0:1,16:0:1,8:1:1,16:1:1",
-                    help="comma list of threads:affinity[:DIPS_CALLBACK_DIRECT]")
+                    help="comma list of threads:affinity[:DIPS_CALLBACK_DIRECT[:DIPS_CB_BLOCKING]]")
     args = ap.parse_args()
     if args.worker:
         print(json.dumps(worker(args.calls)), flush=True)
@@ -93,13 +93,15 @@ def main():
         for v in args.variants.split(","):
             th, aff, *rest = v.split(":")
             direct = rest[0] if rest else "1"
-            env = dict(os.environ, DIPS_COPY_THREADS=th, DIPS_COPY_AFFINITY=aff, DIPS_CALLBACK_DIRECT=direct)
+            blocking = rest[1] if len(rest) > 1 else "0"
+            env = dict(os.environ, DIPS_COPY_THREADS=th, DIPS_COPY_AFFINITY=aff, DIPS_CALLBACK_DIRECT=direct,
+                       DIPS_CB_BLOCKING=blocking)
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--worker", "--calls", str(args.calls)],
                                env=env, capture_output=True, text=True, timeout=300)
             line = [l for l in p.stdout.splitlines() if l.startswith("{")]
             rec = json.loads(line[-1]) if line else {"failed": p.stderr[-800:]}
             rec.update({"round": r, "DIPS_COPY_THREADS": int(th), "DIPS_COPY_AFFINITY": int(aff),
-                        "DIPS_CALLBACK_DIRECT": int(direct)})
+                        "DIPS_CALLBACK_DIRECT": int(direct), "DIPS_CB_BLOCKING": int(blocking)})
             print(json.dumps(rec), flush=True)
 
 
