@@ -274,3 +274,19 @@ def test_pack_frame_for_the_zero_copy_input(tmp_path):
     subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", f"-I{csrc}", str(src), "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout + r.stderr
+
+
+def test_bench_kernel_name_matches_library_choice(monkeypatch):
+    """bench.py names the series_v2 instantiation the library runs, spelled
+    as rocprofv3 prints it (ISI an int): run_series_device's choice of the
+    intensity-sum form."""
+    import bench
+    monkeypatch.delenv("DIPS_SERIES_ISI", raising=False)
+    assert bench._v2_kernel_name(True, 8 / 255) == "series_v2_kernel<3, 0, 4, true, false, false, 1>"
+    assert bench._v2_kernel_name(False, 8 / 255, with_map=True) == "series_v2_kernel<3, 0, 4, false, true, false, 1>"
+    assert bench._series_isi(0.0) == 0 and bench._series_isi(0.03) == 0 and bench._series_isi(1 / 32) == 1
+    assert bench._series_isi(1.0) == 1
+    monkeypatch.setenv("DIPS_SERIES_ISI", "2")
+    assert bench._series_isi(8 / 255) == 2 and bench._series_isi(1.0) == 1
+    monkeypatch.setenv("DIPS_SERIES_ISI", "0")
+    assert bench._series_isi(8 / 255) == 0
