@@ -291,17 +291,25 @@ int gray_lut_layout() {
     return 4;
 }
 
-// Layout 4: layout 3 when at least this fraction of the sampled pixels lies
-// in its band (DIPS_GRAY_AUTO_FRAC for A/B runs).  From the round-3 rates in
-// one process: layout 3 is +7 % on the synthetic clip (63 % of the pixels in
-// the band) and -3.5 % on i.i.d. random frames (3 %); linear in between,
-// even at ~23 %.
+// Layout 4's choice (series_gray.hip): layout 3 when the band holds at least
+// kGrayAutoMin of the sampled pixels and either kGrayAutoHi of them or the
+// sampled waves' frame bytes span kGrayAutoSpread levels on average.  From
+// the layouts measured in one process over five 4K contents
+// (tools/gray_layout_ab.py, profiles/r04/b/gray_layout_ab.jsonl; band
+// fraction / mean spread of 1024 consecutive pixels):
+//   synthetic (0.64 / 247): layout 3 +7 %;  random (0.03 / 248): layout 2;
+//   flat 128 +- 3 (0.51 / 6): layout 2 +5 %;  gradient, moving (0.80 / 70):
+//   layout 3 +1-2 %.
+// DIPS_GRAY_AUTO_FRAC overrides kGrayAutoMin (0: always layout 3, > 1:
+// always layout 2; tests).
+constexpr double kGrayAutoMin = 0.25, kGrayAutoHi = 0.65;
+constexpr uint32_t kGrayAutoSpread = 64;
 double gray_auto_frac() {
     if (const char* e = std::getenv("DIPS_GRAY_AUTO_FRAC")) {
         const double v = std::strtod(e, nullptr);
-        if (v >= 0.0 && v <= 2.0) return v;  // 0: always layout 3, > 1: always layout 2 (tests)
+        if (v >= 0.0 && v <= 2.0) return v;
     }
-    return 0.25;
+    return kGrayAutoMin;
 }
 bool gray_lut_enabled() { return gray_lut_layout() != 0; }
 
@@ -429,12 +437,17 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
             const uint8_t* pf_frame = frames + (n_frames > 1 ? fb : 0);
             const uint8_t* pf_ref = (pf && n_frames > 1) ? frames : ref0;
             hipError_t pe = hipSuccess;
+            uint32_t pw = 0;
             const uint32_t sampled = dips::launch_gray_band_probe(pf_frame, pf_ref, (uint32_t)g.vec_bytes,
                                                                   h->gray_lut.as<uint8_t>(),
-                                                                  h->gray_probe.as<uint32_t>(), s, &pe);
+                                                                  h->gray_probe.as<uint32_t>(), s, &pe, &pw);
             DIPS_HIP(h, pe);
+            const double fmin = gray_auto_frac();
             a.probe = h->gray_probe.as<uint32_t>();
-            a.probe_min = (uint32_t)std::ceil(gray_auto_frac() * (double)sampled);
+            a.probe_min = sampled ? (uint32_t)std::ceil(fmin * (double)sampled) : (fmin > 1.0 ? 1u : 0u);
+            // the forced settings (0, > 1) decide by probe_min alone
+            a.probe_hi = (fmin == 0.0 || fmin > 1.0) ? a.probe_min : (uint32_t)std::ceil(kGrayAutoHi * (double)sampled);
+            a.probe_spread = (fmin == 0.0 || fmin > 1.0) ? 0u : kGrayAutoSpread * pw;
         }
         a.frames = frames;
         a.ref0 = ref0;

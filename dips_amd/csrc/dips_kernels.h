@@ -60,8 +60,10 @@ struct SeriesArgs {
     const void* lut;         // GRAY8 table kernel: T_d / T_c bytes (series_gray.hip), 128 KiB
     uint32_t part_frames;    // frames per part of the part-major schedule (series_v2 SCHED = 1)
     uint32_t thr_int;        // series_v2 SADI (ISI = 2): T = tau * 2^28 as an integer (series_sadi_threshold)
-    const uint32_t* probe;   // GRAY8 table kernel, layout 4: the sampled band count (gray_band_probe_kernel)
-    uint32_t probe_min;      //   layout 3 when *probe >= probe_min, else layout 2
+    const uint32_t* probe;   // GRAY8 table kernel, layout 4: {band pixels, sum of wave spreads} of a sample
+    uint32_t probe_min;      //   layout 3 when band >= probe_min and (band >= probe_hi or spread >= probe_spread)
+    uint32_t probe_hi;
+    uint32_t probe_spread;
 };
 
 struct GenericArgs {
@@ -263,12 +265,13 @@ const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int
 int gray_alu_vecs(float tau);          // arithmetic vecs of this call's table kernel (0 for tau < 2^-5)
 uint32_t gray_lut_waves(int layout, int alu_vecs);  // waves per group of the table kernel
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s);
-// layout 4 (auto): vecs of the band probe (16 px each, strided over the frame)
-constexpr uint32_t kGrayProbeVecs = 16384;
-// the band occupancy sample of frame f against r into *out; returns the
-// pixels sampled (0: none)
+// layout 4 (auto): waves of the content probe (64 consecutive 16-pixel vecs
+// each, spread over the frame)
+constexpr uint32_t kGrayProbeWaves = 256;
+// the content sample of frame f against r into out[0..1]; returns the pixels
+// sampled (0: none), *waves the blocks
 uint32_t launch_gray_band_probe(const uint8_t* f, const uint8_t* r, uint32_t vec_bytes, const uint8_t* lut3,
-                                 uint32_t* out, hipStream_t s, hipError_t* err);
+                                 uint32_t* out, hipStream_t s, hipError_t* err, uint32_t* waves);
 hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
                                   hipStream_t s, int alu_vecs = 0);
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);

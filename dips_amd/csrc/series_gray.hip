@@ -417,19 +417,25 @@ __device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* ld
     }
 }
 
-// LAYOUT 4 (auto, the default): layout 3 when the batch's sampled band
-// occupancy reaches a.probe_min (*a.probe, gray_band_probe_kernel), else
-// layout 2 -- the table of the chosen layout is the one copied into LDS
-// (a.lut: layout 3's table + band word, then layout 2's at
-// kGrayLutAllocBytes).  Layout 3's broadcast pays on consecutive frames of
-// video (most pixels in the band); on content whose pixels all change it
-// is ~3 % slower than layout 2 (its extra VALU), so the choice follows the
-// content (tools/content_rate.py).
+// LAYOUT 4 (auto, the default): layout 3 or 2 per launch from a sample of
+// the batch (gray_band_probe_kernel) -- the table of the chosen layout is the
+// one copied into LDS (a.lut: layout 3's table + band word, then layout 2's
+// at kGrayLutAllocBytes).  Layout 3 turns the lookups of band pixels into
+// broadcasts but costs ~3 VALU more per 4 pixels; layout 2's gathers are
+// nearly conflict-free when a wave's frame bytes span few levels (few table
+// rows, spread over the banks by its swizzle).  So: layout 3 when the band
+// holds >= probe_min of the sampled pixels and either most of them
+// (probe_hi) or the waves' bytes spread widely (probe_spread), else layout 2
+// (tools/gray_layout_ab.py over five contents, profiles/r04/).
 template <int U, bool PF, bool MAP, int LAYOUT, int NA = 0, int GW = kGrayWaves>
 __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) {
     __shared__ uint32_t lds32[32768];  // T_d at byte 0, T_c at byte kGrayLutTcOffset
     bool use3 = LAYOUT == 3;
-    if constexpr (LAYOUT == 4) use3 = __builtin_amdgcn_readfirstlane(*a.probe) >= a.probe_min;
+    if constexpr (LAYOUT == 4) {
+        const uint32_t band = __builtin_amdgcn_readfirstlane(a.probe[0]);
+        const uint32_t spread = __builtin_amdgcn_readfirstlane(a.probe[1]);
+        use3 = band >= a.probe_min && (band >= a.probe_hi || spread >= a.probe_spread);
+    }
     const uint8_t* lut = static_cast<const uint8_t*>(a.lut) + ((LAYOUT == 4 && !use3) ? kGrayLutAllocBytes : 0u);
     {
         const u32x4* src = reinterpret_cast<const u32x4*>(lut);
@@ -448,34 +454,49 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
     }
 }
 
-// Band occupancy of a sample of the batch (LAYOUT 4's choice): over n_vec
-// 16-pixel vecs taken with stride `stride` from frame f and its reference r,
-// the number of pixels whose table row x = a ^ b lies below layout 3's band
-// clamp (x < 2^m, from the band word after layout 3's table) -- the pixels
-// whose lookup becomes a broadcast.  Added to *out (zeroed by the caller).
+// Content of a sample of the batch (LAYOUT 4's choice): n_waves blocks of
+// 64 consecutive 16-pixel vecs (one wave each, as the series kernel's lanes
+// read them), spread `stride` vecs apart, of frame f and its reference r.
+// out[0] += the pixels whose table row x = a ^ b lies below layout 3's band
+// clamp (x < 2^m, from the band word after layout 3's table) -- the lookups
+// that become broadcasts; out[1] += per block, max - min of the frame bytes
+// -- how many table rows layout 2's gathers of that wave touch.
 __global__ __launch_bounds__(256) void gray_band_probe_kernel(const uint8_t* f, const uint8_t* r, uint32_t vb,
                                                               uint32_t n_vec, uint32_t stride,
                                                               const uint8_t* lut3, uint32_t* out) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
     const uint32_t w = *reinterpret_cast<const uint32_t*>(lut3 + kGrayBandOffset);
     const uint32_t first = 256u - min(w, 255u);
     const uint32_t lim = 1u << (31u - __builtin_clz(first));  // 2^m
-    uint32_t c = 0;
-    if (i < n_vec) {
+    const uint32_t v = wave * stride + lane;
+    uint32_t c = 0, mx = 0, mn = 255;
+    if (v < n_vec) {
         const __amdgpu_buffer_rsrc_t rf = make_rsrc(f, vb), rr = make_rsrc(r, vb);
-        const uint32_t off = i * stride * 16u;
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rf, off, 0, kAuxNT);
-        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, kAuxNT);
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rf, v * 16u, 0, kAuxNT);
+        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rr, v * 16u, 0, kAuxNT);
+        const uint32_t fa[4] = {x.x, x.y, x.z, x.w};
         const uint32_t d[4] = {x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k)
 #pragma unroll
-            for (int b = 0; b < 4; ++b) c += ((d[k] >> (8 * b)) & 0xFFu) < lim ? 1u : 0u;
+            for (int b = 0; b < 4; ++b) {
+                c += ((d[k] >> (8 * b)) & 0xFFu) < lim ? 1u : 0u;
+                const uint32_t a = (fa[k] >> (8 * b)) & 0xFFu;
+                mx = max(mx, a);
+                mn = min(mn, a);
+            }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
-    const uint32_t tot = __builtin_amdgcn_readfirstlane(c);
-    if ((threadIdx.x & 63u) == 0u && tot) atomicAdd(out, tot);
+    for (int o = 32; o > 0; o >>= 1) {
+        c += (uint32_t)__shfl_xor((int)c, o);
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+    }
+    if (lane == 0u) {
+        if (c) atomicAdd(out, c);
+        if (mx > mn) atomicAdd(out + 1, mx - mn);
+    }
 }
 
 }  // namespace
@@ -561,17 +582,16 @@ hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
 }
 
 uint32_t launch_gray_band_probe(const uint8_t* f, const uint8_t* r, uint32_t vec_bytes, const uint8_t* lut3,
-                                 uint32_t* out, hipStream_t s, hipError_t* err) {
+                                 uint32_t* out, hipStream_t s, hipError_t* err, uint32_t* waves) {
     const uint32_t nvec = vec_bytes / 16u;
-    const uint32_t n = nvec < kGrayProbeVecs ? nvec : kGrayProbeVecs;
-    *err = hipSuccess;
-    if (n == 0) return 0;
-    *err = hipMemsetAsync(out, 0, 4, s);
-    if (*err != hipSuccess) return 0;
-    hipLaunchKernelGGL(gray_band_probe_kernel, dim3((n + 255u) / 256u), dim3(256), 0, s, f, r, vec_bytes, n,
-                       nvec / n, lut3, out);
+    const uint32_t nw = std::min<uint32_t>(kGrayProbeWaves, nvec / 64u);  // whole 64-vec blocks only
+    *waves = nw;
+    *err = hipMemsetAsync(out, 0, 8, s);  // zero even without a sample: the kernel reads it
+    if (*err != hipSuccess || nw == 0) return 0;
+    hipLaunchKernelGGL(gray_band_probe_kernel, dim3((nw + 3u) / 4u), dim3(256), 0, s, f, r, vec_bytes, nw * 64u,
+                       nvec / nw, lut3, out);
     *err = hipGetLastError();
-    return n * 16u;
+    return nw * 64u * 16u;
 }
 
 hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
