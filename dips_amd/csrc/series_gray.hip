@@ -454,9 +454,10 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
     }
 }
 
-// Content of a sample of the batch (LAYOUT 4's choice): n_waves blocks of
-// 64 consecutive 16-pixel vecs (one wave each, as the series kernel's lanes
-// read them), spread `stride` vecs apart, of frame f and its reference r.
+// Content of a sample of the batch (LAYOUT 4's choice): one block of 64
+// consecutive 16-pixel vecs per wave (as the series kernel's lanes read
+// them), the blocks `stride` vecs apart, of frame f (n_vec vecs) and its
+// reference r.
 // out[0] += the pixels whose table row x = a ^ b lies below layout 3's band
 // clamp (x < 2^m, from the band word after layout 3's table) -- the lookups
 // that become broadcasts; out[1] += per block, max - min of the frame bytes
@@ -588,7 +589,7 @@ uint32_t launch_gray_band_probe(const uint8_t* f, const uint8_t* r, uint32_t vec
     *waves = nw;
     *err = hipMemsetAsync(out, 0, 8, s);  // zero even without a sample: the kernel reads it
     if (*err != hipSuccess || nw == 0) return 0;
-    hipLaunchKernelGGL(gray_band_probe_kernel, dim3((nw + 3u) / 4u), dim3(256), 0, s, f, r, vec_bytes, nw * 64u,
+    hipLaunchKernelGGL(gray_band_probe_kernel, dim3((nw + 3u) / 4u), dim3(256), 0, s, f, r, vec_bytes, nvec,
                        nvec / nw, lut3, out);
     *err = hipGetLastError();
     return nw * 64u * 16u;
