@@ -287,6 +287,7 @@ int gray_lut_layout() {
         if (e[0] == '1') return 1;
         if (e[0] == '2') return 2;
         if (e[0] == '3') return 3;
+        if (e[0] == '5') return 5;  // layout 3 without the bank swizzle (A/B)
     }
     return 4;
 }

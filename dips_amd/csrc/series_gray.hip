@@ -129,9 +129,9 @@ __device__ __forceinline__ void gray_alu_dword(uint32_t f, uint32_t r, float thr
 __global__ __launch_bounds__(256) void gray_lut_kernel(uint8_t* __restrict__ tab, float tau, uint32_t layout) {
     const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
     uint32_t a = idx >> 8, b = idx & 0xFFu;
-    if (layout == 3u) {
+    if (layout == 3u || layout == 5u) {
         const uint32_t x = idx >> 8;
-        a = (idx & 0xFFu) ^ gray_band_swizzle(x);
+        a = (idx & 0xFFu) ^ (layout == 3u ? gray_band_swizzle(x) : 0u);
         b = a ^ x;
     }
     const float di = fabsf(unorm_load(a) - unorm_load(b));
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void gray_lut_kernel(uint8_t* __restrict__ tab
     const uint32_t d = a > b ? a - b : b - a;
     const uint32_t corr = (uint32_t)(v - (uint64_t)kGrayV * d);  // in [0, 128] (exhaustive test)
     const uint16_t e = sel ? (uint16_t)(d | corr << 8) : (uint16_t)0;
-    if (layout == 3u) {
+    if (layout == 3u || layout == 5u) {
         reinterpret_cast<uint16_t*>(tab)[idx] = e;
         if (__syncthreads_or(sel) && threadIdx.x == 0u)
             atomicMax(reinterpret_cast<uint32_t*>(tab + kGrayBandOffset), 256u - blockIdx.x);
@@ -210,9 +210,10 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
             // r_i ^ sw(f_i)); layout 3 x_i * 256 + (f_i ^ sw3(x_i)),
             // x_i = f_i ^ r_i, the indices below the band clamp raised to it
             uint32_t i02, i13;
-            if constexpr (LAYOUT == 3) {
+            if constexpr (LAYOUT == 3 || LAYOUT == 5) {
                 const uint32_t x = f ^ r;
-                const uint32_t col = f ^ ((x << 1) & (gray_band_swizzle(0xFFu) * 0x01010101u));
+                // layout 5: the column is a itself (no bank swizzle; A/B)
+                const uint32_t col = LAYOUT == 5 ? f : f ^ ((x << 1) & (gray_band_swizzle(0xFFu) * 0x01010101u));
                 i02 = as_u32(__builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x06020400u)),
                                                        as_u16x2(kk)));
                 i13 = as_u32(__builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x07030501u)),
@@ -301,7 +302,7 @@ __device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* ld
     const uint32_t rec_off4 = (lane & 15u) == 0u ? (lane >> 4) * 4u : 0x80000000u;
     const float thr28 = a.thr * 268435456.0f;  // 2^28 tau (exact)
     uint32_t kk = 0u;
-    if constexpr (LAYOUT == 3) {
+    if constexpr (LAYOUT == 3 || LAYOUT == 5) {
         // the band clamp from the word after the table: rows x < 2^m hold no
         // selected pair, m = floor(log2(the first row that does)), K = 256 * 2^m - 1
         const uint32_t w = *reinterpret_cast<const uint32_t*>(lut + kGrayBandOffset);
@@ -549,6 +550,7 @@ int gray_lut_unroll() {
 const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs, uint32_t waves) {
     if (layout == 1) return gray_ptr<kUnrollGrayLut, 1>(per_frame, map);
     if (layout == 4) return (alu_vecs != 0 || waves != 16u) ? nullptr : gray_ptr<4, 4>(per_frame, map);
+    if (layout == 5) return (alu_vecs != 0 || waves != 16u) ? nullptr : gray_ptr<4, 5>(per_frame, map);
     if (layout == 3) {
         if (alu_vecs != 0 || waves != 16u) return nullptr;
         switch (gray_lut_unroll()) {
@@ -574,7 +576,7 @@ hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
         const hipError_t e = launch_gray_lut(tab, tau, 3, s);
         return e != hipSuccess ? e : launch_gray_lut(tab + kGrayLutAllocBytes, tau, 2, s);
     }
-    if (layout == 3) {
+    if (layout == 3 || layout == 5) {
         const hipError_t e = hipMemsetAsync(tab + kGrayBandOffset, 0, 4, s);
         if (e != hipSuccess) return e;
     }

@@ -386,7 +386,7 @@ def test_gray_kernels_agree(mode, tau, monkeypatch):
     for (w, h), kind in [((256, 64), "random"), ((640, 48), "synth"), ((37, 23), "random")]:
         frames = _frames(1, w, h, 9, 40 + w, kind)
         out4, si, dmap = oracle.series(frames, mode=mode, tau=tau, want_map=True)
-        for layout in ("3", "2", "1", "0"):
+        for layout in ("4", "5", "3", "2", "1", "0"):
             monkeypatch.setenv("DIPS_GRAY_LUT", layout)
             op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
             try:
@@ -398,7 +398,7 @@ def test_gray_kernels_agree(mode, tau, monkeypatch):
             _check(got_nomap, out4, si)
 
 
-@pytest.mark.parametrize("layout", ["3", "2"])
+@pytest.mark.parametrize("layout", ["3", "2", "5"])
 @pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.1, 0.5, 1.0])
 def test_gray_table_every_byte_pair(tau, layout, monkeypatch):
     """Every (frame byte a, reference byte b) through the swizzled GRAY8

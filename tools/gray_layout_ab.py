@@ -42,7 +42,7 @@ def main():
             ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
             want = None
             for r in range(rounds):
-                for lay in ("2", "3", "4"):
+                for lay in os.environ.get("LAYOUTS", "2,3,4").split(","):
                     os.environ["DIPS_GRAY_LUT"] = lay
                     op.run_device(fr, ser)  # warm (table build)
                     torch.cuda.synchronize()
