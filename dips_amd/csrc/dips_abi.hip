@@ -276,9 +276,10 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
 
 // GRAY8 runs on the table kernel (series_gray.hip) unless DIPS_GRAY_LUT=0
 // (the f32 kernel series_fast_kernel; kept for A/B runs and as a cross-check).
-// Table layout: 4 auto (default): layout 3 or 2 per launch from the band
-// occupancy of a sample of the batch; 3 the u16 table keyed by (a ^ b, a)
-// with the band clamp, 2 the u16 table keyed by (a, b), 1 two byte tables,
+// Table layout: 4 auto (default): layout 5 or 2 per launch from a sample of
+// the batch's content; 5 the u16 table keyed by (a ^ b, a) with the band
+// clamp, 3 the same with a bank swizzle, 2 the u16 table keyed by (a, b)
+// (swizzled), 1 two byte tables,
 // 0 the f32 series_fast_kernel (DIPS_GRAY_LUT, read per call: A/B runs and
 // tests)
 int gray_lut_layout() {
@@ -287,24 +288,25 @@ int gray_lut_layout() {
         if (e[0] == '1') return 1;
         if (e[0] == '2') return 2;
         if (e[0] == '3') return 3;
-        if (e[0] == '5') return 5;  // layout 3 without the bank swizzle (A/B)
+        if (e[0] == '5') return 5;
     }
     return 4;
 }
 
-// Layout 4's choice (series_gray.hip): layout 3 when the band holds at least
+// Layout 4's choice (series_gray.hip): layout 5 when the band holds at least
 // kGrayAutoMin of the sampled pixels and either kGrayAutoHi of them or the
-// sampled waves' frame bytes span kGrayAutoSpread levels on average.  From
-// the layouts measured in one process over five 4K contents
-// (tools/gray_layout_ab.py, profiles/r04/b/gray_layout_ab.jsonl; band
-// fraction / mean spread of 1024 consecutive pixels):
-//   synthetic (0.64 / 247): layout 3 +7 %;  random (0.03 / 248): layout 2;
-//   flat 128 +- 3 (0.51 / 6): layout 2 +5 %;  gradient, moving (0.80 / 70):
-//   layout 3 +1-2 %.
-// DIPS_GRAY_AUTO_FRAC overrides kGrayAutoMin (0: always layout 3, > 1:
+// sampled waves' frame bytes span kGrayAutoSpread levels on average, else
+// layout 2.  From the layouts measured in one process over five 4K contents
+// (tools/gray_layout_ab.py, profiles/r04/d/gray_layout_ab.jsonl; band
+// fraction / mean spread of a wave's 1024 pixels; % of 8 TB/s):
+//   synthetic (0.64 / 247): layout 5 71.8-72.3, 3 64-70, 2 63-66;
+//   random (0.03 / 248): 2 61-63, 5 62-63, 3 60;
+//   flat 128 +- 3 (0.51 / 6): 2 70-71, 3 69, 5 58 (bank conflicts);
+//   gradient (0.80 / 70): all 69-70;  moving (0.80 / 70): 5 72.2-72.4, 2, 3 68-71.
+// DIPS_GRAY_AUTO_FRAC overrides kGrayAutoMin (0: always layout 5, > 1:
 // always layout 2; tests).
-constexpr double kGrayAutoMin = 0.25, kGrayAutoHi = 0.65;
-constexpr uint32_t kGrayAutoSpread = 64;
+constexpr double kGrayAutoMin = 0.25, kGrayAutoHi = 0.9;
+constexpr uint32_t kGrayAutoSpread = 48;
 double gray_auto_frac() {
     if (const char* e = std::getenv("DIPS_GRAY_AUTO_FRAC")) {
         const double v = std::strtod(e, nullptr);

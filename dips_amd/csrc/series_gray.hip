@@ -418,26 +418,29 @@ __device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* ld
     }
 }
 
-// LAYOUT 4 (auto, the default): layout 3 or 2 per launch from a sample of
+// LAYOUT 4 (auto, the default): layout 5 or 2 per launch from a sample of
 // the batch (gray_band_probe_kernel) -- the table of the chosen layout is the
-// one copied into LDS (a.lut: layout 3's table + band word, then layout 2's
-// at kGrayLutAllocBytes).  Layout 3 turns the lookups of band pixels into
-// broadcasts but costs ~3 VALU more per 4 pixels; layout 2's gathers are
-// nearly conflict-free when a wave's frame bytes span few levels (few table
-// rows, spread over the banks by its swizzle).  So: layout 3 when the band
-// holds >= probe_min of the sampled pixels and either most of them
-// (probe_hi) or the waves' bytes spread widely (probe_spread), else layout 2
-// (tools/gray_layout_ab.py over five contents, profiles/r04/).
+// one copied into LDS (a.lut: layout 5's table + band word, then layout 2's
+// at kGrayLutAllocBytes).  Layout 5 (keyed by (a ^ b, a), band clamp, no
+// bank swizzle) turns the lookups of band pixels into broadcasts, and its
+// other lookups spread over the banks as the frame bytes a do: well when a
+// wave's 64 lanes see many levels, badly when they see a handful (flat
+// content: 16-way conflicts).  Layout 2 (keyed by (a, b), swizzled) has no
+// broadcasts but few conflicts on such narrow content.  So: layout 5 when
+// the band holds >= probe_min of the sampled pixels and either nearly all
+// of them (probe_hi) or the waves' bytes spread over >= probe_spread / waves
+// levels, else layout 2 (tools/gray_layout_ab.py over five contents,
+// profiles/r04/d/).
 template <int U, bool PF, bool MAP, int LAYOUT, int NA = 0, int GW = kGrayWaves>
 __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) {
     __shared__ uint32_t lds32[32768];  // T_d at byte 0, T_c at byte kGrayLutTcOffset
-    bool use3 = LAYOUT == 3;
+    bool use5 = true;
     if constexpr (LAYOUT == 4) {
         const uint32_t band = __builtin_amdgcn_readfirstlane(a.probe[0]);
         const uint32_t spread = __builtin_amdgcn_readfirstlane(a.probe[1]);
-        use3 = band >= a.probe_min && (band >= a.probe_hi || spread >= a.probe_spread);
+        use5 = band >= a.probe_min && (band >= a.probe_hi || spread >= a.probe_spread);
     }
-    const uint8_t* lut = static_cast<const uint8_t*>(a.lut) + ((LAYOUT == 4 && !use3) ? kGrayLutAllocBytes : 0u);
+    const uint8_t* lut = static_cast<const uint8_t*>(a.lut) + ((LAYOUT == 4 && !use5) ? kGrayLutAllocBytes : 0u);
     {
         const u32x4* src = reinterpret_cast<const u32x4*>(lut);
         u32x4* dst = reinterpret_cast<u32x4*>(lds32);
@@ -446,8 +449,8 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
     __syncthreads();
     const uint8_t* lds = reinterpret_cast<const uint8_t*>(lds32);
     if constexpr (LAYOUT == 4) {
-        if (use3)
-            gray_walk<U, PF, MAP, 3, NA, GW>(a, lds, lut);
+        if (use5)
+            gray_walk<U, PF, MAP, 5, NA, GW>(a, lds, lut);
         else
             gray_walk<U, PF, MAP, 2, NA, GW>(a, lds, lut);
     } else {
@@ -459,10 +462,11 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
 // consecutive 16-pixel vecs per wave (as the series kernel's lanes read
 // them), the blocks `stride` vecs apart, of frame f (n_vec vecs) and its
 // reference r.
-// out[0] += the pixels whose table row x = a ^ b lies below layout 3's band
-// clamp (x < 2^m, from the band word after layout 3's table) -- the lookups
-// that become broadcasts; out[1] += per block, max - min of the frame bytes
-// -- how many table rows layout 2's gathers of that wave touch.
+// out[0] += the pixels whose table row x = a ^ b lies below layout 5's band
+// clamp (x < 2^m, from the band word after its table) -- the lookups that
+// become broadcasts; out[1] += per block, max - min of the frame bytes --
+// over how many levels (columns of layout 5, banks) the wave's other
+// lookups spread.
 __global__ __launch_bounds__(256) void gray_band_probe_kernel(const uint8_t* f, const uint8_t* r, uint32_t vb,
                                                               uint32_t n_vec, uint32_t stride,
                                                               const uint8_t* lut3, uint32_t* out) {
@@ -572,8 +576,8 @@ const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int
 }
 
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
-    if (layout == 4) {  // auto: layout 3 (+ band word), then layout 2 after it
-        const hipError_t e = launch_gray_lut(tab, tau, 3, s);
+    if (layout == 4) {  // auto: layout 5 (+ band word), then layout 2 after it
+        const hipError_t e = launch_gray_lut(tab, tau, 5, s);
         return e != hipSuccess ? e : launch_gray_lut(tab + kGrayLutAllocBytes, tau, 2, s);
     }
     if (layout == 3 || layout == 5) {

@@ -584,7 +584,7 @@ def test_4k_forms_agree_and_match_oracle(mode, monkeypatch):
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     w, h, n, tau = 3840, 2160, 48, 8 / 255
-    for fmt, env, forms in ((PixelFormat.Gray8, "DIPS_GRAY_LUT", ("3", "2")),
+    for fmt, env, forms in ((PixelFormat.Gray8, "DIPS_GRAY_LUT", ("4", "5", "3", "2")),
                             (PixelFormat.RGB8, "DIPS_SERIES_ISI", ("1", "2", "0"))):
         c = int(fmt)
         shape = (n, h, w) if c == 1 else (n, h, w, c)
@@ -657,9 +657,9 @@ def test_part_major_schedule_matches_contiguous_and_oracle(fmt_name, w, h, n, mo
 @pytest.mark.parametrize("frac", ["0", "2", None])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_gray_auto_layout_branches_match_oracle(frac, mode, monkeypatch):
-    """GRAY8 table layout 4 (the default): one kernel that takes layout 3
-    (band clamp) or layout 2 per launch from the band occupancy of a sampled
-    frame pair.  DIPS_GRAY_AUTO_FRAC=0 forces the layout-3 branch, 2 the
+    """GRAY8 table layout 4 (the default): one kernel that takes layout 5
+    (band clamp) or layout 2 per launch from a content sample of the batch's
+    first frame pair.  DIPS_GRAY_AUTO_FRAC=0 forces the layout-5 branch, 2 the
     layout-2 branch, unset the content's own choice -- every branch against
     the oracle on synthetic, random, identical and ragged clips, tau 0 / 8/255
     / 0.5, with and without the map, one-frame batches included."""
