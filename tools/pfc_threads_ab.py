@@ -24,7 +24,25 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _bind_node(node: str) -> None:
+    """PFC_BIND_NODE=n: run this process (every thread it starts, and so the
+    first touch of its buffers) on NUMA node n's CPUs."""
+    cpus = set()
+    try:
+        with open(f"/sys/devices/system/node/node{int(node)}/cpulist") as f:
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+    except (OSError, ValueError):
+        return
+    cpus &= os.sched_getaffinity(0)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+
+
 def worker(calls: int, warm: int = 8):
+    if os.environ.get("PFC_BIND_NODE"):
+        _bind_node(os.environ["PFC_BIND_NODE"])
     import torch
     from dips_amd import ChromaFilter, ComputeState, DiffSeriesOperator, DiPsFilter, PixelFormat
     W, H = 3840, 2160
@@ -84,7 +102,7 @@ def main():
     ap.add_argument("--calls", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--variants", default="8:0:1,12:0:1,16:0:1,8:1:1,16:1:1",
-                    help="comma list of threads:affinity[:DIPS_CALLBACK_DIRECT[:DIPS_CB_BLOCKING]]")
+                    help="comma list of threads:affinity[:DIPS_CALLBACK_DIRECT[:DIPS_CB_BLOCKING[:PFC_BIND_NODE]]]")
     args = ap.parse_args()
     if args.worker:
         print(json.dumps(worker(args.calls)), flush=True)
@@ -94,14 +112,16 @@ def main():
             th, aff, *rest = v.split(":")
             direct = rest[0] if rest else "1"
             blocking = rest[1] if len(rest) > 1 else "0"
+            node = rest[2] if len(rest) > 2 else ""
             env = dict(os.environ, DIPS_COPY_THREADS=th, DIPS_COPY_AFFINITY=aff, DIPS_CALLBACK_DIRECT=direct,
-                       DIPS_CB_BLOCKING=blocking)
+                       DIPS_CB_BLOCKING=blocking, PFC_BIND_NODE=node)
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--worker", "--calls", str(args.calls)],
                                env=env, capture_output=True, text=True, timeout=300)
             line = [l for l in p.stdout.splitlines() if l.startswith("{")]
             rec = json.loads(line[-1]) if line else {"failed": p.stderr[-800:]}
             rec.update({"round": r, "DIPS_COPY_THREADS": int(th), "DIPS_COPY_AFFINITY": int(aff),
-                        "DIPS_CALLBACK_DIRECT": int(direct), "DIPS_CB_BLOCKING": int(blocking)})
+                        "DIPS_CALLBACK_DIRECT": int(direct), "DIPS_CB_BLOCKING": int(blocking),
+                        "PFC_BIND_NODE": node})
             print(json.dumps(rec), flush=True)
 
 
