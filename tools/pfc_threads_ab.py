@@ -103,9 +103,22 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--variants", default="8:0:1,12:0:1,16:0:1,8:1:1,16:1:1",
                     help="comma list of threads:affinity[:DIPS_CALLBACK_DIRECT[:DIPS_CB_BLOCKING[:PFC_BIND_NODE]]]")
+    ap.add_argument("--env-variants", default=None,
+                    help="instead of --variants: '|'-separated variants of 'KEY=VAL,KEY=VAL' environment settings")
     args = ap.parse_args()
     if args.worker:
         print(json.dumps(worker(args.calls)), flush=True)
+        return
+    if args.env_variants is not None:
+        for r in range(args.rounds):
+            for v in args.env_variants.split("|"):
+                kv = dict(x.split("=", 1) for x in v.split(",") if x)
+                p = subprocess.run([sys.executable, os.path.abspath(__file__), "--worker", "--calls", str(args.calls)],
+                                   env=dict(os.environ, **kv), capture_output=True, text=True, timeout=300)
+                line = [l for l in p.stdout.splitlines() if l.startswith("{")]
+                rec = json.loads(line[-1]) if line else {"failed": p.stderr[-800:]}
+                rec.update({"round": r, "env": kv})
+                print(json.dumps(rec), flush=True)
         return
     for r in range(args.rounds):
         for v in args.variants.split(","):
