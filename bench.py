@@ -548,7 +548,8 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
     breakdown = {
         "phases_ms_median": {
             "sync": med("sync_us"), "staged": med("staged_us"), "launched": med("launched_us"),
-            "kernels_done": med("kernels_us"), "wall_in_library": med("wall_us")},
+            "expand_start": med("expand_start_us"), "last_kernel_wait_end": med("kernels_us"),
+            "wall_in_library": med("wall_us")},
         "cpu_ms_per_call_median": {"pack": med("pack_cpu_us"), "expand": med("expand_cpu_us"),
                                    "wait_for_kernels": med("wait_cpu_us")},
         "pool_threads": int(ph[0]["threads"]) if ph else None,
@@ -560,9 +561,17 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
                        if cg0 and cg1 and "usage_usec" in cg0 else None),
         "stripes": int(ph[0]["stripes"]) if ph else None,
         "host": _host_cpu(),
+        "cpu_bound": {"cpu_ms_per_call_over_threads": (round((med("pack_cpu_us") + med("expand_cpu_us"))
+                                                              / int(ph[0]["threads"]), 4) if ph else None),
+                      "host_bytes_per_call": 2 * W * H * 4 + W * H * 3,
+                      "note": "the pool's pack + expand work spread over its threads, against wall_in_library: the "
+                              "CPU side (host memory traffic: the RGBA8 frame read, 2 B/px packed, 1 B/px keys "
+                              "read, the RGBA8 output written) bounds the call; the GPU side alone moves a "
+                              "frame's packed input and keys in 0.31-0.34 ms (tools/zc_probe.hip)"},
         "note": "phase times from the call's start (dips_callback_phases): staged = last input piece packed "
-                "into pinned memory, launched = last stripe kernel launched, kernels_done = last stripe kernel "
-                "seen complete, wall_in_library = return; cpu sums over the copy pool's tasks",
+                "into pinned memory, launched = last stripe kernel launched, expand_start = first output task "
+                "started (the pool runs every staging task first), last_kernel_wait_end = last output task past "
+                "its wait for its stripe's kernel, wall_in_library = return; cpu sums over the copy pool's tasks",
     } if ph else {"phases": "not recorded (call did not take the zero-copy path)"}
     rec = {"frames_per_s": round(n_timed / tot, 1), "calls": n_timed,
            "ms_per_call_median": round(float(np.median(times)) * 1e3, 4),

@@ -293,7 +293,7 @@ class ComputeState:
         return ms.value, cnt.value
 
     CALLBACK_PHASES = ("sync_us", "staged_us", "launched_us", "kernels_us", "wall_us", "pack_cpu_us",
-                       "expand_cpu_us", "wait_cpu_us", "threads", "stripes")
+                       "expand_cpu_us", "wait_cpu_us", "threads", "stripes", "expand_start_us")
 
     def callback_phases(self) -> Optional[dict]:
         """Where the last zero-copy frame_callback spent its time

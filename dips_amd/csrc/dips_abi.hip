@@ -1563,7 +1563,8 @@ dips_status dips_callback_phases(const dips_handle* h, double* us, uint32_t cap,
     if (!h->cb_phases_valid) return DIPS_ERR_STATE;
     const dips_host::CallPhases& p = h->cb_phases;
     const double v[DIPS_CALLBACK_PHASES] = {p.sync_us,     p.staged_us,     p.launched_us, p.kernels_us, p.wall_us,
-                                            p.pack_cpu_us, p.expand_cpu_us, p.wait_cpu_us, p.threads,    p.stripes};
+                                            p.pack_cpu_us, p.expand_cpu_us, p.wait_cpu_us, p.threads,    p.stripes,
+                                            p.expand_us};
     for (uint32_t i = 0; i < cap && i < DIPS_CALLBACK_PHASES; ++i) us[i] = v[i];
     if (n) *n = DIPS_CALLBACK_PHASES;
     return DIPS_OK;

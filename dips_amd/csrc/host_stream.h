@@ -276,7 +276,9 @@ struct CallPhases {
     double sync_us = 0;      // the start-of-call stream synchronisations (caller)
     double staged_us = 0;    // the last input piece staged (packed) into pinned memory
     double launched_us = 0;  // the last stripe's kernel launched
-    double kernels_us = 0;   // the last stripe's kernel seen complete by a copy-out task
+    double kernels_us = 0;   // the last copy-out task past its wait for its stripe's kernel
+    double expand_us = 0;    // the first copy-out task started (all staging tasks taken: the
+                             // pool's tasks run in order, staging first)
     double wall_us = 0;      // the call returned (caller)
     double pack_cpu_us = 0;  // sum over staging tasks
     double expand_cpu_us = 0;  // sum over copy-out tasks, excluding their waits
@@ -326,6 +328,7 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
     // phase record: latest-event times as integer ns since t0 (atomic max),
     // CPU sums in ns
     std::atomic<int64_t> p_staged{0}, p_launched{0}, p_kernels{0}, p_pack{0}, p_expand{0}, p_wait{0};
+    std::atomic<int64_t> p_exp0{INT64_MAX};
     auto ns_since_t0 = [&]() {
         return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t0).count();
     };
@@ -373,6 +376,11 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
             return;
         }
         const int64_t w0 = ph ? ns_since_t0() : 0;
+        if (ph) {
+            int64_t cur = p_exp0.load(std::memory_order_relaxed);
+            while (w0 < cur && !p_exp0.compare_exchange_weak(cur, w0, std::memory_order_relaxed)) {
+            }
+        }
         int st;
         if (blocking) {
             std::unique_lock<std::mutex> lk(ready_mu);
@@ -409,6 +417,7 @@ hipError_t run_striped_frame_direct(const uint8_t* frame, uint8_t* out, uint32_t
         ph->staged_us = p_staged.load() * 1e-3;
         ph->launched_us = p_launched.load() * 1e-3;
         ph->kernels_us = p_kernels.load() * 1e-3;
+        ph->expand_us = p_exp0.load() == INT64_MAX ? 0.0 : p_exp0.load() * 1e-3;
         ph->pack_cpu_us = p_pack.load() * 1e-3;
         ph->expand_cpu_us = p_expand.load() * 1e-3;
         ph->wait_cpu_us = p_wait.load() * 1e-3;
@@ -459,6 +468,7 @@ hipError_t run_striped_frame_dma_keys(const uint8_t* frame, uint8_t* out, uint32
     std::atomic<int> err{(int)hipSuccess};
     using clk = std::chrono::steady_clock;
     std::atomic<int64_t> p_staged{0}, p_launched{0}, p_kernels{0}, p_pack{0}, p_expand{0}, p_wait{0};
+    std::atomic<int64_t> p_exp0{INT64_MAX};
     auto ns_since_t0 = [&]() {
         return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t0).count();
     };
@@ -510,6 +520,11 @@ hipError_t run_striped_frame_dma_keys(const uint8_t* frame, uint8_t* out, uint32
             return;
         }
         const int64_t w0 = ph ? ns_since_t0() : 0;
+        if (ph) {
+            int64_t cur = p_exp0.load(std::memory_order_relaxed);
+            while (w0 < cur && !p_exp0.compare_exchange_weak(cur, w0, std::memory_order_relaxed)) {
+            }
+        }
         int st;
         if (blocking) {
             std::unique_lock<std::mutex> lk(ready_mu);
@@ -536,6 +551,7 @@ hipError_t run_striped_frame_dma_keys(const uint8_t* frame, uint8_t* out, uint32
         ph->staged_us = p_staged.load() * 1e-3;
         ph->launched_us = p_launched.load() * 1e-3;
         ph->kernels_us = p_kernels.load() * 1e-3;
+        ph->expand_us = p_exp0.load() == INT64_MAX ? 0.0 : p_exp0.load() * 1e-3;
         ph->pack_cpu_us = p_pack.load() * 1e-3;
         ph->expand_cpu_us = p_expand.load() * 1e-3;
         ph->wait_cpu_us = p_wait.load() * 1e-3;

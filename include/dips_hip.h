@@ -187,14 +187,17 @@ dips_status dips_frame_callback_batch(dips_handle *h, uint32_t width, uint32_t h
  *   0 sync     us from the call's start to the end of its stream syncs
  *   1 staged   .. to the last input piece packed into pinned memory
  *   2 launched .. to the last stripe's kernel launch
- *   3 kernels  .. to the last stripe's kernel seen complete
+ *   3 kernels  .. to the last output task past its wait for its stripe's
+ *              kernel (output tasks start once every input piece is taken,
+ *              so this is max(kernel done, output task start))
  *   4 wall     .. to the call's return
  *   5 pack_cpu, 6 expand_cpu, 7 wait_cpu: thread-time sums (us) of the copy
  *     pool's staging tasks, output tasks and their waits for the kernels
  *   8 threads  copy-pool threads (workers + the calling thread)
  *   9 stripes  row stripes the frame was cut into
+ *  10 expand   us from the call's start to the first output task's start
  * DIPS_ERR_STATE if no such call has completed on `h`. */
-#define DIPS_CALLBACK_PHASES 10u
+#define DIPS_CALLBACK_PHASES 11u
 dips_status dips_callback_phases(const dips_handle *h, double *us, uint32_t cap, uint32_t *n);
 
 /* Copy the start texture (RGBA8 gray, pre_compute_shader.wgsl:92-132) built

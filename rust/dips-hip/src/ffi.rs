@@ -36,7 +36,7 @@ pub const DIPS_MODE_PER_FRAME: u32 = 1;
 pub const DIPS_FLAG_DEVICE_PTRS: u32 = 0x1;
 pub const DIPS_FLAG_TIME_KERNEL: u32 = 0x2;
 pub const DIPS_FLAG_FORCE_GENERIC: u32 = 0x4;
-pub const DIPS_CALLBACK_PHASES: u32 = 10;
+pub const DIPS_CALLBACK_PHASES: u32 = 11;
 
 /// `dips_params`: ComputeState::new's arguments (dips/src/gpu/mod.rs:59-65,
 /// DiPsProperties dips/src/lib.rs:63-86) + the batch series configuration.

@@ -223,7 +223,8 @@ impl ComputeState {
 
     /// Where the last zero-copy `frame_callback` spent its time
     /// (dips_callback_phases: sync, staged, launched, kernels, wall, pack /
-    /// expand / wait CPU sums in microseconds, pool threads, stripes).
+    /// expand / wait CPU sums in microseconds, pool threads, stripes, expand
+    /// start).
     pub fn callback_phases(&self) -> Option<[f64; ffi::DIPS_CALLBACK_PHASES as usize]> {
         let mut v = [0f64; ffi::DIPS_CALLBACK_PHASES as usize];
         let mut n = 0u32;
