@@ -51,28 +51,6 @@ class CopyPool {
 
     unsigned threads() const { return (unsigned)th_.size() + 1u; }
 
-    // Pin worker k to the k-th of the process's allowed CPUs taken `stride`
-    // apart (stride 16 on a 2 x 64-core EPYC: every other 8-core CCD, both
-    // sockets), so that the workers' memory streams do not share a CCD's
-    // fabric link.  Returns the workers pinned.
-    unsigned pin_workers_spread(unsigned stride) {
-        cpu_set_t allowed;
-        if (stride == 0 || sched_getaffinity(0, sizeof allowed, &allowed) != 0) return 0;
-        std::vector<int> cpus;
-        for (int c = 0; c < CPU_SETSIZE; ++c)
-            if (CPU_ISSET(c, &allowed)) cpus.push_back(c);
-        unsigned n = 0;
-        for (size_t k = 0; k < th_.size(); ++k) {
-            const size_t idx = k * stride;
-            if (idx >= cpus.size()) break;
-            cpu_set_t one;
-            CPU_ZERO(&one);
-            CPU_SET(cpus[idx], &one);
-            if (pthread_setaffinity_np(th_[k].native_handle(), sizeof one, &one) == 0) ++n;
-        }
-        return n;
-    }
-
     // Pin the workers to the CPUs of NUMA node `node` that this process may
     // use (the calling thread is left alone).  Returns the CPU count pinned
     // to, 0 if the node's CPU list is unreadable or disjoint from the

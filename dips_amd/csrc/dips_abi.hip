@@ -524,18 +524,12 @@ dips_status dips_params_default(dips_params* p) {
 }
 
 // DIPS_COPY_AFFINITY=1: pin the copy pool's workers to the CPUs of the NUMA
-// node the device hangs off (sysfs numa_node of its PCI function); =s<N>:
-// worker k on the process's (k * N)-th allowed CPU (spread over CCDs).  Once
-// per process, at the first handle (A/B runs: tools/pfc_threads_ab.py).
+// node the device hangs off (sysfs numa_node of its PCI function), once per
+// process, at the first handle (A/B runs: tools/pfc_threads_ab.py).
 void maybe_pin_copy_pool(int device) {
     static std::once_flag once;
     const char* e = std::getenv("DIPS_COPY_AFFINITY");
-    if (!e || (e[0] != '1' && e[0] != 's')) return;
-    if (e[0] == 's') {
-        const unsigned stride = (unsigned)std::strtoul(e + 1, nullptr, 10);
-        std::call_once(once, [stride]() { dips_host::CopyPool::global().pin_workers_spread(stride); });
-        return;
-    }
+    if (!e || e[0] != '1') return;
     std::call_once(once, [device]() {
         char bus[64] = {0};
         if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) != hipSuccess) return;
