@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <condition_variable>
 #include <cstddef>
@@ -98,6 +99,7 @@ class CopyPool {
             next_.store(0, std::memory_order_relaxed);
             busy_ = (unsigned)th_.size();
             ++gen_;
+            gen_seen_.store(gen_, std::memory_order_release);
         }
         cv_.notify_all();
         drain(fn, n);
@@ -134,9 +136,22 @@ class CopyPool {
     }
     void loop() {
         uint64_t seen = 0;
+        // DIPS_POOL_SPIN_US: after a run, watch for the next one this long
+        // before parking on the condition variable (back-to-back per-frame
+        // calls then skip the wake-up; A/B, tools/pfc_threads_ab.py)
+        static const long spin_us = []() {
+            const char* e = std::getenv("DIPS_POOL_SPIN_US");
+            const long v = e ? std::strtol(e, nullptr, 10) : 0;
+            return v > 0 && v <= 10000 ? v : 0L;
+        }();
         for (;;) {
             const std::function<void(size_t)>* fn;
             size_t n;
+            if (spin_us > 0 && seen != 0) {
+                const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
+                while (gen_seen_.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() < until)
+                    _mm_pause();
+            }
             {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_.wait(lk, [&]() { return stop_ || gen_ != seen; });
@@ -161,6 +176,7 @@ class CopyPool {
     std::atomic<size_t> next_{0};
     unsigned busy_ = 0;
     uint64_t gen_ = 0;
+    std::atomic<uint64_t> gen_seen_{0};  // gen_, readable without the mutex (the spin before parking)
     bool stop_ = false;
 };
 
