@@ -269,7 +269,10 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
     const uint64_t resident = per_simd * (uint64_t)h->cu_count * 4u;
     g.n_waves = g.items < resident ? g.items : resident;
     g.blocks = (g.n_waves + 3) / 4;
-    if ((C == 3 || C == 4) && pf) part_geometry(g, n_frames, resident);
+    // the part-major schedule: 'per-frame' batches; DIPS_SERIES_PARTS=2
+    // 'overall' ones too (A/B)
+    const char* pe = std::getenv("DIPS_SERIES_PARTS");
+    if ((C == 3 || C == 4) && (pf || (pe && pe[0] == '2'))) part_geometry(g, n_frames, resident);
     g.ok = g.n_tiles < (1ull << 32) && g.blocks < (1ull << 31);
     return g;
 }

@@ -683,3 +683,36 @@ def test_gray_auto_layout_branches_match_oracle(frac, mode, monkeypatch):
                 _check(got, out4, si)
         finally:
             op.close()
+
+
+@pytest.mark.parametrize("fmt_name,w,h,n", [("RGB8", 1920, 1080, 523), ("RGBA8", 1920, 1080, 525)])
+def test_part_major_overall_matches_contiguous_and_oracle(fmt_name, w, h, n, monkeypatch):
+    """'Overall' batches on the part-major schedule (DIPS_SERIES_PARTS=2:
+    each item loads the fixed reference tile at its part's first frame) --
+    series and map equal to the contiguous schedule's and every frame equal
+    to the oracle."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    fmt = getattr(PixelFormat, fmt_name)
+    c, tau = int(fmt), 8 / 255
+    op = DiffSeriesOperator(fmt, Mode.Overall, tau, 0)
+    try:
+        dev = torch.empty((n, h, w, c), dtype=torch.uint8, device="cuda")
+        op.synth_device(dev, w, h, 0xB0B, 11)
+        ref = dev[0].clone()
+        got, maps = {}, {}
+        for parts in ("2", "0"):
+            monkeypatch.setenv("DIPS_SERIES_PARTS", parts)
+            ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+            dmap = torch.empty_like(dev)
+            op.run_device(dev, ser, ref=ref, map_out=dmap)
+            torch.cuda.synchronize()
+            got[parts], maps[parts] = ser.cpu().numpy().view(np.uint64), dmap
+        monkeypatch.delenv("DIPS_SERIES_PARTS")
+        assert np.array_equal(got["2"], got["0"])
+        assert torch.equal(maps["2"], maps["0"])
+        out4, _, _ = oracle.series(dev.cpu().numpy(), mode=0, tau=tau, ref=ref.cpu().numpy(), nthreads=16)
+        bad = np.nonzero(~np.all(got["2"] == out4, axis=1))[0]
+        assert bad.size == 0, f"frames differing from the oracle: {bad[:10]}"
+    finally:
+        op.close()

@@ -33,7 +33,8 @@ def main():
     mode = Mode.PerFrame if (len(sys.argv) <= 4 or sys.argv[4] == "per-frame") else Mode.Overall
     names = (sys.argv[5] if len(sys.argv) > 5 else "isi,f64").split(",")
     env_of = {"f64": ("DIPS_SERIES_ISI", "0"), "isi": ("DIPS_SERIES_ISI", "1"), "sadi": ("DIPS_SERIES_ISI", "2"),
-              "contig": ("DIPS_SERIES_PARTS", "0"), "parts": ("DIPS_SERIES_PARTS", "1")}
+              "contig": ("DIPS_SERIES_PARTS", "0"), "parts": ("DIPS_SERIES_PARTS", "1"),
+              "partsall": ("DIPS_SERIES_PARTS", "2")}
     frames = torch.empty((F, H, W, 3), dtype=torch.uint8, device="cuda")
     op = DiffSeriesOperator(PixelFormat.RGB8, mode, 8 / 255, time_kernel=True)
     op.synth_device(frames, W, H, 0xD1B5, 0)
