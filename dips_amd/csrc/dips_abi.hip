@@ -203,10 +203,11 @@ struct FastGeom {
 // slot), else the best-filling one; the waves then get ceil(items / n_waves)
 // or one fewer items each (4K RGB8, 5000 frames: L = 1000, 5,063 waves).  Batches of
 // fewer than 256 frames keep the contiguous ranges (DIPS_SERIES_PARTS=0:
-// always, A/B runs).  'Per-frame' mode only: in one process, alternated
-// (tools/isi_ab.py, profiles/r03/parts/), per-frame 77.3 % against 75.4 %
-// of 8 TB/s with 1.2 % less energy per frame; 'overall' 73.8 % against
-// 73.9 % (no gain: it keeps the contiguous ranges).
+// always, A/B runs).  In one process, alternated (tools/isi_ab.py,
+// profiles/r03/parts/), per-frame 77.3 % against 75.4 % of 8 TB/s with 1.2 %
+// less energy per frame; 'overall' measured 73.8 against 73.9 % in round 3
+// and 74.1 against 72.05 % in round 4 (profiles/r04/l/), so since round 4
+// 'overall' batches take it too (fast_geometry).
 void part_geometry(FastGeom& g, uint64_t n_frames, uint64_t resident) {
     const char* e = std::getenv("DIPS_SERIES_PARTS");
     if ((e && e[0] == '0') || n_frames < 256 || g.n_tiles == 0 || resident == 0) return;
@@ -269,10 +270,13 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
     const uint64_t resident = per_simd * (uint64_t)h->cu_count * 4u;
     g.n_waves = g.items < resident ? g.items : resident;
     g.blocks = (g.n_waves + 3) / 4;
-    // the part-major schedule: 'per-frame' batches; DIPS_SERIES_PARTS=2
-    // 'overall' ones too (A/B)
+    // the part-major schedule for 'per-frame' and 'overall' batches alike
+    // (DIPS_SERIES_PARTS=1: 'per-frame' only, the round-3 default; =0: off).
+    // 'Overall' at 4K, three alternated rounds in one process
+    // (tools/isi_ab.py, profiles/r04/l/): 74.1 % of 8 TB/s against 72.05 %
+    // with contiguous ranges, 5.37 against 5.62 mJ per frame
     const char* pe = std::getenv("DIPS_SERIES_PARTS");
-    if ((C == 3 || C == 4) && (pf || (pe && pe[0] == '2'))) part_geometry(g, n_frames, resident);
+    if ((C == 3 || C == 4) && (pf || !(pe && pe[0] == '1'))) part_geometry(g, n_frames, resident);
     g.ok = g.n_tiles < (1ull << 32) && g.blocks < (1ull << 31);
     return g;
 }

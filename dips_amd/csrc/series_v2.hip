@@ -265,8 +265,7 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
 
     uint64_t i = (uint64_t)wave * a.items / a.n_waves;
     const uint64_t iend = (uint64_t)(wave + 1) * a.items / a.n_waves;
-    const bool parts = SCHED == 1 || a.part_frames != 0u;  // wave-uniform (part_geometry: per-frame batches,
-                                                           // 'overall' too with DIPS_SERIES_PARTS=2)
+    const bool parts = SCHED == 1 || a.part_frames != 0u;  // wave-uniform (part_geometry)
     const uint32_t plen = parts ? a.part_frames : 1u;
     const uint64_t pitems = parts ? (uint64_t)((a.n_frames + plen - 1) / plen) * a.n_tiles : 0u;
     uint64_t it = wave;

@@ -687,8 +687,9 @@ def test_gray_auto_layout_branches_match_oracle(frac, mode, monkeypatch):
 
 @pytest.mark.parametrize("fmt_name,w,h,n", [("RGB8", 1920, 1080, 523), ("RGBA8", 1920, 1080, 525)])
 def test_part_major_overall_matches_contiguous_and_oracle(fmt_name, w, h, n, monkeypatch):
-    """'Overall' batches on the part-major schedule (DIPS_SERIES_PARTS=2:
-    each item loads the fixed reference tile at its part's first frame) --
+    """'Overall' batches on the part-major schedule (the default since round
+    4, DIPS_SERIES_PARTS=2 forces it: each item loads the fixed reference
+    tile at its part's first frame) --
     series and map equal to the contiguous schedule's and every frame equal
     to the oracle."""
     import torch

@@ -9,7 +9,7 @@ runs it with 3 parts of 174 frames (the last 172) on a 256-CU MI355X, so
 items start mid-batch and the last part is short -- asserted through the
 library's own geometry, then every one of the 520 series entries must equal
 the oracle's (get_intensity, dips/src/gpu/shaders/dips_shader.wgsl:64-82).
-Also at 4K: 'overall' (configs[3]'s mode, the contiguous schedule) and
+Also at 4K: 'overall' (configs[3]'s mode, part-major since round 4) and
 RGBA8 frames at a +2-byte offset (the aligned-load form a caller's ring
 buffer lands on)."""
 import numpy as np
