@@ -104,7 +104,6 @@ struct dips_handle {
     int cb_occupancy = 0;
     DevBuf gray_lut;          // T_d / T_c tables of series_gray_lut_kernel (128 KiB) for gray_lut_tau
                               // (layout 4: layout 3's and layout 2's, kGrayLutAllocBytes apart)
-    DevBuf gray_probe;        // layout 4: the sampled band count of the current launch
     DevBuf pk_in, pk_out;     // DIPS_CALLBACK_DIRECT=2: packed input / keys of the per-frame call in HBM
     bool gray_lut_valid = false;
     float gray_lut_tau = 0.0f;
@@ -385,8 +384,6 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     const bool pf = h->p.mode == DIPS_MODE_PER_FRAME;
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t fb = npx * (uint64_t)C;
-    DIPS_HIP(h, hipMemsetAsync(series, 0, sizeof(dips_series_entry) * (size_t)n_frames, s));
-
     FastGeom g;
     const bool glut = C == 1 && gray_lut_enabled();
     // RGB8 / RGBA8 frames off a 4-byte boundary (an odd frame stride or an
@@ -403,6 +400,12 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC))
         g = glut ? gray_lut_geometry(h, width, height, n_frames)
                  : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr, align, isi);
+    // the series starts at zero: the table and RGB(A) kernels clear it
+    // themselves (SeriesArgs::zero), saving a fill launch; the others after a
+    // fill (DIPS_SERIES_KZERO=0: always the fill, A/B runs)
+    const char* kz_env = std::getenv("DIPS_SERIES_KZERO");
+    const bool kzero = g.ok && (glut || C != 1) && n_frames < (1u << 30) && !(kz_env && kz_env[0] == '0');
+    if (!kzero) DIPS_HIP(h, hipMemsetAsync(series, 0, sizeof(dips_series_entry) * (size_t)n_frames, s));
     auto launch_generic = [&](uint64_t px0) -> dips_status {
         const uint64_t bpf = (npx - px0 + 255u) / 256u;
         if (bpf * (uint64_t)n_frames >= (1ull << 31))
@@ -441,23 +444,17 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
         DIPS_HIP(h, h->partials.ensure((size_t)g.items * 16u));
         dips::SeriesArgs a{};
         if (glut && h->gray_lut_layout == 4) {
-            // the band occupancy of one frame pair of the batch (inside the
-            // timed region: it is part of the launch)
-            DIPS_HIP(h, h->gray_probe.ensure(256));
-            const uint8_t* pf_frame = frames + (n_frames > 1 ? fb : 0);
-            const uint8_t* pf_ref = (pf && n_frames > 1) ? frames : ref0;
-            hipError_t pe = hipSuccess;
-            uint32_t pw = 0;
-            const uint32_t sampled = dips::launch_gray_band_probe(pf_frame, pf_ref, (uint32_t)g.vec_bytes,
-                                                                  h->gray_lut.as<uint8_t>(),
-                                                                  h->gray_probe.as<uint32_t>(), s, &pe, &pw);
-            DIPS_HIP(h, pe);
+            // layout 4's thresholds in 1/1024 of the sampled pixels (each
+            // workgroup samples its own items, series_gray.hip gray_sample);
+            // the forced settings: 0 -> always layout 5, > 1024 -> always 2
             const double fmin = gray_auto_frac();
-            a.probe = h->gray_probe.as<uint32_t>();
-            a.probe_min = sampled ? (uint32_t)std::ceil(fmin * (double)sampled) : (fmin > 1.0 ? 1u : 0u);
-            // the forced settings (0, > 1) decide by probe_min alone
-            a.probe_hi = (fmin == 0.0 || fmin > 1.0) ? a.probe_min : (uint32_t)std::ceil(kGrayAutoHi * (double)sampled);
-            a.probe_spread = (fmin == 0.0 || fmin > 1.0) ? 0u : kGrayAutoSpread * pw;
+            a.probe_min = fmin == 0.0 ? 0u : (fmin > 1.0 ? 1025u : std::max(1u, (uint32_t)std::ceil(fmin * 1024.0)));
+            a.probe_hi = (uint32_t)std::ceil(kGrayAutoHi * 1024.0);
+            a.probe_spread = kGrayAutoSpread;
+        }
+        if (kzero) {
+            a.zero = reinterpret_cast<uint64_t*>(series);
+            a.zero_n = 4u * n_frames;
         }
         a.frames = frames;
         a.ref0 = ref0;
@@ -629,7 +626,6 @@ void dips_destroy(dips_handle* h) {
     h->cb_lut.release();
     h->pk_in.release();
     h->pk_out.release();
-    h->gray_probe.release();
     h->gray_lut.release();
     h->start.release();
     h->out.release();

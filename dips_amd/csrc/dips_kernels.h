@@ -60,10 +60,16 @@ struct SeriesArgs {
     const void* lut;         // GRAY8 table kernel: T_d / T_c bytes (series_gray.hip), 128 KiB
     uint32_t part_frames;    // frames per part of the part-major schedule (series_v2 SCHED = 1)
     uint32_t thr_int;        // series_v2 SADI (ISI = 2): T = tau * 2^28 as an integer (series_sadi_threshold)
-    const uint32_t* probe;   // GRAY8 table kernel, layout 4: {band pixels, sum of wave spreads} of a sample
-    uint32_t probe_min;      //   layout 3 when band >= probe_min and (band >= probe_hi or spread >= probe_spread)
+    // GRAY8 table kernel, layout 4: each workgroup samples its waves' first
+    // items and takes layout 5 when band >= probe_min / 1024 of the sampled
+    // pixels and (band >= probe_hi / 1024 of them or the waves' byte spreads
+    // average >= probe_spread), else layout 2 (probe_min 0: always 5, > 1024:
+    // always 2)
+    uint32_t probe_min;
     uint32_t probe_hi;
     uint32_t probe_spread;
+    uint64_t* zero;          // when set: the kernel zeroes zero[0 .. zero_n) (the series, before its
+    uint32_t zero_n;         // reduce's atomics; replaces a separate fill launch)
 };
 
 struct GenericArgs {
@@ -260,18 +266,12 @@ hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, boo
 hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
                                 dips_series_entry* series, hipStream_t s, uint32_t thr_int = 0);
 // GRAY8 table kernel, table layout 1 (two byte tables), 2 (one u16 table) or
-// 3 (the u16 table keyed by (a ^ b, a), band clamp: the default)
+// 3 (the u16 table keyed by (a ^ b, a), band clamp), 5 (the same unswizzled)
+// or 4 (5 or 2 per workgroup from a sample of its items: the default)
 const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs = 0, uint32_t waves = 16);
 int gray_alu_vecs(float tau);          // arithmetic vecs of this call's table kernel (0 for tau < 2^-5)
 uint32_t gray_lut_waves(int layout, int alu_vecs);  // waves per group of the table kernel
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s);
-// layout 4 (auto): waves of the content probe (64 consecutive 16-pixel vecs
-// each, spread over the frame)
-constexpr uint32_t kGrayProbeWaves = 256;
-// the content sample of frame f against r into out[0..1]; returns the pixels
-// sampled (0: none), *waves the blocks
-uint32_t launch_gray_band_probe(const uint8_t* f, const uint8_t* r, uint32_t vec_bytes, const uint8_t* lut3,
-                                 uint32_t* out, hipStream_t s, hipError_t* err, uint32_t* waves);
 hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
                                   hipStream_t s, int alu_vecs = 0);
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);

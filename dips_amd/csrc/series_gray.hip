@@ -418,27 +418,119 @@ __device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* ld
     }
 }
 
-// LAYOUT 4 (auto, the default): layout 5 or 2 per launch from a sample of
-// the batch (gray_band_probe_kernel) -- the table of the chosen layout is the
-// one copied into LDS (a.lut: layout 5's table + band word, then layout 2's
-// at kGrayLutAllocBytes).  Layout 5 (keyed by (a ^ b, a), band clamp, no
-// bank swizzle) turns the lookups of band pixels into broadcasts, and its
-// other lookups spread over the banks as the frame bytes a do: well when a
-// wave's 64 lanes see many levels, badly when they see a handful (flat
-// content: 16-way conflicts).  Layout 2 (keyed by (a, b), swizzled) has no
-// broadcasts but few conflicts on such narrow content.  So: layout 5 when
-// the band holds >= probe_min of the sampled pixels and either nearly all
-// of them (probe_hi) or the waves' bytes spread over >= probe_spread / waves
-// levels, else layout 2 (tools/gray_layout_ab.py over five contents,
-// profiles/r04/d/).
+// LAYOUT 4 (auto, the default): layout 5 or 2 per workgroup from a sample of
+// its own items (gray_sample) -- the table of the chosen layout is the one
+// copied into LDS (a.lut: layout 5's table + band word, then layout 2's at
+// kGrayLutAllocBytes).  Layout 5 (keyed by (a ^ b, a), band clamp, no bank
+// swizzle) turns the lookups of band pixels into broadcasts, and its other
+// lookups spread over the banks as the frame bytes a do: well when a wave's
+// 64 lanes see many levels, badly when they see a handful (flat content:
+// 16-way conflicts).  Layout 2 (keyed by (a, b), swizzled) has no broadcasts
+// but few conflicts on such narrow content.  So: layout 5 when the band holds
+// >= probe_min / 1024 of the sampled pixels and either nearly all of them
+// (probe_hi / 1024) or the waves' bytes spread over >= probe_spread levels on
+// average, else layout 2 (tools/gray_layout_ab.py over five contents,
+// profiles/r04/d/).  Until round 4's last pass a separate probe kernel took
+// one sample per launch; sampling inside the kernel drops that launch and its
+// fill (11-12 us of a 640x480 x 300-frame batch, profiles/r04/small/) and
+// lets each workgroup follow the content of the tiles it walks.
+
+// One wave's sample: the first 64-vec row of its first item's tile (a frame
+// and its reference, as gray_walk will read them), band pixels below layout 5's clamp
+// (x = a ^ b < 2^m), the spread max - min of the frame bytes, pixels counted.
+template <int U, bool PF>
+__device__ __forceinline__ void gray_sample(const SeriesArgs& a, uint32_t wave, uint32_t lane, const uint8_t* lut5,
+                                            uint32_t& band, uint32_t& spread, uint32_t& px) {
+    band = 0u;
+    spread = 0u;
+    px = 0u;
+    if (wave >= a.n_waves) return;
+    uint32_t tile, t0;
+    if (PF && a.part_frames != 0u) {  // item `wave` of the part-major order
+        const uint32_t part = wave / a.n_tiles;
+        tile = wave - part * a.n_tiles;
+        t0 = part * a.part_frames;
+    } else {
+        const uint64_t i = (uint64_t)wave * a.items / a.n_waves;
+        tile = (uint32_t)(i / a.n_frames);
+        t0 = (uint32_t)(i - (uint64_t)tile * a.n_frames);
+    }
+    // the item's second frame when it has one: its first can be the batch's
+    // frame 0, which a caller often passes as its own reference too (an
+    // identical pair, all band: the flat-content rate fell to 52 % when half
+    // the workgroups sampled that pair)
+    const uint32_t ts = min(t0 + 1u, a.n_frames - 1u);
+    const uint8_t* f = a.frames + (uint64_t)ts * a.frame_bytes;
+    const uint8_t* r = PF ? (ts == 0 ? a.ref0 : f - a.frame_bytes) : a.ref0;
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(lut5 + kGrayBandOffset);
+    const uint32_t first = 256u - min(w, 255u);
+    const uint32_t lim = 1u << (31u - __builtin_clz(first));  // 2^m
+    const uint32_t off = (tile * U * 64u + lane) * 16u;
+    uint32_t c = 0u, mx = 0u, mn = 255u, n = 0u;
+    if (off < a.vec_bytes) {
+        const __amdgpu_buffer_rsrc_t rf = make_rsrc(f, a.vec_bytes), rr = make_rsrc(r, a.vec_bytes);
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rf, off, 0, 0);
+        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0);
+        const uint32_t fa[4] = {x.x, x.y, x.z, x.w};
+        const uint32_t d[4] = {x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                c += ((d[k] >> (8 * b)) & 0xFFu) < lim ? 1u : 0u;
+                const uint32_t v = (fa[k] >> (8 * b)) & 0xFFu;
+                mx = max(mx, v);
+                mn = min(mn, v);
+            }
+        n = 16u;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        c += (uint32_t)__shfl_xor((int)c, o);
+        n += (uint32_t)__shfl_xor((int)n, o);
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+    }
+    band = c;
+    spread = mx > mn ? mx - mn : 0u;
+    px = n;
+}
+
 template <int U, bool PF, bool MAP, int LAYOUT, int NA = 0, int GW = kGrayWaves>
 __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) {
     __shared__ uint32_t lds32[32768];  // T_d at byte 0, T_c at byte kGrayLutTcOffset
+    zero_series(a);
     bool use5 = true;
     if constexpr (LAYOUT == 4) {
-        const uint32_t band = __builtin_amdgcn_readfirstlane(a.probe[0]);
-        const uint32_t spread = __builtin_amdgcn_readfirstlane(a.probe[1]);
-        use5 = band >= a.probe_min && (band >= a.probe_hi || spread >= a.probe_spread);
+        __shared__ uint32_t smp[3 * GW];
+        const uint32_t lane = threadIdx.x & 63u, wl = threadIdx.x >> 6;
+        uint32_t band, spread, px;
+        gray_sample<U, PF>(a, __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)GW + wl), lane,
+                           static_cast<const uint8_t*>(a.lut), band, spread, px);
+        if (lane == 0u) {
+            smp[3 * wl] = band;
+            smp[3 * wl + 1] = spread;
+            smp[3 * wl + 2] = px;
+        }
+        __syncthreads();
+        uint32_t sb = 0u, ss = 0u, sp = 0u, nw = 0u;
+#pragma unroll
+        for (int k = 0; k < GW; ++k) {
+            sb += smp[3 * k];
+            ss += smp[3 * k + 1];
+            sp += smp[3 * k + 2];
+            nw += smp[3 * k + 2] != 0u ? 1u : 0u;
+        }
+        sb = __builtin_amdgcn_readfirstlane(sb);
+        ss = __builtin_amdgcn_readfirstlane(ss);
+        sp = __builtin_amdgcn_readfirstlane(sp);
+        nw = __builtin_amdgcn_readfirstlane(nw);
+        if (a.probe_min == 0u)
+            use5 = true;
+        else if (a.probe_min > 1024u)
+            use5 = false;
+        else
+            use5 = sb * 1024u >= a.probe_min * sp && (sb * 1024u >= a.probe_hi * sp || ss >= a.probe_spread * nw);
     }
     const uint8_t* lut = static_cast<const uint8_t*>(a.lut) + ((LAYOUT == 4 && !use5) ? kGrayLutAllocBytes : 0u);
     {
@@ -455,53 +547,6 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
             gray_walk<U, PF, MAP, 2, NA, GW>(a, lds, lut);
     } else {
         gray_walk<U, PF, MAP, LAYOUT, NA, GW>(a, lds, lut);
-    }
-}
-
-// Content of a sample of the batch (LAYOUT 4's choice): one block of 64
-// consecutive 16-pixel vecs per wave (as the series kernel's lanes read
-// them), the blocks `stride` vecs apart, of frame f (n_vec vecs) and its
-// reference r.
-// out[0] += the pixels whose table row x = a ^ b lies below layout 5's band
-// clamp (x < 2^m, from the band word after its table) -- the lookups that
-// become broadcasts; out[1] += per block, max - min of the frame bytes --
-// over how many levels (columns of layout 5, banks) the wave's other
-// lookups spread.
-__global__ __launch_bounds__(256) void gray_band_probe_kernel(const uint8_t* f, const uint8_t* r, uint32_t vb,
-                                                              uint32_t n_vec, uint32_t stride,
-                                                              const uint8_t* lut3, uint32_t* out) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const uint32_t w = *reinterpret_cast<const uint32_t*>(lut3 + kGrayBandOffset);
-    const uint32_t first = 256u - min(w, 255u);
-    const uint32_t lim = 1u << (31u - __builtin_clz(first));  // 2^m
-    const uint32_t v = wave * stride + lane;
-    uint32_t c = 0, mx = 0, mn = 255;
-    if (v < n_vec) {
-        const __amdgpu_buffer_rsrc_t rf = make_rsrc(f, vb), rr = make_rsrc(r, vb);
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rf, v * 16u, 0, kAuxNT);
-        const u32x4 y = __builtin_amdgcn_raw_buffer_load_b128(rr, v * 16u, 0, kAuxNT);
-        const uint32_t fa[4] = {x.x, x.y, x.z, x.w};
-        const uint32_t d[4] = {x.x ^ y.x, x.y ^ y.y, x.z ^ y.z, x.w ^ y.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                c += ((d[k] >> (8 * b)) & 0xFFu) < lim ? 1u : 0u;
-                const uint32_t a = (fa[k] >> (8 * b)) & 0xFFu;
-                mx = max(mx, a);
-                mn = min(mn, a);
-            }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        c += (uint32_t)__shfl_xor((int)c, o);
-        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-    }
-    if (lane == 0u) {
-        if (c) atomicAdd(out, c);
-        if (mx > mn) atomicAdd(out + 1, mx - mn);
     }
 }
 
@@ -586,19 +631,6 @@ hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
     }
     hipLaunchKernelGGL(gray_lut_kernel, dim3(256), dim3(256), 0, s, tab, tau, (uint32_t)layout);
     return hipGetLastError();
-}
-
-uint32_t launch_gray_band_probe(const uint8_t* f, const uint8_t* r, uint32_t vec_bytes, const uint8_t* lut3,
-                                 uint32_t* out, hipStream_t s, hipError_t* err, uint32_t* waves) {
-    const uint32_t nvec = vec_bytes / 16u;
-    const uint32_t nw = std::min<uint32_t>(kGrayProbeWaves, nvec / 64u);  // whole 64-vec blocks only
-    *waves = nw;
-    *err = hipMemsetAsync(out, 0, 8, s);  // zero even without a sample: the kernel reads it
-    if (*err != hipSuccess || nw == 0) return 0;
-    hipLaunchKernelGGL(gray_band_probe_kernel, dim3((nw + 3u) / 4u), dim3(256), 0, s, f, r, vec_bytes, nvec,
-                       nvec / nw, lut3, out);
-    *err = hipGetLastError();
-    return nw * 64u * 16u;
 }
 
 hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,

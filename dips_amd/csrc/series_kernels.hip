@@ -666,8 +666,13 @@ hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, boo
 
 hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
                                 dips_series_entry* series, hipStream_t s, uint32_t thr_int) {
-    const uint32_t tpb = 64;
-    dim3 grid((n_frames + 255u) / 256u, (n_tiles + tpb - 1u) / tpb);
+    // 64 tiles per thread (eight rounds of eight loads) when that still
+    // gives >= 2048 groups (4K: 20 x 127), else down to 8 (one round): small
+    // batches are latency-bound here (640x480 x 300 frames: 4 groups, 6 us)
+    const uint32_t gx = (n_frames + 255u) / 256u;
+    uint32_t tpb = 64;
+    while (tpb > 8u && (uint64_t)gx * ((n_tiles + tpb - 1u) / tpb) < 2048u && n_tiles / (tpb >> 1) < 65535u) tpb >>= 1;
+    dim3 grid(gx, (n_tiles + tpb - 1u) / tpb);
     hipLaunchKernelGGL(series_reduce_kernel, grid, dim3(256), 0, s, partials, n_frames, n_tiles, tpb, (uint32_t)layout,
                        thr_int, series);
     return hipGetLastError();

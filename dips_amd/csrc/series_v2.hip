@@ -254,6 +254,7 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
     constexpr bool A4 = ALIGN && C == 4;  // RGBA8: the fifth dword from the next lane
     constexpr int LW = (ALIGN && C == 3) ? F::NDW + 1 : F::NDW;  // dwords loaded per vec
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
+    zero_series(a);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (wave >= a.n_waves) return;

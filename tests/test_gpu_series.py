@@ -657,9 +657,9 @@ def test_part_major_schedule_matches_contiguous_and_oracle(fmt_name, w, h, n, mo
 @pytest.mark.parametrize("frac", ["0", "2", None])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_gray_auto_layout_branches_match_oracle(frac, mode, monkeypatch):
-    """GRAY8 table layout 4 (the default): one kernel that takes layout 5
-    (band clamp) or layout 2 per launch from a content sample of the batch's
-    first frame pair.  DIPS_GRAY_AUTO_FRAC=0 forces the layout-5 branch, 2 the
+    """GRAY8 table layout 4 (the default): one kernel whose workgroups each
+    take layout 5 (band clamp) or layout 2 from a sample of their own first
+    items.  DIPS_GRAY_AUTO_FRAC=0 forces the layout-5 branch, 2 the
     layout-2 branch, unset the content's own choice -- every branch against
     the oracle on synthetic, random, identical and ragged clips, tau 0 / 8/255
     / 0.5, with and without the map, one-frame batches included."""
@@ -681,6 +681,63 @@ def test_gray_auto_layout_branches_match_oracle(frac, mode, monkeypatch):
                 _check(got, out4, si, gmap, dmap)
                 got, _ = op(fr)
                 _check(got, out4, si)
+        finally:
+            op.close()
+
+
+@pytest.mark.parametrize("mode,n", [(0, 40), (1, 300)])
+def test_gray_auto_mixed_content_per_workgroup(mode, n, monkeypatch):
+    """Layout 4 decides per workgroup, so one launch can run both tables: a
+    2048 x 512 clip whose row bands are flat noise (128 +- 3: layout 2),
+    slowly varying synthetic content and i.i.d. random bytes, 'overall' (40
+    frames, contiguous ranges) and 'per-frame' (300 frames, the part-major
+    schedule) -- every frame and the map equal to the oracle."""
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    monkeypatch.delenv("DIPS_GRAY_AUTO_FRAC", raising=False)
+    monkeypatch.delenv("DIPS_GRAY_LUT", raising=False)
+    rng = np.random.default_rng(77 + mode)
+    w, h = 2048, 512
+    fr = oracle.synth(1, w, h, 0xD1B5, 0, n)
+    fr[:, :128] = (128 + rng.integers(-3, 4, (n, 128, w))).astype(np.uint8)
+    fr[:, 384:] = rng.integers(0, 256, (n, 128, w), dtype=np.uint8)
+    op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), 8 / 255, 0)
+    try:
+        out4, si, dmap = oracle.series(fr, mode=mode, tau=8 / 255, want_map=True, nthreads=8)
+        got, gmap = op(fr, want_map=True)
+        _check(got, out4, si, gmap, dmap)
+    finally:
+        op.close()
+
+
+@pytest.mark.parametrize("fmt_name,env", [("RGB8", {}), ("RGBA8", {}), ("Gray8", {}), ("Gray8", {"DIPS_GRAY_LUT": "0"}),
+                                          ("RGB8", {"DIPS_SERIES_KZERO": "0"})])
+def test_series_starts_from_zero_on_a_dirty_buffer(fmt_name, env, monkeypatch):
+    """The RGB(A) and GRAY8 table kernels clear the caller's series
+    themselves (SeriesArgs::zero, no fill launch); the f32 GRAY8 kernel
+    (DIPS_GRAY_LUT=0) and DIPS_SERIES_KZERO=0 after a fill.  A series tensor
+    full of garbage, twice in a row, must come out equal to the oracle -- at
+    300 frames (part-major, the adaptive reduce grid) and 3 frames."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    for k in ("DIPS_GRAY_LUT", "DIPS_SERIES_KZERO"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    lut = env
+    fmt = getattr(PixelFormat, fmt_name)
+    c = int(fmt)
+    for n, w, h in ((300, 256, 96), (3, 640, 480)):
+        frames = _frames(c, w, h, n, 5 + n, "synth")
+        want, _, _ = oracle.series(frames, mode=1, tau=8 / 255, nthreads=8)
+        op = DiffSeriesOperator(fmt, Mode.PerFrame, 8 / 255, 0)
+        try:
+            dev = torch.from_numpy(frames).cuda()
+            ser = torch.full((n, 4), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device="cuda")
+            for _ in range(2):
+                op.run_device(dev, ser)
+                torch.cuda.synchronize()
+                assert np.array_equal(ser.cpu().numpy().view(np.uint64), want), (fmt_name, lut, n)
+                ser.fill_(-1)
         finally:
             op.close()
 

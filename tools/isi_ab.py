@@ -34,7 +34,8 @@ def main():
     names = (sys.argv[5] if len(sys.argv) > 5 else "isi,f64").split(",")
     env_of = {"f64": ("DIPS_SERIES_ISI", "0"), "isi": ("DIPS_SERIES_ISI", "1"), "sadi": ("DIPS_SERIES_ISI", "2"),
               "contig": ("DIPS_SERIES_PARTS", "0"), "parts": ("DIPS_SERIES_PARTS", "1"),
-              "partsall": ("DIPS_SERIES_PARTS", "2")}
+              "partsall": ("DIPS_SERIES_PARTS", "2"), "kzero": ("DIPS_SERIES_KZERO", "1"),
+              "fill": ("DIPS_SERIES_KZERO", "0")}
     frames = torch.empty((F, H, W, 3), dtype=torch.uint8, device="cuda")
     op = DiffSeriesOperator(PixelFormat.RGB8, mode, 8 / 255, time_kernel=True)
     op.synth_device(frames, W, H, 0xD1B5, 0)
@@ -55,6 +56,7 @@ def main():
         for name, (var, env) in (order if rnd % 2 == 0 else order[::-1]):
             os.environ.pop("DIPS_SERIES_ISI", None)
             os.environ.pop("DIPS_SERIES_PARTS", None)
+            os.environ.pop("DIPS_SERIES_KZERO", None)
             os.environ[var] = env
             r = None if mode == Mode.PerFrame else ref
             op.run_device(frames, series[name], ref=r)  # warm
