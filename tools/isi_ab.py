@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 def main():
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    W, H = 3840, 2160
+    W, H = (int(v) for v in (sys.argv[6] if len(sys.argv) > 6 else "3840x2160").split("x"))
     F = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
@@ -87,11 +87,13 @@ def main():
             print(json.dumps(rec), flush=True)
     os.environ.pop("DIPS_SERIES_ISI", None)
     os.environ.pop("DIPS_SERIES_PARTS", None)
+    os.environ.pop("DIPS_SERIES_KZERO", None)
     same = all(bool(torch.equal(series[names[0]], series[k])) for k in names[1:])
-    summ = {"summary": True, "mode": "per-frame" if mode == Mode.PerFrame else "overall", "series_equal": same}
+    summ = {"summary": True, "size": f"{W}x{H}", "frames": F, "mode": "per-frame" if mode == Mode.PerFrame else "overall", "series_equal": same}
     for k, v in res.items():
         summ[k] = {"frac_median": float(np.median([r["frac_of_8TBps"] for r in v])),
-                   "mJ_per_frame_median": float(np.median([r.get("mJ_per_frame", np.nan) for r in v]))}
+                   "mJ_per_frame_median": float(np.median([r.get("mJ_per_frame", np.nan) for r in v])),
+                   "wall_frames_per_s_median": float(np.median([r["wall_frames_per_s"] for r in v]))}
     print(json.dumps(summ), flush=True)
     op.close()
 
