@@ -60,3 +60,53 @@ def test_avx2_packers_equal_scalar(tmp_path):
         pytest.skip(out.stdout.strip())
     assert out.returncode == 0, out.stdout + out.stderr
     assert "bad 0" in out.stdout
+
+
+POOL_HARNESS = r'''
+#include "copy_pool.h"
+#include <atomic>
+#include <cstdio>
+#include <thread>
+#include <vector>
+using namespace dips_host;
+int main() {
+    // back-to-back runs of varying size on one pool, each task bumping its own
+    // slot: every slot of every run exactly once, nothing after run() returns
+    CopyPool pool(7);
+    long bad = 0;
+    for (int r = 0; r < 20000; ++r) {
+        const size_t n = 1 + (size_t)(r * 7919) % 37;
+        std::vector<std::atomic<int>> hits(n);
+        for (auto& h : hits) h.store(0);
+        pool.run(n, [&](size_t i) {
+            if (i % 5 == 0) std::this_thread::yield();
+            hits[i].fetch_add(1);
+        });
+        for (size_t i = 0; i < n; ++i) bad += hits[i].load() != 1;
+    }
+    std::printf("bad %ld\n", bad);
+    return bad != 0;
+}
+'''
+
+
+@pytest.mark.parametrize("tsan", [False, True])
+def test_pool_runs_every_task_once(tmp_path, tsan):
+    """CopyPool::run: 20,000 back-to-back runs of 1-37 tasks on one pool,
+    every task exactly once per run, none after the run returned (its slots
+    live on the caller's stack); also under ThreadSanitizer."""
+    src = tmp_path / "p.cpp"
+    src.write_text(POOL_HARNESS)
+    exe = tmp_path / "p"
+    flags = ["-O1", "-g", "-fsanitize=thread"] if tsan else ["-O2"]
+    r = subprocess.run(["g++", *flags, "-std=c++17", "-pthread", "-I", os.path.join(ROOT, "dips_amd", "csrc"),
+                        str(src), "-o", str(exe)], capture_output=True, text=True)
+    if tsan and r.returncode != 0:
+        pytest.skip("no ThreadSanitizer runtime: " + r.stderr[-200:])
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    out = subprocess.run([str(exe)], capture_output=True, text=True, env=env, timeout=300)
+    if tsan and "FATAL: ThreadSanitizer" in out.stderr:
+        pytest.skip("ThreadSanitizer cannot run here: " + out.stderr[-200:])
+    assert out.returncode == 0, out.stdout + out.stderr[-3000:]
+    assert "bad 0" in out.stdout
