@@ -2,11 +2,12 @@
 """gray_layout_ab.py -- the GRAY8 table kernel's layouts on several contents,
 in one process over one resident batch per content (4K gray8, 3000 frames,
 'per-frame', tau = 8/255): layout 2 (u16 table keyed by (a, b)), layout 3
-(keyed by (a ^ b, a), band clamp), layout 4 (auto: 3 or 2 per launch from a
-sampled band occupancy, the default), alternated over --rounds rounds.
+(keyed by (a ^ b, a), band clamp, swizzled), layout 5 (the same unswizzled),
+layout 4 (the default: 5 or 2 per workgroup from a sample of its own items),
+as listed in LAYOUTS, alternated over ROUNDS rounds.
 Contents: the bench's synthetic clip, i.i.d. uniform random frames, and the
 smooth contents of tools/content_rate.py (flat, gradient, moving).  Kernel
-time from the library's hipEvents (the probe of layout 4 included); the
+time from the library's hipEvents (layout 4's in-kernel sample included); the
 series of every layout must be equal.  One JSON line per (content, layout,
 round).
 """
