@@ -742,6 +742,30 @@ def test_series_starts_from_zero_on_a_dirty_buffer(fmt_name, env, monkeypatch):
             op.close()
 
 
+@pytest.mark.parametrize("fmt_name,n", [("RGB8", 1), ("RGB8", 3), ("Gray8", 2), ("RGBA8", 2)])
+def test_reduce_grid_for_few_large_frames(fmt_name, n):
+    """Few 8K frames: the reduce kernel takes 8 tiles per thread (one round of
+    loads) over a grid of up to 4,050 groups in y (series_kernels.hip
+    launch_series_reduce), the main kernel clears the series -- every frame
+    equal to the oracle, both modes."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    fmt = getattr(PixelFormat, fmt_name)
+    c = int(fmt)
+    frames = _frames(c, 7680, 4320, n, 90 + n, "synth")
+    dev = torch.from_numpy(frames).cuda()
+    for mode in (0, 1):
+        want, _, _ = oracle.series(frames, mode=mode, tau=8 / 255, nthreads=8)
+        op = DiffSeriesOperator(fmt, Mode(mode), 8 / 255, 0)
+        try:
+            ser = torch.full((n, 4), -1, dtype=torch.int64, device="cuda")
+            op.run_device(dev, ser)
+            torch.cuda.synchronize()
+            assert np.array_equal(ser.cpu().numpy().view(np.uint64), want), (fmt_name, n, mode)
+        finally:
+            op.close()
+
+
 @pytest.mark.parametrize("fmt_name,w,h,n", [("RGB8", 1920, 1080, 523), ("RGBA8", 1920, 1080, 525)])
 def test_part_major_overall_matches_contiguous_and_oracle(fmt_name, w, h, n, monkeypatch):
     """'Overall' batches on the part-major schedule (the default since round
