@@ -35,7 +35,9 @@ def main():
     env_of = {"f64": ("DIPS_SERIES_ISI", "0"), "isi": ("DIPS_SERIES_ISI", "1"), "sadi": ("DIPS_SERIES_ISI", "2"),
               "contig": ("DIPS_SERIES_PARTS", "0"), "parts": ("DIPS_SERIES_PARTS", "1"),
               "partsall": ("DIPS_SERIES_PARTS", "2"), "kzero": ("DIPS_SERIES_KZERO", "1"),
-              "fill": ("DIPS_SERIES_KZERO", "0")}
+              "fill": ("DIPS_SERIES_KZERO", "0"),
+              "w5": ("DIPS_SERIES_WAVES_PER_SIMD", "5"), "w4": ("DIPS_SERIES_WAVES_PER_SIMD", "4"),
+              "w3": ("DIPS_SERIES_WAVES_PER_SIMD", "3"), "w2": ("DIPS_SERIES_WAVES_PER_SIMD", "2")}
     frames = torch.empty((F, H, W, 3), dtype=torch.uint8, device="cuda")
     op = DiffSeriesOperator(PixelFormat.RGB8, mode, 8 / 255, time_kernel=True)
     op.synth_device(frames, W, H, 0xD1B5, 0)
@@ -57,6 +59,7 @@ def main():
             os.environ.pop("DIPS_SERIES_ISI", None)
             os.environ.pop("DIPS_SERIES_PARTS", None)
             os.environ.pop("DIPS_SERIES_KZERO", None)
+            os.environ.pop("DIPS_SERIES_WAVES_PER_SIMD", None)
             os.environ[var] = env
             r = None if mode == Mode.PerFrame else ref
             op.run_device(frames, series[name], ref=r)  # warm
@@ -88,6 +91,7 @@ def main():
     os.environ.pop("DIPS_SERIES_ISI", None)
     os.environ.pop("DIPS_SERIES_PARTS", None)
     os.environ.pop("DIPS_SERIES_KZERO", None)
+    os.environ.pop("DIPS_SERIES_WAVES_PER_SIMD", None)
     same = all(bool(torch.equal(series[names[0]], series[k])) for k in names[1:])
     summ = {"summary": True, "size": f"{W}x{H}", "frames": F, "mode": "per-frame" if mode == Mode.PerFrame else "overall", "series_equal": same}
     for k, v in res.items():
