@@ -68,6 +68,7 @@ def parse():
                     help="rank 0 recomputes the series of all N*F frames in one single-device launch "
                          "and requires the gathered series to equal it (functional check of the N>1 path)")
     ap.add_argument("--no-map", action="store_true", help="skip the map_variant measurement")
+    ap.add_argument("--no-tau0", action="store_true", help="skip the tau = 0 leg at the headline shape")
     ap.add_argument("--map-frames", type=int, default=2500,
                     help="frames of the map_variant launch (frames + maps stay resident beside the batch)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -92,17 +93,9 @@ def parse():
 
 
 def _series_isi(tau: float) -> int:
-    """The intensity-sum form run_series_device (dips_abi.hip) picks: 0 (f64
-    sum) below tau = 2^-5 or with DIPS_SERIES_ISI=0, 2 (SADI) with
-    DIPS_SERIES_ISI=2 and tau < 1, else 1 (the integer sum)."""
-    if not tau >= 0.03125:
-        return 0
-    env = os.environ.get("DIPS_SERIES_ISI", "1")[:1]
-    if env == "0":
-        return 0
-    if env == "2" and tau < 1.0:
-        return 2
-    return 1
+    """The intensity-sum form run_series_device (series_abi.hip) picks: 0 (the
+    exact f64 sum) below tau = 2^-5, else 1 (the integer sum)."""
+    return 1 if tau >= 0.03125 else 0
 
 
 def _v2_kernel_name(per_frame: bool, tau: float, with_map: bool = False) -> str:
@@ -297,41 +290,49 @@ def _config0_gpu(torch, frames_host, want):
             "note": "92 MB batch: launch-bound (a 300-frame 640x480 clip is ~0.03 ms of HBM streaming)"}
 
 
-def _start_power(torch, local):
-    """Socket energy / clock / PPT throttling of this rank's GPU over the timed
-    region (tools/power_probe.py's amdsmi reader, read-only queries): one
-    reading right before the timed steps and one right after, so nothing runs
-    beside them; None where amdsmi is unavailable."""
+def _power_sampler(torch, local):
+    """amdsmi reader of this rank's GPU (tools/power_probe.py, read-only
+    queries), not started: legs take one reading right before and one right
+    after themselves (_power_leg), so nothing runs beside them; None where
+    amdsmi is unavailable."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         from power_probe import Sampler
         bus = torch.cuda.get_device_properties(local).pci_bus_id
-        smp = Sampler(pci_bus=bus)  # not started: explicit readings only
-        if len(smp.handles) != 1:
-            return None
-        smp.sample()
-        return smp
+        smp = Sampler(pci_bus=bus)
+        return smp if len(smp.handles) == 1 else None
     except Exception:  # report nothing rather than fail the bench
         return None
 
 
-def _power_report(smp, t0, t1, frames):
+def _power_leg(smp, run, frames, what):
+    """run() between two readings of the socket energy counter, the PPT
+    residency accumulator and the gfx clocks: average W, PPT throttle
+    residency, clock before / after and mJ per frame (`frames` = the frames
+    run() read) of exactly that interval; (run()'s result, report or None)."""
     if smp is None:
-        return None
+        return run(), None
     try:
         smp.sample()
-        g = smp.window(t0 - 1.0, t1 + 1.0)[0]
-        if not g or not g.get("avg_power_W_energy"):
-            return None
-        fps = frames / (t1 - t0)
-        clocks = [r[4] for r in smp.rows if t0 - 1.0 <= r[0] <= t1 + 1.0]
-        return {"avg_W": g["avg_power_W_energy"], "gfxclk_MHz_before_after": clocks,
-                "ppt_throttle_residency": g.get("ppt_residency_frac"),
-                "mJ_per_frame": round(g["avg_power_W_energy"] / fps * 1e3, 4),
-                "source": "amdsmi energy counter and PPT residency accumulator read right before and right after "
-                          "the timed steps, gfx clock at both readings (tools/power_probe.py); DESIGN.md 'the limiter'"}
+        ta = smp.rows[-1][0]
     except Exception:
-        return None
+        return run(), None
+    res = run()
+    try:
+        smp.sample()
+        tb = smp.rows[-1][0]
+        g = smp.window(ta, tb)[0]
+        if not g or not g.get("avg_power_W_energy"):
+            return res, None
+        return res, {"avg_W": g["avg_power_W_energy"],
+                     "gfxclk_MHz_before_after": [r[4] for r in smp.rows if ta <= r[0] <= tb],
+                     "ppt_throttle_residency": g.get("ppt_residency_frac"),
+                     "seconds": round(tb - ta, 3),
+                     "mJ_per_frame": round(g["avg_power_W_energy"] * (tb - ta) / frames * 1e3, 4),
+                     "source": f"amdsmi energy counter and PPT residency accumulator read right before and right "
+                               f"after {what}, gfx clock at both readings (tools/power_probe.py)"}
+    except Exception:
+        return res, None
 
 
 def _map_variant(torch, op_cls, frames, n, W, H, mode_pf, tau):
@@ -375,6 +376,48 @@ def _map_variant(torch, op_cls, frames, n, W, H, mode_pf, tau):
                 "bytes_note": "2*W*H*C per frame: F_t read once + D_t written once (R is the previous frame, "
                               "already in registers)",
                 "series_equals_nomap_run": same, "map_matches_torch": ok}
+    finally:
+        op.close()
+
+
+def _tau0_leg(torch, smp, op_cls, frames, series_hl, mode_pf, tau_hl, steps):
+    """The headline shape at tau = 0 (BASELINE.json configs[2] does not state
+    tau): every pixel with dI > 0 counted, the exact f64 intensity sum
+    (series_v2.hip ISI = 0) instead of the integer sum the headline's tau >=
+    2^-5 admits; `steps` back-to-back launches between power readings.  Checks
+    that need no oracle: SAD and SJ do not depend on tau (equal the headline
+    series), count and SI at tau 0 are >= the headline's for every frame."""
+    from dips_amd import Mode, PixelFormat
+    F = frames.shape[0]
+    fb = frames[0].numel()
+    op = op_cls(PixelFormat.RGB8, Mode.PerFrame if mode_pf else Mode.Overall, 0.0, time_kernel=True)
+    try:
+        ser = torch.zeros((F, 4), dtype=torch.int64, device=frames.device)
+        op.run_device(frames, ser)  # warm
+        torch.cuda.synchronize()
+        op.kernel_time(reset=True)
+
+        def run():
+            t = time.perf_counter()
+            for _ in range(steps):
+                op.run_device(frames, ser)
+            torch.cuda.synchronize()
+            return time.perf_counter() - t
+
+        wall, pw = _power_leg(smp, run, F * steps, f"{steps} back-to-back tau = 0 launches")
+        each = op.kernel_times()
+        a = ser.cpu().numpy().view(np.uint64)
+        b = series_hl.cpu().numpy().view(np.uint64)
+        kms = float(np.median(each))
+        ach = F * fb / (kms / 1e3) / 1e9
+        return {"workload": f"the headline batch at tau = 0 ({'per-frame' if mode_pf else 'overall'})",
+                "kernel": _v2_kernel_name(mode_pf, 0.0), "steps": steps,
+                "frames_per_s": round(F * steps / wall, 1), "kernel_ms_median": round(kms, 4),
+                "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                "power": pw,
+                "sad_sj_equal_headline": bool(np.array_equal(a[:, :2], b[:, :2])),
+                "count_si_ge_headline": bool(np.all(a[:, 2:] >= b[:, 2:])),
+                "note": f"headline tau = {tau_hl:.6g} runs the integer sum (ISI = 1); tau = 0 the f64 sum (ISI = 0)"}
     finally:
         op.close()
 
@@ -700,32 +743,43 @@ def _main(args):
             shard.per_frame_overlapped(frames, ref, series, compute)
         return gather(series)
 
+    smp = _power_sampler(torch, local) if rank == 0 else None
     final = None
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     op.kernel_time(reset=True)
-    if world > 1:
-        dist.barrier()
-    smp = _start_power(torch, local) if rank == 0 else None
-    torch.cuda.synchronize()
-    t = time.perf_counter()
-    tm0 = time.monotonic()
-    for _ in range(args.steps):
-        final = step()
-    torch.cuda.synchronize()
-    tm1 = time.monotonic()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t
-    power = _power_report(smp, tm0, tm1, F * args.steps)
+
+    def timed_steps():
+        # barrier + synchronize on both sides (rank 0's power reading before
+        # this is outside every rank's clock)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        out = None
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return out, time.perf_counter() - t
+
+    (final, elapsed), power = _power_leg(smp, timed_steps, F * args.steps, "the timed steps")
     kms, launches = op.kernel_time()
     each = op.kernel_times()  # one launch per step at N = 1 (two at N > 1 per-frame)
-    # measured read-only ceiling on this GPU, outside the timed region: one
-    # plain stream over the same resident bytes (median of 3)
-    read_ms = float(np.median([op.read_ceiling_ms(frames) for _ in range(3)]))
-    # and with the series kernel's own access shape (tile walk, 12-B vecs)
-    walk_ms = float(np.median([op.read_ceiling_walk_ms(frames) for _ in range(3)]))
+    # measured read-only ceilings on this GPU, outside the timed region, each
+    # as many back-to-back launches as the timed steps ran, between power
+    # readings of its own (does the gap to the ceiling coincide with
+    # throttling the ceiling does not see?): one plain stream over the same
+    # resident bytes, and the series kernel's own access shape (tile walk,
+    # schedule, 12-B vecs, no compute)
+    reps = max(3, args.steps)
+    read_all, read_power = _power_leg(smp, lambda: [op.read_ceiling_ms(frames) for _ in range(reps)], F * reps,
+                                      f"{reps} back-to-back read_ceiling_kernel launches")
+    walk_all, walk_power = _power_leg(smp, lambda: [op.read_ceiling_walk_ms(frames) for _ in range(reps)],
+                                      F * reps, f"{reps} back-to-back read_walk_kernel launches")
+    read_ms, walk_ms = float(np.median(read_all)), float(np.median(walk_all))
     # series-kernel time per step (one launch per step, two when the halo
     # overlap splits a per-frame batch at N > 1)
     tt = torch.tensor([elapsed, kms / args.steps], dtype=torch.float64, device=dev)
@@ -750,7 +804,7 @@ def _main(args):
     achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
     value = world * F * args.steps / elapsed_max
 
-    pcie = mapv = cpu = pfc = None
+    pcie = mapv = cpu = pfc = tau0 = None
     if rank == 0:
         final_np = final.cpu().numpy().view(np.uint64)
         assert final_np.shape == (world * F, 4)
@@ -789,6 +843,13 @@ def _main(args):
             del host
         except Exception as e:  # report, never hide
             pcie = {"skipped": str(e)}
+        if not args.no_tau0:
+            try:
+                tau0 = _tau0_leg(torch, smp, DiffSeriesOperator, frames, series, mode == Mode.PerFrame, args.tau,
+                                 max(3, args.steps))
+                log(f"tau0: frac {tau0['frac']}, power {tau0['power']}")
+            except Exception as e:  # report, never hide
+                tau0 = {"skipped": str(e)}
         if not args.no_map:
             try:
                 mapv = _map_variant(torch, DiffSeriesOperator, frames, min(F, args.map_frames), W, H,
@@ -902,11 +963,15 @@ def _main(args):
                     "frac": round(achieved / (F * fb / (read_ms / 1e3) / 1e9), 4),
                     "kernel": "read_ceiling_kernel: non-temporal 16-B loads, 4 in flight per lane, grid-stride, "
                               "over the same frames (no compute)",
+                    "launches": len(read_all),
+                    "power": read_power,
                     "series_shape": {
                         "achieved": round(F * fb / (walk_ms / 1e3) / 1e9, 1),
                         "frac": round(achieved / (F * fb / (walk_ms / 1e3) / 1e9), 4),
                         "kernel": "read_walk_kernel: the series kernel's tile walk, schedule (part-major for "
-                                  "'per-frame' batches) and vecs over the same frames, no compute",
+                                  "batches of >= 256 frames, either mode) and vecs over the same frames, no compute",
+                        "launches": len(walk_all),
+                        "power": walk_power,
                     },
                 },
                 "algorithmic_bytes_per_launch": algo_bytes,
@@ -917,6 +982,7 @@ def _main(args):
             },
             "cpu_baseline": cpu,
             "power": power,
+            "tau0": tau0,
             "pcie_inclusive": pcie,
             "map_variant": mapv,
             "per_frame_call": pfc,

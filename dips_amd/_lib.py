@@ -23,10 +23,14 @@ DIPS_ERR_STATE = -3
 DIPS_ERR_NOMEM = -4
 DIPS_ERR_CAPACITY = -5
 DIPS_ERR_NODEVICE = -6
+DIPS_ERR_INTERNAL = -7
 
 FLAG_DEVICE_PTRS = 0x1
 FLAG_TIME_KERNEL = 0x2
 FLAG_FORCE_GENERIC = 0x4
+FLAG_CROSSCHECK = 0x8
+FLAG_GRAY_BAND_TABLE = 0x10
+FLAG_GRAY_PAIR_TABLE = 0x20
 
 FMT_GRAY8 = 1
 FMT_RGB8 = 3

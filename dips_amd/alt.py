@@ -143,11 +143,12 @@ class DiPsCompute:
 
     def __init__(self, num_textures: int, textures_width: int, textures_height: int,
                  dips_properties: Optional[DiPsProperties] = None, device: int = 0,
-                 time_kernel: bool = False, force_generic: bool = False):
+                 time_kernel: bool = False, force_generic: bool = False, crosscheck: bool = False):
         self.rows, self.cols = int(textures_width), int(textures_height)
         self.num_textures = int(num_textures)
         self.properties = dips_properties or DiPsProperties()
-        flags = (_lib.FLAG_TIME_KERNEL if time_kernel else 0) | (_lib.FLAG_FORCE_GENERIC if force_generic else 0)
+        flags = ((_lib.FLAG_TIME_KERNEL if time_kernel else 0) | (_lib.FLAG_FORCE_GENERIC if force_generic else 0)
+                 | (_lib.FLAG_CROSSCHECK if crosscheck else 0))
         p = _params(self.properties, num_textures, flags)
         self._host = _AltHandle(p, self.cols, self.rows, device)
         self._dev_flags = flags | _lib.FLAG_DEVICE_PTRS
@@ -247,8 +248,9 @@ class DiPsRunner:
     snapshot / refresh-marker loop, fed frames in pieces of any size."""
 
     def __init__(self, rows: int, cols: int, properties: Optional[DiPsProperties] = None,
-                 refresh_markers: Iterable[int] = (), device: int = 0, num_textures: int = FRAME_COUNT):
-        self.compute = DiPsCompute(num_textures, rows, cols, properties, device)
+                 refresh_markers: Iterable[int] = (), device: int = 0, num_textures: int = FRAME_COUNT,
+                 crosscheck: bool = False):
+        self.compute = DiPsCompute(num_textures, rows, cols, properties, device, crosscheck=crosscheck)
         self.markers = np.ascontiguousarray(np.asarray(list(refresh_markers), dtype=np.uint64))
 
     def __call__(self, frames) -> np.ndarray:

@@ -189,10 +189,12 @@ class ComputeState:
 
     def __init__(self, colorize: bool, spatial_window_size: int, sensitivity: float,
                  filter_type: DiPsFilter, chroma_filter: ChromaFilter, device: int = 0,
-                 time_kernel: bool = False):
+                 time_kernel: bool = False, crosscheck: bool = False):
+        """crosscheck: the plain kernels and transfers (DIPS_FLAG_CROSSCHECK):
+        same outputs, for tests."""
+        flags = (_lib.FLAG_TIME_KERNEL if time_kernel else 0) | (_lib.FLAG_CROSSCHECK if crosscheck else 0)
         self._hd = _Handle(_params(colorize, spatial_window_size, sensitivity, filter_type,
-                                   chroma_filter, fmt=PixelFormat.RGBA8,
-                                   flags=_lib.FLAG_TIME_KERNEL if time_kernel else 0), device)
+                                   chroma_filter, fmt=PixelFormat.RGBA8, flags=flags), device)
         self._dev: Optional[_Handle] = None
         self._w = 0
         self._h = 0
@@ -209,6 +211,9 @@ class ComputeState:
         self._w, self._h = width, height
 
     def dispatch(self) -> Optional[np.ndarray]:
+        """gpu/mod.rs:306-397: None only while the ring warms up (frames
+        0..2); a device or argument error raises DipsError (the reference's
+        wgpu path panics), so None never hides a failure."""
         out = np.empty((self._h, self._w, 4), dtype=np.uint8)
         r = self._hd.check(self._hd._lib.dips_dispatch(self._hd.ptr, out.ctypes.data, out.nbytes))
         return out if r == 1 else None
@@ -318,7 +323,9 @@ class ComputeState:
 
 
 def frame_callback(width: int, height: int, frame_data, compute: ComputeState) -> np.ndarray:
-    """dips/src/lib.rs:233-246 through the C ABI's dips_frame_callback."""
+    """dips/src/lib.rs:233-246 through the C ABI's dips_frame_callback: the
+    visualisation, or the input passed through while the ring warms up; an
+    error raises DipsError instead of passing the input through."""
     a = _as_u8(frame_data)
     out = np.empty((height, width, 4), dtype=np.uint8)
     compute._hd.check(compute._hd._lib.dips_frame_callback(
@@ -408,8 +415,18 @@ class DiffSeriesOperator:
 
     def __init__(self, fmt: PixelFormat = PixelFormat.RGB8, mode: Mode = Mode.Overall,
                  tau: float = 0.0, chroma_filter: ChromaFilter = ChromaFilter.None_,
-                 device: int = 0, time_kernel: bool = False, force_generic: bool = False):
-        flags = (_lib.FLAG_TIME_KERNEL if time_kernel else 0) | (_lib.FLAG_FORCE_GENERIC if force_generic else 0)
+                 device: int = 0, time_kernel: bool = False, force_generic: bool = False,
+                 crosscheck: bool = False, gray_table: str = "auto"):
+        """force_generic: the any-shape kernel; crosscheck: the plain kernels
+        (DIPS_FLAG_CROSSCHECK; GRAY8 f32 kernel, f64 intensity sums);
+        gray_table: "auto" (the GRAY8 table kernel picks its layout per
+        workgroup from the content), "band" or "pair" (pinned,
+        DIPS_FLAG_GRAY_BAND_TABLE / _PAIR_TABLE).  All give the same series."""
+        tables = {"auto": 0, "band": _lib.FLAG_GRAY_BAND_TABLE, "pair": _lib.FLAG_GRAY_PAIR_TABLE}
+        if gray_table not in tables:
+            raise ValueError("gray_table must be 'auto', 'band' or 'pair'")
+        flags = ((_lib.FLAG_TIME_KERNEL if time_kernel else 0) | (_lib.FLAG_FORCE_GENERIC if force_generic else 0)
+                 | (_lib.FLAG_CROSSCHECK if crosscheck else 0) | tables[gray_table])
         self.fmt = PixelFormat(fmt)
         self.mode = Mode(mode)
         self.tau = float(tau)
@@ -536,11 +553,12 @@ class DiffSeriesOperator:
 def diff_series(frames: np.ndarray, *, fmt: Optional[PixelFormat] = None, mode: Mode = Mode.Overall,
                 tau: float = 0.0, chroma_filter: ChromaFilter = ChromaFilter.None_,
                 ref: Optional[np.ndarray] = None, want_map: bool = False, device: int = 0,
-                force_generic: bool = False) -> Tuple[Series, Optional[np.ndarray]]:
+                force_generic: bool = False, crosscheck: bool = False) -> Tuple[Series, Optional[np.ndarray]]:
     """One-shot helper over DiffSeriesOperator for host arrays."""
     if fmt is None:
         fmt = PixelFormat.Gray8 if frames.ndim == 3 else PixelFormat(frames.shape[-1])
-    op = DiffSeriesOperator(fmt, mode, tau, chroma_filter, device, force_generic=force_generic)
+    op = DiffSeriesOperator(fmt, mode, tau, chroma_filter, device, force_generic=force_generic,
+                            crosscheck=crosscheck)
     try:
         return op(frames, ref=ref, want_map=want_map)
     finally:

@@ -2,8 +2,9 @@
 // "dips_alt operator").  The handle plays DiPsCompute
 // (dips_alt/src/dips_compute/mod.rs:243-267: texture slots, texture_index,
 // snapshot texture, output) plus the loop state of run_dips_on_file
-// (dips_alt/src/lib.rs:566-567: index, overall_frame).  No exception leaves
-// this file; every entry point returns a dips_status.
+// (dips_alt/src/lib.rs:566-567: index, overall_frame).  Every extern "C"
+// body runs inside dips_abi::guard (abi_guard.h): no C++ exception leaves
+// the library; every entry point returns a dips_status.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,6 +18,7 @@
 #include <vector>
 
 #include "../../include/dips_hip.h"
+#include "abi_guard.h"
 #include "alt_lut.h"
 #include "dips_kernels.h"
 #include "host_buffers.h"
@@ -168,7 +170,30 @@ struct dips_alt_handle {
 
     size_t frame_bytes() const { return (size_t)width * height * 4u; }
     size_t n_px() const { return (size_t)width * height; }
+    bool crosscheck() const { return (p.flags & DIPS_FLAG_CROSSCHECK) != 0; }
 };
+
+namespace dips_abi {
+
+void note_error(dips_alt_handle* h, const char* msg) noexcept {
+    if (!h) return;
+    try {
+        h->err = msg;
+    } catch (...) {
+    }
+}
+
+void note_error(AltCreateTag, const char* msg) noexcept {
+    try {
+        std::lock_guard<std::mutex> lk(g_alt_err_mu);
+        g_alt_create_err = msg;
+    } catch (...) {
+    }
+}
+
+}  // namespace dips_abi
+
+using dips_abi::guard;
 
 namespace {
 
@@ -300,11 +325,8 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
     const bool pre = prev0 != nullptr;
     const int chroma = pre ? -1 : (int)h->p.chroma_filter;
     const bool fast = dips::alt_fast_epilogue_ok(h->p.filter_type, h->p.sigmoid_horizontal_scalar);
-    // the epilogue-table kernel (default) or the per-pixel arithmetic one
-    // (DIPS_ALT_LUT=0: kept for A/B runs and as a cross-check in the tests)
-    bool lut = true;
-    if (const char* e = std::getenv("DIPS_ALT_LUT"))
-        if (e[0] == '0') lut = false;
+    // the epilogue-table kernel, or the per-pixel arithmetic one (DIPS_FLAG_CROSSCHECK)
+    const bool lut = !h->crosscheck();
     const void* k = lut ? dips::alt_batch_lut_kernel_ptr(chroma)
                         : dips::alt_batch_kernel_ptr(chroma, (int)h->p.filter_type, h->p.colorize != 0, fast);
     if (!k) return fail(h, DIPS_ERR_INVALID, "no batch kernel for these parameters");
@@ -321,7 +343,7 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
         if (st != DIPS_OK) return st;
     }
     const uint64_t n_vec = h->n_px() / 4u;
-    const uint64_t U = lut ? (uint64_t)dips::alt_lut_unroll() : (uint64_t)dips::kUnrollAlt;
+    const uint64_t U = lut ? (uint64_t)dips::kUnrollAltLut : (uint64_t)dips::kUnrollAlt;
     const uint64_t n_tiles = (n_vec + 64u * U - 1) / (64u * U);
     const uint64_t resident = (uint64_t)occ * 4u * (uint64_t)h->cu_count;
     // chunks of >= 16 frames; enough (tile, chunk) items to fill the chip
@@ -415,6 +437,7 @@ dips_status run_fast(dips_alt_handle* h, const uint8_t* frames, uint32_t n, cons
 dips_status run_prefiltered(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags,
                             uint8_t* out, hipStream_t s) {
     const size_t fb = h->frame_bytes();
+    // DIPS_WINDOW_BATCH_FRAMES sets the frames per chunk
     uint64_t g = std::max<uint64_t>(16u, (1ull << 30) / fb);
     if (const char* e = std::getenv("DIPS_WINDOW_BATCH_FRAMES")) g = std::max(1ul, std::strtoul(e, nullptr, 10));
     g = std::min<uint64_t>(std::min<uint64_t>(g, n), 65534u);
@@ -498,229 +521,239 @@ dips_status send_frames_device(dips_alt_handle* h, const uint8_t* frames, uint32
 extern "C" {
 
 dips_status dips_alt_params_default(dips_alt_params* p) {
-    if (!p) return DIPS_ERR_INVALID;
-    std::memset(p, 0, sizeof(*p));
-    p->colorize = 1;
-    p->window_size = 1;
-    p->sigmoid_horizontal_scalar = 5.0f;
-    p->filter_type = DIPS_FILTER_SIGMOID;
-    p->chroma_filter = DIPS_CHROMA_NONE;
-    p->num_textures = (uint32_t)kFrameCount;
-    p->flags = 0;
-    return DIPS_OK;
+    return guard(nullptr, [&]() -> dips_status {
+        if (!p) return DIPS_ERR_INVALID;
+        std::memset(p, 0, sizeof(*p));
+        p->colorize = 1;
+        p->window_size = 1;
+        p->sigmoid_horizontal_scalar = 5.0f;
+        p->filter_type = DIPS_FILTER_SIGMOID;
+        p->chroma_filter = DIPS_CHROMA_NONE;
+        p->num_textures = (uint32_t)kFrameCount;
+        p->flags = 0;
+        return DIPS_OK;
+    });
 }
 
 dips_status dips_alt_create(const dips_alt_params* params, uint32_t width, uint32_t height, int device,
                             dips_alt_handle** out) {
-    if (!out) return DIPS_ERR_INVALID;
-    *out = nullptr;
-    dips_alt_params p;
-    if (params) p = *params;
-    else dips_alt_params_default(&p);
-    std::string why;
-    if (validate(&p, width, height, &why) != DIPS_OK) {
-        std::lock_guard<std::mutex> lk(g_alt_err_mu);
-        g_alt_create_err = why;
-        return DIPS_ERR_INVALID;
-    }
-    int count = 0;
-    hipError_t e = hipGetDeviceCount(&count);
-    if (e != hipSuccess || count <= 0 || device < 0 || device >= count) {
-        std::lock_guard<std::mutex> lk(g_alt_err_mu);
-        g_alt_create_err = std::string("no HIP device ") + std::to_string(device) + " (" +
-                           (e == hipSuccess ? std::to_string(count) + " visible" : hipGetErrorString(e)) + ")";
-        return DIPS_ERR_NODEVICE;
-    }
-    dips_alt_handle* h = new (std::nothrow) dips_alt_handle();
-    if (!h) return DIPS_ERR_NOMEM;
-    h->p = p;
-    h->device = device;
-    h->width = width;
-    h->height = height;
-    e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&h->cu_count, hipDeviceAttributeMultiprocessorCount, device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamDefault);  // blocking: ordered with stream 0 (see dips_set_stream)
-    for (int k = 0; k < 2 && e == hipSuccess; ++k) e = hipEventCreateWithFlags(&h->meta_done[k], hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->meta_free, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventRecord(h->meta_free, h->own_stream);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->meta_stream, hipStreamNonBlocking);
-    // wgpu zero-initialises textures: slots, snapshot and output start at 0
-    for (uint32_t k = 0; k < p.num_textures && e == hipSuccess; ++k) {
-        e = h->slots[k].ensure(h->frame_bytes());
-        if (e == hipSuccess) e = hipMemsetAsync(h->slots[k].p, 0, h->frame_bytes(), h->own_stream);
-    }
-    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
-        e = h->snap[k].ensure(h->n_px());
-        if (e == hipSuccess) e = hipMemsetAsync(h->snap[k].p, 0, h->n_px(), h->own_stream);
-    }
-    if (e == hipSuccess) e = hipStreamSynchronize(h->own_stream);
-    if (e != hipSuccess) {
-        std::lock_guard<std::mutex> lk(g_alt_err_mu);
-        g_alt_create_err = std::string("HIP initialisation failed: ") + hipGetErrorString(e);
-        dips_alt_destroy(h);
-        return e == hipErrorOutOfMemory ? DIPS_ERR_NOMEM : DIPS_ERR_HIP;
-    }
-    h->stream = h->own_stream;
-    *out = h;
-    return DIPS_OK;
+    return guard(dips_abi::AltCreateTag{}, [&]() -> dips_status {
+        if (!out) return DIPS_ERR_INVALID;
+        *out = nullptr;
+        dips_alt_params p;
+        if (params) p = *params;
+        else dips_alt_params_default(&p);
+        std::string why;
+        if (validate(&p, width, height, &why) != DIPS_OK) {
+            std::lock_guard<std::mutex> lk(g_alt_err_mu);
+            g_alt_create_err = why;
+            return DIPS_ERR_INVALID;
+        }
+        int count = 0;
+        hipError_t e = hipGetDeviceCount(&count);
+        if (e != hipSuccess || count <= 0 || device < 0 || device >= count) {
+            std::lock_guard<std::mutex> lk(g_alt_err_mu);
+            g_alt_create_err = std::string("no HIP device ") + std::to_string(device) + " (" +
+                               (e == hipSuccess ? std::to_string(count) + " visible" : hipGetErrorString(e)) + ")";
+            return DIPS_ERR_NODEVICE;
+        }
+        dips_alt_handle* h = new (std::nothrow) dips_alt_handle();
+        if (!h) return DIPS_ERR_NOMEM;
+        h->p = p;
+        h->device = device;
+        h->width = width;
+        h->height = height;
+        e = hipSetDevice(device);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&h->cu_count, hipDeviceAttributeMultiprocessorCount, device);
+        // blocking: ordered with stream 0 (see dips_set_stream)
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own_stream, hipStreamDefault);
+        for (int k = 0; k < 2 && e == hipSuccess; ++k)
+            e = hipEventCreateWithFlags(&h->meta_done[k], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->meta_free, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(h->meta_free, h->own_stream);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->meta_stream, hipStreamNonBlocking);
+        // wgpu zero-initialises textures: slots, snapshot and output start at 0
+        for (uint32_t k = 0; k < p.num_textures && e == hipSuccess; ++k) {
+            e = h->slots[k].ensure(h->frame_bytes());
+            if (e == hipSuccess) e = hipMemsetAsync(h->slots[k].p, 0, h->frame_bytes(), h->own_stream);
+        }
+        for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+            e = h->snap[k].ensure(h->n_px());
+            if (e == hipSuccess) e = hipMemsetAsync(h->snap[k].p, 0, h->n_px(), h->own_stream);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(h->own_stream);
+        if (e != hipSuccess) {
+            {
+                std::lock_guard<std::mutex> lk(g_alt_err_mu);
+                g_alt_create_err = std::string("HIP initialisation failed: ") + hipGetErrorString(e);
+            }
+            dips_alt_destroy(h);
+            return e == hipErrorOutOfMemory ? DIPS_ERR_NOMEM : DIPS_ERR_HIP;
+        }
+        h->stream = h->own_stream;
+        *out = h;
+        return DIPS_OK;
+    });
 }
 
 void dips_alt_destroy(dips_alt_handle* h) {
-    if (!h) return;
-    (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
-    for (auto& pr : h->ev_pending) {
-        (void)hipEventDestroy(pr.first);
-        (void)hipEventDestroy(pr.second);
-    }
-    for (auto e : h->ev_free) (void)hipEventDestroy(e);
-    if (h->meta_stream) (void)hipStreamSynchronize(h->meta_stream);
-    for (auto& ev : h->meta_done)
-        if (ev) (void)hipEventDestroy(ev);
-    if (h->meta_free) (void)hipEventDestroy(h->meta_free);
-    if (h->switch_ev) (void)hipEventDestroy(h->switch_ev);
-    if (h->join_ev) (void)hipEventDestroy(h->join_ev);
-    if (h->meta_stream) (void)hipStreamDestroy(h->meta_stream);
-    for (auto& mp : h->meta_pin) mp.release();
-    for (auto& s : h->slots) s.release();
-    for (auto& s : h->snap) s.release();
-    h->filtered.release();
-    h->lut_l1.release();
-    h->lut_diffs.release();
-    h->lut_slots.release();
-    h->lut_l2.release();
-    h->out1.release();
-    h->pipe.release();
-    h->pieces.release();
-    h->up_pieces.release();
-    h->io_out.release();
-    h->meta.release();
-    h->io.release();
-    if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
-    delete h;
+    guard(h, [&]() -> void {
+        if (!h) return;
+        (void)hipSetDevice(h->device);
+        if (h->stream) (void)hipStreamSynchronize(h->stream);
+        for (auto& pr : h->ev_pending) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+        for (auto e : h->ev_free) (void)hipEventDestroy(e);
+        if (h->meta_stream) (void)hipStreamSynchronize(h->meta_stream);
+        for (auto& ev : h->meta_done)
+            if (ev) (void)hipEventDestroy(ev);
+        if (h->meta_free) (void)hipEventDestroy(h->meta_free);
+        if (h->switch_ev) (void)hipEventDestroy(h->switch_ev);
+        if (h->join_ev) (void)hipEventDestroy(h->join_ev);
+        if (h->meta_stream) (void)hipStreamDestroy(h->meta_stream);
+        for (auto& mp : h->meta_pin) mp.release();
+        for (auto& s : h->slots) s.release();
+        for (auto& s : h->snap) s.release();
+        h->filtered.release();
+        h->lut_l1.release();
+        h->lut_diffs.release();
+        h->lut_slots.release();
+        h->lut_l2.release();
+        h->out1.release();
+        h->pipe.release();
+        h->pieces.release();
+        h->up_pieces.release();
+        h->io_out.release();
+        h->meta.release();
+        h->io.release();
+        if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+        delete h;
+    });
 }
 
 const char* dips_alt_last_error(const dips_alt_handle* h) {
-    if (h) return h->err.c_str();
-    std::lock_guard<std::mutex> lk(g_alt_err_mu);
-    return g_alt_create_err.c_str();
+    return guard(h, [&]() -> const char* {
+        if (h) return h->err.c_str();
+        std::lock_guard<std::mutex> lk(g_alt_err_mu);
+        return g_alt_create_err.c_str();
+    });
 }
 
 dips_status dips_alt_set_stream(dips_alt_handle* h, void* stream) {
-    if (!h) return DIPS_ERR_INVALID;
-    hipStream_t next = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
-    if (next == h->stream) return DIPS_OK;
-    // slots, snapshot and tables serve every stream: work issued on the new
-    // stream waits for all work issued on the old one
-    dips_status st = bind(h);
-    if (st != DIPS_OK) return st;
-    if (!h->switch_ev) ALT_HIP(h, hipEventCreateWithFlags(&h->switch_ev, hipEventDisableTiming));
-    ALT_HIP(h, hipEventRecord(h->switch_ev, h->stream));
-    ALT_HIP(h, hipStreamWaitEvent(next, h->switch_ev, 0));
-    h->stream = next;
-    return DIPS_OK;
+    return guard(h, [&]() -> dips_status {
+        if (!h) return DIPS_ERR_INVALID;
+        hipStream_t next = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+        if (next == h->stream) return DIPS_OK;
+        // slots, snapshot and tables serve every stream: work issued on the new
+        // stream waits for all work issued on the old one
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        if (!h->switch_ev) ALT_HIP(h, hipEventCreateWithFlags(&h->switch_ev, hipEventDisableTiming));
+        ALT_HIP(h, hipEventRecord(h->switch_ev, h->stream));
+        ALT_HIP(h, hipStreamWaitEvent(next, h->switch_ev, 0));
+        h->stream = next;
+        return DIPS_OK;
+    });
 }
 
 dips_status dips_alt_synchronize(dips_alt_handle* h) {
-    dips_status st = bind(h);
-    if (st != DIPS_OK) return st;
-    ALT_HIP(h, hipStreamSynchronize(h->stream));
-    return DIPS_OK;
+    return guard(h, [&]() -> dips_status {
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        ALT_HIP(h, hipStreamSynchronize(h->stream));
+        return DIPS_OK;
+    });
 }
 
 dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t len, int snapshot, uint8_t* out,
                                 size_t cap) {
-    dips_status st = bind(h);
-    if (st != DIPS_OK) return st;
-    const size_t fb = h->frame_bytes();
-    if (!frame || len != fb) return fail(h, DIPS_ERR_INVALID, "send_frame: len != width*height*4 (RGBA8, stride width*4)");
-    if (!out || cap < fb) return fail(h, DIPS_ERR_CAPACITY, "send_frame: output buffer smaller than width*height*4");
-    ALT_HIP(h, h->io.ensure(fb));
-    ALT_HIP(h, h->out1.ensure(fb));
-    ALT_HIP(h, hipStreamSynchronize(h->stream));
-    // queue.write_texture into slot texture_index, then texture_index += 1
-    // (through the pinned buffer in pieces: host copy and DMA overlapped)
-    const uint32_t N = h->p.num_textures;
-    uint8_t* slot = h->slots[h->sent % N].as<uint8_t>();
-    const char* striped_env = std::getenv("DIPS_CALLBACK_STRIPED");  // "0": whole-frame transfers
-    const bool striped = h->p.window_size == 1 && (!striped_env || striped_env[0] != '0');
-    const char* direct_env = std::getenv("DIPS_CALLBACK_DIRECT");
-    const bool direct = !direct_env || direct_env[0] != '0';
-    // W > 1, zero-copy form (default): the stripes go into the slot by copy
-    // kernels as the pool stages them, the frame kernel runs on the whole
-    // frame, and its output comes back by copy kernels into pinned memory,
-    // stripe by stripe, copied out as each lands
-    const bool window_direct = h->p.window_size > 1 && direct && fb % 4u == 0;
-    if (!striped && !window_direct) ALT_HIP(h, dips_host::upload_via(slot, frame, fb, h->io.bytes(), h->stream));
-    h->sent += 1;
-    dips::AltArgs a{};
-    for (uint32_t k = 0; k < N; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
-    a.snap = h->snap[h->cur].as<uint8_t>();
-    a.out = h->out1.as<uint8_t>();
-    a.width = h->width;
-    a.height = h->height;
-    a.n_tex = N;
-    a.window = h->p.window_size;
-    a.chroma = h->p.chroma_filter;
-    a.filter = h->p.filter_type;
-    a.scalar = h->p.sigmoid_horizontal_scalar;
-    a.colorize = h->p.colorize ? 1u : 0u;
-    a.snapshot = snapshot ? 1u : 0u;
-    if (window_direct) {
-        ALT_HIP(h, h->io_out.ensure(fb));
-        ALT_HIP(h, hipStreamSynchronize(h->meta_stream));
-        void *din = nullptr, *dout = nullptr;
-        ALT_HIP(h, hipHostGetDevicePointer(&din, h->io.p, 0));
-        ALT_HIP(h, hipHostGetDevicePointer(&dout, h->io_out.p, 0));
-        const size_t row = (size_t)h->width * 4u;
-        dips_host::DirectGeom g;
-        g.init(h->height, row);
-        const hipStream_t cs[2] = {h->stream, h->meta_stream};
-        const uint8_t* src = static_cast<const uint8_t*>(din);
-        ALT_HIP(h, dips_host::direct_stage_launch(frame, h->io.bytes(), cs, h->device, h->up_pieces, g,
-                                                  [&](uint32_t y0, uint32_t y1, hipStream_t st) {
-                                                      return dips::launch_copy_from_host(src + (size_t)y0 * row,
-                                                                                         slot + (size_t)y0 * row,
-                                                                                         (uint64_t)(y1 - y0) * row, st);
-                                                  }));
-        if (!h->join_ev) ALT_HIP(h, hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
-        ALT_HIP(h, hipEventRecord(h->join_ev, h->meta_stream));
-        ALT_HIP(h, hipStreamWaitEvent(h->stream, h->join_ev, 0));
-        ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
-        ALT_HIP(h, h->pieces.ensure(g.n_s));
-        const uint8_t* o1 = h->out1.as<uint8_t>();
-        uint8_t* dst = static_cast<uint8_t*>(dout);
-        for (uint32_t si = 0; si < g.n_s; ++si) {
-            const size_t o = (size_t)g.y0(si) * row, len = (size_t)(g.y1(si) - g.y0(si)) * row;
-            ALT_HIP(h, dips::launch_copy_to_host(o1 + o, dst + o, len, h->stream));
-            ALT_HIP(h, hipEventRecord(h->pieces.ev[si], h->stream));
+    return guard(h, [&]() -> dips_status {
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        const size_t fb = h->frame_bytes();
+        if (!frame || len != fb)
+            return fail(h, DIPS_ERR_INVALID, "send_frame: len != width*height*4 (RGBA8, stride width*4)");
+        if (!out || cap < fb) return fail(h, DIPS_ERR_CAPACITY, "send_frame: output buffer smaller than width*height*4");
+        ALT_HIP(h, h->io.ensure(fb));
+        ALT_HIP(h, h->out1.ensure(fb));
+        ALT_HIP(h, hipStreamSynchronize(h->stream));
+        // queue.write_texture into slot texture_index, then texture_index += 1
+        const uint32_t N = h->p.num_textures;
+        uint8_t* slot = h->slots[h->sent % N].as<uint8_t>();
+        // the zero-copy forms (W = 1: per pixel in row stripes; W > 1: the
+        // stripes into the slot by copy kernels, the frame kernel on the
+        // whole frame, its output back by copy kernels), or whole-frame DMA
+        // transfers through the pinned buffer (DIPS_FLAG_CROSSCHECK, and
+        // frames of a byte count off a multiple of 4 with W > 1)
+        const bool striped = h->p.window_size == 1 && !h->crosscheck();
+        const bool window_direct = h->p.window_size > 1 && fb % 4u == 0 && !h->crosscheck();
+        if (!striped && !window_direct) ALT_HIP(h, dips_host::upload_via(slot, frame, fb, h->io.bytes(), h->stream));
+        h->sent += 1;
+        dips::AltArgs a{};
+        for (uint32_t k = 0; k < N; ++k) a.slots[k] = h->slots[k].as<uint8_t>();
+        a.snap = h->snap[h->cur].as<uint8_t>();
+        a.out = h->out1.as<uint8_t>();
+        a.width = h->width;
+        a.height = h->height;
+        a.n_tex = N;
+        a.window = h->p.window_size;
+        a.chroma = h->p.chroma_filter;
+        a.filter = h->p.filter_type;
+        a.scalar = h->p.sigmoid_horizontal_scalar;
+        a.colorize = h->p.colorize ? 1u : 0u;
+        a.snapshot = snapshot ? 1u : 0u;
+        if (window_direct) {
+            ALT_HIP(h, h->io_out.ensure(fb));
+            ALT_HIP(h, hipStreamSynchronize(h->meta_stream));
+            void *din = nullptr, *dout = nullptr;
+            ALT_HIP(h, hipHostGetDevicePointer(&din, h->io.p, 0));
+            ALT_HIP(h, hipHostGetDevicePointer(&dout, h->io_out.p, 0));
+            const size_t row = (size_t)h->width * 4u;
+            dips_host::DirectGeom g;
+            g.init(h->height, row);
+            const hipStream_t cs[2] = {h->stream, h->meta_stream};
+            const uint8_t* src = static_cast<const uint8_t*>(din);
+            ALT_HIP(h, dips_host::direct_stage_launch(frame, h->io.bytes(), cs, h->device, h->up_pieces, g,
+                                                      [&](uint32_t y0, uint32_t y1, hipStream_t st) {
+                                                          return dips::launch_copy_from_host(
+                                                              src + (size_t)y0 * row, slot + (size_t)y0 * row,
+                                                              (uint64_t)(y1 - y0) * row, st);
+                                                      }));
+            if (!h->join_ev) ALT_HIP(h, hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+            ALT_HIP(h, hipEventRecord(h->join_ev, h->meta_stream));
+            ALT_HIP(h, hipStreamWaitEvent(h->stream, h->join_ev, 0));
+            ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
+            ALT_HIP(h, h->pieces.ensure(g.n_s));
+            const uint8_t* o1 = h->out1.as<uint8_t>();
+            uint8_t* dst = static_cast<uint8_t*>(dout);
+            for (uint32_t si = 0; si < g.n_s; ++si) {
+                const size_t o = (size_t)g.y0(si) * row, len2 = (size_t)(g.y1(si) - g.y0(si)) * row;
+                ALT_HIP(h, dips::launch_copy_to_host(o1 + o, dst + o, len2, h->stream));
+                ALT_HIP(h, hipEventRecord(h->pieces.ev[si], h->stream));
+            }
+            ALT_HIP(h, dips_host::direct_collect(out, h->io_out.bytes(), h->pieces, g));
+            return DIPS_OK;
         }
-        ALT_HIP(h, dips_host::direct_collect(out, h->io_out.bytes(), h->pieces, g));
-        return DIPS_OK;
-    }
-    if (!striped) {
-        ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
-        // copy_texture_to_buffer + map_async + de-pad (mod.rs:597-643)
-        ALT_HIP(h, dips_host::download_via(out, h->out1.p, fb, h->io.bytes(), h->stream, h->pieces));
-        return DIPS_OK;
-    }
-    // W = 1 (per pixel): ~4 MiB row stripes -- stripe s goes up on the
-    // upload stream, is processed as soon as it has landed and comes back on
-    // the compute stream while stripes s+1.. still go up
-    ALT_HIP(h, h->io_out.ensure(fb));
-    ALT_HIP(h, hipStreamSynchronize(h->meta_stream));  // no upload of an earlier call still reads `io`
-    // zero-copy form (default; DIPS_CALLBACK_DIRECT=0 selects the DMA form
-    // after this block): the kernel reads the staged stripe from pinned host memory,
-    // stores it into the slot and writes its output to pinned host memory;
-    // odd stripes on meta_stream (idle here, synchronised above)
-    if (direct) {
+        if (!striped) {
+            ALT_HIP(h, dips::launch_alt_frame(a, h->stream));
+            // copy_texture_to_buffer + map_async + de-pad (mod.rs:597-643)
+            ALT_HIP(h, dips_host::download_via(out, h->out1.p, fb, h->io.bytes(), h->stream, h->pieces));
+            return DIPS_OK;
+        }
+        // W = 1 (per pixel), zero-copy: ~4 MiB row stripes; the kernel reads
+        // the staged stripe from pinned host memory, stores it into the slot
+        // and writes its output to pinned host memory; odd stripes on
+        // meta_stream (idle once synchronised here)
+        ALT_HIP(h, h->io_out.ensure(fb));
+        ALT_HIP(h, hipStreamSynchronize(h->meta_stream));  // no upload of an earlier call still reads `io`
         void *din = nullptr, *dout = nullptr;
         ALT_HIP(h, hipHostGetDevicePointer(&din, h->io.p, 0));
         ALT_HIP(h, hipHostGetDevicePointer(&dout, h->io_out.p, 0));
         a.out = static_cast<uint8_t*>(dout);
         const uint32_t newest = (uint32_t)((h->sent - 1) % N);
-        const char* one_env = std::getenv("DIPS_DIRECT_STREAMS");  // "1": every stripe on the compute stream
-        const hipStream_t cs[2] = {h->stream, (one_env && one_env[0] == '1') ? h->stream : h->meta_stream};
+        const hipStream_t cs[2] = {h->stream, h->meta_stream};
         ALT_HIP(h, dips_host::run_striped_frame_direct(
                        frame, out, h->height, (size_t)h->width * 4u, h->io.bytes(), h->io_out.bytes(), cs, h->device,
                        h->pieces, [&](uint32_t y0, uint32_t y1, hipStream_t s) {
@@ -729,132 +762,140 @@ dips_status dips_alt_send_frame(dips_alt_handle* h, const uint8_t* frame, size_t
                            return dips::launch_alt_frame_host(a, static_cast<const uint8_t*>(din), slot, newest, s);
                        }));
         return DIPS_OK;
-    }
-    ALT_HIP(h, dips_host::run_striped_frame(frame, out, h->height, (size_t)h->width * 4u, h->io.bytes(),
-                                            h->io_out.bytes(), slot, h->out1.as<uint8_t>(), h->meta_stream,
-                                            h->stream, h->up_pieces, h->pieces, [&](uint32_t y0, uint32_t y1) {
-                                                a.y0 = y0;
-                                                a.y1 = y1;
-                                                return dips::launch_alt_frame(a, h->stream);
-                                            }));
-    return DIPS_OK;
+    });
 }
 
 dips_status dips_alt_send_frames(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint8_t* flags,
                                  uint8_t* out) {
-    dips_status st = bind(h);
-    if (st != DIPS_OK) return st;
-    if (n == 0) return DIPS_OK;
-    if (!frames || !out) return fail(h, DIPS_ERR_INVALID, "send_frames: null frames or output");
-    if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) return send_frames_device(h, frames, n, flags, out, h->stream);
-    // host frames: pipelined upload / batch kernel / download in chunks
-    const size_t fb = h->frame_bytes();
-    const uint64_t chunk = dips_host::feed_chunk_frames(fb);
-    uint64_t done = 0;
-    int fst = 0;
-    ALT_HIP(h, dips_host::run_stream_pipe(
-                   h->pipe, h->stream, n, fb, fb, chunk, frames, out,
-                   [&](const uint8_t* din, uint8_t* dout, uint64_t m) {
-                       const int r = (int)send_frames_device(h, din, (uint32_t)m, flags ? flags + done : nullptr,
-                                                             dout, h->stream);
-                       done += m;
-                       return r;
-                   },
-                   &fst));
-    if (fst < 0) return (dips_status)fst;
-    ALT_HIP(h, hipStreamSynchronize(h->stream));
-    return DIPS_OK;
+    return guard(h, [&]() -> dips_status {
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        if (n == 0) return DIPS_OK;
+        if (!frames || !out) return fail(h, DIPS_ERR_INVALID, "send_frames: null frames or output");
+        if (h->p.flags & DIPS_FLAG_DEVICE_PTRS) return send_frames_device(h, frames, n, flags, out, h->stream);
+        // host frames: pipelined upload / batch kernel / download in chunks
+        const size_t fb = h->frame_bytes();
+        const uint64_t chunk = dips_host::feed_chunk_frames(fb, n);
+        uint64_t done = 0;
+        int fst = 0;
+        ALT_HIP(h, dips_host::run_stream_pipe(
+                       h->pipe, h->stream, n, fb, fb, chunk, frames, out,
+                       [&](const uint8_t* din, uint8_t* dout, uint64_t m) {
+                           const int r = (int)send_frames_device(h, din, (uint32_t)m, flags ? flags + done : nullptr,
+                                                                 dout, h->stream);
+                           done += m;
+                           return r;
+                       },
+                       &fst));
+        if (fst < 0) return (dips_status)fst;
+        ALT_HIP(h, hipStreamSynchronize(h->stream));
+        return DIPS_OK;
+    });
 }
 
 dips_status dips_alt_run(dips_alt_handle* h, const uint8_t* frames, uint32_t n, const uint64_t* markers,
                          uint32_t n_markers, uint8_t* out) {
-    if (!h) return DIPS_ERR_INVALID;
-    if (n_markers && !markers) return fail(h, DIPS_ERR_INVALID, "run: null refresh markers");
-    std::vector<uint8_t> flags(n);
-    for (uint32_t t = 0; t < n; ++t) {
-        flags[t] = h->index == kFrameCount ? 1 : 0;  // match index { FRAME_COUNT => Some(()) } (lib.rs:636-639)
-        if (h->index <= kFrameCount) h->index += 1;  // lib.rs:662-664
-        h->overall += 1;                             // lib.rs:666
-        for (uint32_t k = 0; k < n_markers; ++k)     // refresh_markers.contains (lib.rs:668-670)
-            if (markers[k] == h->overall) {
-                h->index = 0;
-                break;
-            }
-    }
-    return dips_alt_send_frames(h, frames, n, flags.data(), out);
+    return guard(h, [&]() -> dips_status {
+        if (!h) return DIPS_ERR_INVALID;
+        if (n_markers && !markers) return fail(h, DIPS_ERR_INVALID, "run: null refresh markers");
+        std::vector<uint8_t> flags(n);
+        for (uint32_t t = 0; t < n; ++t) {
+            flags[t] = h->index == kFrameCount ? 1 : 0;  // match index { FRAME_COUNT => Some(()) } (lib.rs:636-639)
+            if (h->index <= kFrameCount) h->index += 1;  // lib.rs:662-664
+            h->overall += 1;                             // lib.rs:666
+            for (uint32_t k = 0; k < n_markers; ++k)     // refresh_markers.contains (lib.rs:668-670)
+                if (markers[k] == h->overall) {
+                    h->index = 0;
+                    break;
+                }
+        }
+        return dips_alt_send_frames(h, frames, n, flags.data(), out);
+    });
 }
 
 dips_status dips_alt_snapshot_texture(dips_alt_handle* h, uint8_t* out, size_t cap) {
-    dips_status st = bind(h);
-    if (st != DIPS_OK) return st;
-    if (!out || cap < h->n_px()) return fail(h, DIPS_ERR_CAPACITY, "snapshot_texture: output smaller than width*height");
-    ALT_HIP(h, hipMemcpyAsync(out, h->snap[h->cur].p, h->n_px(), hipMemcpyDeviceToHost, h->stream));
-    ALT_HIP(h, hipStreamSynchronize(h->stream));
-    return DIPS_OK;
+    return guard(h, [&]() -> dips_status {
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        if (!out || cap < h->n_px())
+            return fail(h, DIPS_ERR_CAPACITY, "snapshot_texture: output smaller than width*height");
+        ALT_HIP(h, hipMemcpyAsync(out, h->snap[h->cur].p, h->n_px(), hipMemcpyDeviceToHost, h->stream));
+        ALT_HIP(h, hipStreamSynchronize(h->stream));
+        return DIPS_OK;
+    });
 }
 
 dips_status dips_alt_kernel_time(dips_alt_handle* h, double* total_ms, uint64_t* launches) {
-    dips_status st = bind(h);
-    if (st != DIPS_OK) return st;
-    for (auto& pr : h->ev_pending) {
-        ALT_HIP(h, hipEventSynchronize(pr.second));
-        float ms = 0.0f;
-        ALT_HIP(h, hipEventElapsedTime(&ms, pr.first, pr.second));
-        h->t_ms += ms;
-        h->t_launches += 1;
-        h->ev_free.push_back(pr.first);
-        h->ev_free.push_back(pr.second);
-    }
-    h->ev_pending.clear();
-    if (total_ms) *total_ms = h->t_ms;
-    if (launches) *launches = h->t_launches;
-    return DIPS_OK;
+    return guard(h, [&]() -> dips_status {
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        for (auto& pr : h->ev_pending) {
+            ALT_HIP(h, hipEventSynchronize(pr.second));
+            float ms = 0.0f;
+            ALT_HIP(h, hipEventElapsedTime(&ms, pr.first, pr.second));
+            h->t_ms += ms;
+            h->t_launches += 1;
+            h->ev_free.push_back(pr.first);
+            h->ev_free.push_back(pr.second);
+        }
+        h->ev_pending.clear();
+        if (total_ms) *total_ms = h->t_ms;
+        if (launches) *launches = h->t_launches;
+        return DIPS_OK;
+    });
 }
 
 dips_status dips_alt_kernel_time_reset(dips_alt_handle* h) {
-    dips_status st = dips_alt_kernel_time(h, nullptr, nullptr);
-    if (st != DIPS_OK) return st;
-    h->t_ms = 0.0;
-    h->t_launches = 0;
-    return DIPS_OK;
+    return guard(h, [&]() -> dips_status {
+        dips_status st = dips_alt_kernel_time(h, nullptr, nullptr);
+        if (st != DIPS_OK) return st;
+        h->t_ms = 0.0;
+        h->t_launches = 0;
+        return DIPS_OK;
+    });
 }
 
 dips_status dips_alt_lut_index(uint32_t* l1, uint32_t l1_cap, float* diffs, uint16_t* slots, uint32_t cap,
                                uint32_t* n_diffs, uint32_t* l2_entries) {
-    const dips::AltLutIndex& ix = dips::alt_lut_index();
-    if (n_diffs) *n_diffs = (uint32_t)ix.diffs.size();
-    if (l2_entries) *l2_entries = ix.l2_entries;
-    if (l1) {
-        if (l1_cap < 2u * dips::kAltLutClusters) return DIPS_ERR_CAPACITY;
-        std::memcpy(l1, ix.l1, sizeof(ix.l1));
-    }
-    if (diffs || slots) {
-        if (cap < ix.diffs.size()) return DIPS_ERR_CAPACITY;
-        if (diffs) std::memcpy(diffs, ix.diffs.data(), ix.diffs.size() * sizeof(float));
-        if (slots) std::memcpy(slots, ix.slots.data(), ix.slots.size() * sizeof(uint16_t));
-    }
-    return DIPS_OK;
+    return guard(nullptr, [&]() -> dips_status {
+        const dips::AltLutIndex& ix = dips::alt_lut_index();
+        if (n_diffs) *n_diffs = (uint32_t)ix.diffs.size();
+        if (l2_entries) *l2_entries = ix.l2_entries;
+        if (l1) {
+            if (l1_cap < 2u * dips::kAltLutClusters) return DIPS_ERR_CAPACITY;
+            std::memcpy(l1, ix.l1, sizeof(ix.l1));
+        }
+        if (diffs || slots) {
+            if (cap < ix.diffs.size()) return DIPS_ERR_CAPACITY;
+            if (diffs) std::memcpy(diffs, ix.diffs.data(), ix.diffs.size() * sizeof(float));
+            if (slots) std::memcpy(slots, ix.slots.data(), ix.slots.size() * sizeof(uint16_t));
+        }
+        return DIPS_OK;
+    });
 }
 
 dips_status dips_alt_lut_selfcheck(dips_alt_handle* h, uint64_t* mismatches) {
-    dips_status st = bind(h);
-    if (st != DIPS_OK) return st;
-    if (!mismatches) return fail(h, DIPS_ERR_INVALID, "lut_selfcheck: null argument");
-    st = ensure_lut(h, h->stream);
-    if (st != DIPS_OK) return st;
-    DevBuf bad;
-    ALT_HIP(h, bad.ensure(sizeof(unsigned long long)));
-    ALT_HIP(h, hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), h->stream));
-    const hipError_t e = dips::launch_alt_lut_check(h->lut_l1.as<uint32_t>(), h->lut_l2.as<uint16_t>(),
-                                                    h->p.filter_type, h->p.sigmoid_horizontal_scalar,
-                                                    h->p.colorize != 0, bad.as<unsigned long long>(), h->stream);
-    unsigned long long n = 0;
-    hipError_t e2 = e == hipSuccess ? hipMemcpyAsync(&n, bad.p, sizeof(n), hipMemcpyDeviceToHost, h->stream) : e;
-    if (e2 == hipSuccess) e2 = hipStreamSynchronize(h->stream);
-    bad.release();
-    if (e2 != hipSuccess) return hip_fail(h, e2, "lut_selfcheck");
-    *mismatches = n;
-    return DIPS_OK;
+    return guard(h, [&]() -> dips_status {
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        if (!mismatches) return fail(h, DIPS_ERR_INVALID, "lut_selfcheck: null argument");
+        st = ensure_lut(h, h->stream);
+        if (st != DIPS_OK) return st;
+        DevBuf bad;
+        ALT_HIP(h, bad.ensure(sizeof(unsigned long long)));
+        ALT_HIP(h, hipMemsetAsync(bad.p, 0, sizeof(unsigned long long), h->stream));
+        const hipError_t e = dips::launch_alt_lut_check(h->lut_l1.as<uint32_t>(), h->lut_l2.as<uint16_t>(),
+                                                        h->p.filter_type, h->p.sigmoid_horizontal_scalar,
+                                                        h->p.colorize != 0, bad.as<unsigned long long>(), h->stream);
+        unsigned long long n = 0;
+        hipError_t e2 =
+            e == hipSuccess ? hipMemcpyAsync(&n, bad.p, sizeof(n), hipMemcpyDeviceToHost, h->stream) : e;
+        if (e2 == hipSuccess) e2 = hipStreamSynchronize(h->stream);
+        bad.release();
+        if (e2 != hipSuccess) return hip_fail(h, e2, "lut_selfcheck");
+        *mismatches = n;
+        return DIPS_OK;
+    });
 }
 
 }  // extern "C"

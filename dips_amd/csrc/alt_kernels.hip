@@ -500,26 +500,7 @@ static const void* alt_lut_ptr(int chroma) {
     }
 }
 
-int alt_lut_variant() {
-    // DIPS_ALT_LUT_VARIANT = "<U><D>" (A/B runs): 22, 23, 33, 42, 43
-    if (const char* e = std::getenv("DIPS_ALT_LUT_VARIANT")) {
-        const int v = std::atoi(e);
-        if (v == 22 || v == 23 || v == 33 || v == 42 || v == 43) return v;
-    }
-    return 10 * kUnrollAltLut + kDepthAltLut;
-}
-
-int alt_lut_unroll() { return alt_lut_variant() / 10; }
-
-const void* alt_batch_lut_kernel_ptr(int chroma) {
-    switch (alt_lut_variant()) {
-        case 23: return alt_lut_ptr<2, 3>(chroma);
-        case 33: return alt_lut_ptr<3, 3>(chroma);
-        case 42: return alt_lut_ptr<4, 2>(chroma);
-        case 43: return alt_lut_ptr<4, 3>(chroma);
-        default: return alt_lut_ptr<2, 2>(chroma);
-    }
-}
+const void* alt_batch_lut_kernel_ptr(int chroma) { return alt_lut_ptr<kUnrollAltLut, kDepthAltLut>(chroma); }
 
 hipError_t launch_alt_batch_lut(const AltBatchArgs& a, int chroma, uint32_t blocks, hipStream_t s) {
     const void* k = alt_batch_lut_kernel_ptr(chroma);

@@ -407,27 +407,7 @@ static const void* cbl_ptr(int chroma) {
     }
 }
 
-int compat_lut_variant() {
-    // DIPS_COMPAT_LUT_VARIANT = "<U><D>" (A/B runs): 22, 23, 33, 42, 43, 44
-    if (const char* e = std::getenv("DIPS_COMPAT_LUT_VARIANT")) {
-        const int v = std::atoi(e);
-        if (v == 22 || v == 23 || v == 42 || v == 43 || v == 33 || v == 44) return v;
-    }
-    return 10 * kUnrollCompatLut + kDepthCompatLut;
-}
-
-int compat_lut_unroll() { return compat_lut_variant() / 10; }
-
-const void* compat_batch_lut_kernel_ptr(int chroma) {
-    switch (compat_lut_variant()) {
-        case 23: return cbl_ptr<2, 3>(chroma);
-        case 42: return cbl_ptr<4, 2>(chroma);
-        case 43: return cbl_ptr<4, 3>(chroma);
-        case 33: return cbl_ptr<3, 3>(chroma);
-        case 44: return cbl_ptr<4, 4>(chroma);
-        default: return cbl_ptr<2, 2>(chroma);
-    }
-}
+const void* compat_batch_lut_kernel_ptr(int chroma) { return cbl_ptr<kUnrollCompatLut, kDepthCompatLut>(chroma); }
 
 hipError_t launch_compat_lut(uint16_t* lut, uint32_t filter, float k, bool colorize, hipStream_t s) {
     hipLaunchKernelGGL(compat_lut_kernel, dim3(256), dim3(256), 0, s, lut, filter, k, colorize ? 1u : 0u);

@@ -210,47 +210,6 @@ __global__ __launch_bounds__(256) void compat_main_host_kernel(CompatArgs a) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The same, two pixels per thread (out_key 1 / 2 only): one 8-byte
-// system-scope load of the pair's RGBA8 texels and one 2- / 4-byte store of
-// their keys per thread, over the absolute pixel pairs (2k, 2k + 1) that the
-// rows [y0, y1) touch, so every full pair is naturally aligned; a pair cut by
-// the range's ends (odd y0 * width or y1 * width) does its pixel alone.
-// Wider host reads per thread (the host copy kernels' 8-byte words reach the
-// DMA rate, host_stream.h pipe_h2d).
-template <int SLOT_MODE>
-__global__ __launch_bounds__(256) void compat_main_host2_kernel(CompatArgs a) {
-    const uint32_t yend = a.y1 ? a.y1 : a.height;
-    const uint64_t p0 = (uint64_t)a.y0 * a.width, p1 = (uint64_t)yend * a.width;
-    const uint64_t q = (p0 & ~1ull) + 2u * ((uint64_t)blockIdx.x * 256u + threadIdx.x);  // even pixel
-    if (q >= p1) return;
-    if (q >= p0 && q + 2u <= p1) {
-        const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a.raw + 4 * q), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint32_t v0 = (uint32_t)v, v1 = (uint32_t)(v >> 32);
-        const uint32_t t0 =
-            compat_texel(a, q, intensity_rgb(v0 & 0xFFu, (v0 >> 8) & 0xFFu, (v0 >> 16) & 0xFFu, a.chroma), SLOT_MODE, v0);
-        const uint32_t t1 = compat_texel(a, q + 1, intensity_rgb(v1 & 0xFFu, (v1 >> 8) & 0xFFu, (v1 >> 16) & 0xFFu, a.chroma),
-                                         SLOT_MODE, v1);
-        if (a.out_key == 1u)
-            __hip_atomic_store(reinterpret_cast<uint16_t*>(a.out + q), (uint16_t)((t0 & 0xFFu) | ((t1 & 0xFFu) << 8)),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        else
-            __hip_atomic_store(reinterpret_cast<uint32_t*>(a.out + 2 * q), (t0 & 0xFFFFu) | (t1 << 16),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
-    }
-    const uint64_t p = q >= p0 ? q : q + 1u;  // the one pixel of a cut pair inside [p0, p1)
-    const uint32_t v = __hip_atomic_load(reinterpret_cast<const uint32_t*>(a.raw + 4 * p), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t texel =
-        compat_texel(a, p, intensity_rgb(v & 0xFFu, (v >> 8) & 0xFFu, (v >> 16) & 0xFFu, a.chroma), SLOT_MODE, v);
-    if (a.out_key == 1u)
-        __hip_atomic_store(a.out + p, (uint8_t)texel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else
-        __hip_atomic_store(reinterpret_cast<uint16_t*>(a.out + 2 * p), (uint16_t)texel, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // The same from the packed input (in_key 1 / 2, pack_frame): a pixel is its
 // chroma channel v, or its (max, min) of R, G, B, which is all get_intensity
 // reads (dips_shader.wgsl:64-82): the intensity of (max, min, min) equals the
@@ -521,19 +480,6 @@ hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, int slot_
         const uint64_t groups = (p1 + G - 1) / G - p0 / G;
         const dim3 gp((uint32_t)((groups + 255) / 256));
         return launch_packed(a, gp, s, slot_mode);
-    }
-    if (a.out_key != 0u && a.host_pairs != 0u) {
-        // two pixels per thread over the absolute pixel pairs the rows touch
-        const uint64_t p0 = (uint64_t)a.y0 * a.width, p1 = (uint64_t)yend * a.width;
-        const uint64_t pairs = (p1 + 1) / 2 - p0 / 2;
-        const dim3 g2((uint32_t)((pairs + 255) / 256));
-        switch (slot_mode) {
-            case kSlotQ: hipLaunchKernelGGL(compat_main_host2_kernel<kSlotQ>, g2, dim3(256), 0, s, a); break;
-            case kSlotRaw: hipLaunchKernelGGL(compat_main_host2_kernel<kSlotRaw>, g2, dim3(256), 0, s, a); break;
-            case kSlotNone: hipLaunchKernelGGL(compat_main_host2_kernel<kSlotNone>, g2, dim3(256), 0, s, a); break;
-            default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
     }
     const dim3 grid((uint32_t)((n_px + 255) / 256));
     switch (slot_mode) {

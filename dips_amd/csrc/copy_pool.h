@@ -10,11 +10,17 @@
 // handles are not internally synchronised, but different handles may be
 // driven from different threads.  A child process created by fork() gets a
 // fresh pool (the parent's workers do not exist there).
+//
+// Failure model: a worker that cannot be started (std::thread throws
+// std::system_error on EAGAIN -- a thread or process limit) is simply not
+// there: the pool runs with the workers it got, down to none, where the
+// calling thread runs every task itself.  A task that throws does not end its
+// worker: the first exception is kept and rethrown on the calling thread
+// when the run is over, where the ABI guard (abi_guard.h) turns it into a
+// status.
 #pragma once
 
 #include <immintrin.h>
-#include <pthread.h>
-#include <sched.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -25,10 +31,10 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
-#include <fstream>
+#include <exception>
 #include <functional>
-#include <string>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -37,7 +43,14 @@ namespace dips_host {
 class CopyPool {
    public:
     explicit CopyPool(unsigned workers) {
-        for (unsigned i = 0; i < workers; ++i) th_.emplace_back([this]() { loop(); });
+        th_.reserve(workers);  // emplace_back below never reallocates
+        for (unsigned i = 0; i < workers; ++i) {
+            try {
+                th_.emplace_back([this]() { loop(); });
+            } catch (const std::system_error&) {
+                break;  // no more threads: keep the ones started
+            }
+        }
     }
     ~CopyPool() {
         {
@@ -52,50 +65,29 @@ class CopyPool {
 
     unsigned threads() const { return (unsigned)th_.size() + 1u; }
 
-    // Pin the workers to the CPUs of NUMA node `node` that this process may
-    // use (the calling thread is left alone).  Returns the CPU count pinned
-    // to, 0 if the node's CPU list is unreadable or disjoint from the
-    // process's affinity (nothing changed then).
-    unsigned pin_workers_to_node(int node) {
-        std::ifstream f("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
-        std::string list;
-        if (node < 0 || !(f >> list)) return 0;
-        cpu_set_t allowed, set;
-        CPU_ZERO(&set);
-        if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return 0;
-        unsigned n = 0;
-        size_t pos = 0;
-        while (pos < list.size()) {
-            const size_t comma = list.find(',', pos);
-            const std::string r = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
-            const size_t dash = r.find('-');
-            const long a = std::strtol(r.c_str(), nullptr, 10);
-            const long b = dash == std::string::npos ? a : std::strtol(r.c_str() + dash + 1, nullptr, 10);
-            for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
-                if (c >= 0 && CPU_ISSET(c, &allowed)) {
-                    CPU_SET(c, &set);
-                    ++n;
-                }
-            if (comma == std::string::npos) break;
-            pos = comma + 1;
-        }
-        if (n == 0) return 0;
-        for (auto& t : th_) pthread_setaffinity_np(t.native_handle(), sizeof set, &set);
-        return n;
-    }
-
     // fn(i) for every i in [0, n), spread over the workers and the caller.
-    void run(size_t n, const std::function<void(size_t)>& fn) {
+    // With `spin`, the workers watch for the next run for kSpinUs after this
+    // one before parking (the per-frame pipelines: back-to-back calls).
+    void run(size_t n, const std::function<void(size_t)>& fn, bool spin = false) {
         if (n == 0) return;
         std::lock_guard<std::mutex> one_run(run_mu_);
         if (n == 1 || th_.empty()) {
-            for (size_t i = 0; i < n; ++i) fn(i);
+            std::exception_ptr ex;  // the same semantics as with workers: every task runs
+            for (size_t i = 0; i < n; ++i) {
+                try {
+                    fn(i);
+                } catch (...) {
+                    if (!ex) ex = std::current_exception();
+                }
+            }
+            if (ex) std::rethrow_exception(ex);
             return;
         }
         {
             std::lock_guard<std::mutex> lk(mu_);
             fn_ = &fn;
             n_ = n;
+            spin_ = spin;
             next_.store(0, std::memory_order_relaxed);
             busy_ = (unsigned)th_.size();
             ++gen_;
@@ -103,9 +95,14 @@ class CopyPool {
         }
         cv_.notify_all();
         drain(fn, n);
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this]() { return busy_ == 0; });
-        fn_ = nullptr;
+        std::exception_ptr ex;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            done_cv_.wait(lk, [this]() { return busy_ == 0; });
+            fn_ = nullptr;
+            std::swap(ex, ex_);
+        }
+        if (ex) std::rethrow_exception(ex);
     }
 
     // The process-wide pool: min(8, hardware threads) - 1 workers.
@@ -132,19 +129,28 @@ class CopyPool {
 
    private:
     void drain(const std::function<void(size_t)>& fn, size_t n) {
-        for (size_t i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) fn(i);
+        for (size_t i = next_.fetch_add(1); i < n; i = next_.fetch_add(1)) {
+            try {
+                fn(i);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (!ex_) ex_ = std::current_exception();
+            }
+        }
     }
     void loop() {
         uint64_t seen = 0;
-        // After a run, watch for the next one for 200 us before parking on the
-        // condition variable: back-to-back per-frame calls then find the
-        // workers awake on warm cores.  Measured over four alternated rounds
-        // of 200 4K frame_callback calls (tools/pfc_threads_ab.py,
+        bool spin = false;  // the last run asked for the spin
+        // After a per-frame run, watch for the next one for 200 us before
+        // parking on the condition variable: back-to-back per-frame calls then
+        // find the workers awake on warm cores.  Measured over four alternated
+        // rounds of 200 4K frame_callback calls (tools/pfc_threads_ab.py,
         // profiles/r04/k/): 1,689-1,837 frames/s (p90 0.56-0.63 ms) against
         // 1,363-1,687 (p90 0.61-0.88 ms) parking at once; the pool's own
         // pack / expand thread time drops too (1.6-1.8 vs 1.9-2.5 ms per
         // call).  Costs <= 200 us of each worker's time per call when calls
-        // are sparse.  DIPS_POOL_SPIN_US overrides it (0: park at once).
+        // are sparse; batch copies (pool_copy) never spin.
+        // DIPS_POOL_SPIN_US overrides the 200 us (0: park at once).
         static const long spin_us = []() {
             const char* e = std::getenv("DIPS_POOL_SPIN_US");
             const long v = e ? std::strtol(e, nullptr, 10) : 200;
@@ -153,7 +159,7 @@ class CopyPool {
         for (;;) {
             const std::function<void(size_t)>* fn;
             size_t n;
-            if (spin_us > 0 && seen != 0) {
+            if (spin_us > 0 && spin) {
                 const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us);
                 while (gen_seen_.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() < until)
                     _mm_pause();
@@ -165,6 +171,7 @@ class CopyPool {
                 seen = gen_;
                 fn = fn_;
                 n = n_;
+                spin = spin_;
             }
             drain(*fn, n);
             {
@@ -179,6 +186,8 @@ class CopyPool {
     std::condition_variable cv_, done_cv_;
     const std::function<void(size_t)>* fn_ = nullptr;
     size_t n_ = 0;
+    bool spin_ = false;
+    std::exception_ptr ex_;  // the run's first task exception (under mu_)
     std::atomic<size_t> next_{0};
     unsigned busy_ = 0;
     uint64_t gen_ = 0;
@@ -211,21 +220,11 @@ __attribute__((target("avx2"))) inline void stream_copy_avx2(uint8_t* d, const u
     _mm_sfence();
 }
 
-// Whether the staging copies use streaming stores: DIPS_NT_COPY=0 selects
-// memcpy.  Read on the CALLING thread once per operation (so one process can
-// A/B the two, tools/callback_rate.py) and handed to the pool's workers as a
-// value -- the workers never touch the environment, which another thread may
-// be changing (setenv is not safe beside a concurrent getenv).
-inline bool nt_copy() {
-    const char* e = std::getenv("DIPS_NT_COPY");
-    return !(e && e[0] == '0');
-}
-
 // The staging copy: streaming stores for pieces of >= 64 KiB on CPUs with
-// AVX2 when `nt`, memcpy otherwise.
-inline void host_copy(uint8_t* dst, const uint8_t* src, size_t bytes, bool nt) {
+// AVX2, memcpy otherwise.
+inline void host_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
     static const bool avx2 = __builtin_cpu_supports("avx2");
-    if (avx2 && nt && bytes >= (64u << 10))
+    if (avx2 && bytes >= (64u << 10))
         stream_copy_avx2(dst, src, bytes);
     else
         std::memcpy(dst, src, bytes);
@@ -377,15 +376,14 @@ inline void pack_frame(uint8_t* dst, const uint8_t* src, size_t npx, int in_byte
 // Host copy in ~4 MiB pieces over the pool.
 inline void pool_copy(uint8_t* dst, const uint8_t* src, size_t bytes) {
     const size_t kPiece = 4u << 20;
-    const bool nt = nt_copy();
     if (bytes < 2 * kPiece) {
-        host_copy(dst, src, bytes, nt);
+        host_copy(dst, src, bytes);
         return;
     }
     const size_t n = (bytes + kPiece - 1) / kPiece;
     CopyPool::global().run(n, [&](size_t i) {
         const size_t o = i * kPiece;
-        host_copy(dst + o, src + o, std::min(kPiece, bytes - o), nt);
+        host_copy(dst + o, src + o, std::min(kPiece, bytes - o));
     });
 }
 

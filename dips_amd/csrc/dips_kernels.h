@@ -20,20 +20,10 @@ constexpr int kUnrollV2 = 4;    // series_v2_kernel (RGB8/RGBA8): 1024 px / wave
 #define DIPS_UNROLL_GRAY_LUT 4
 #endif
 constexpr int kUnrollGrayLut = DIPS_UNROLL_GRAY_LUT;
-int gray_lut_unroll();  // U of this call's GRAY8 table kernel (DIPS_GRAY_LUT_U for A/B runs)
-// Arithmetic vecs of the U = 4 table kernel for tau >= 2^-5 (series_gray.hip)
-#ifndef DIPS_GRAY_ALU_VECS
-#define DIPS_GRAY_ALU_VECS 0
-#endif
-constexpr int kGrayAluVecs = DIPS_GRAY_ALU_VECS;
-#ifndef DIPS_GRAY_ALU_WAVES
-#define DIPS_GRAY_ALU_WAVES 12
-#endif
-constexpr uint32_t kGrayAluWaves = DIPS_GRAY_ALU_WAVES;
 constexpr uint32_t kGrayLutWaves = 16;  // its waves per workgroup (one 1024-thread group per CU)
 constexpr size_t kGrayLutBytes = 131072;  // its T_d / T_c tables
-constexpr size_t kGrayLutAllocBytes = kGrayLutBytes + 256;  // + layout 3's band word (series_gray.hip)
-// layout 4 (auto) keeps layout 3's table + band word and layout 2's after it
+constexpr size_t kGrayLutAllocBytes = kGrayLutBytes + 256;  // + layout 5's band word (series_gray.hip)
+// layout 4 (auto) keeps layout 5's table + band word and layout 2's after it
 // Prefetch depth: frames of loads each wave keeps in flight.
 #ifndef DIPS_DEPTH_RGB
 #define DIPS_DEPTH_RGB 2
@@ -59,12 +49,11 @@ struct SeriesArgs {
     float thr;               // threshold in kernel units: series_threshold()
     const void* lut;         // GRAY8 table kernel: T_d / T_c bytes (series_gray.hip), 128 KiB
     uint32_t part_frames;    // frames per part of the part-major schedule (series_v2 SCHED = 1)
-    uint32_t thr_int;        // series_v2 SADI (ISI = 2): T = tau * 2^28 as an integer (series_sadi_threshold)
     // GRAY8 table kernel, layout 4: each workgroup samples its waves' first
     // items and takes layout 5 when band >= probe_min / 1024 of the sampled
     // pixels and (band >= probe_hi / 1024 of them or the waves' byte spreads
     // average >= probe_spread), else layout 2 (probe_min 0: always 5, > 1024:
-    // always 2)
+    // always 2 -- the pinned layouts)
     uint32_t probe_min;
     uint32_t probe_hi;
     uint32_t probe_spread;
@@ -115,7 +104,6 @@ struct CompatArgs {
     uint32_t out_key;        // compat_main_host: 0 RGBA8 texels; 1 one byte (gray: R = G = B, A = 255);
                              // 2 two bytes R | G << 8 (colorized: B = min(R, G), A = 255) -- the host
                              // expands them (host_stream.h expand_keys)
-    uint32_t host_pairs;     // out_key != 0: two pixels per thread (compat_main_host2_kernel)
     uint32_t in_key;         // compat_main_host: raw holds RGBA8 texels (0), or per pixel the chroma
                              // channel (1) / (max, min) of R, G, B (2) (copy_pool.h pack_frame);
                              // compat_main_host_packed_kernel, out_key 1 / 2 only
@@ -144,10 +132,6 @@ constexpr int kUnrollCompatBatch = 2;
 // budget is 128, and D = 4 spills.
 constexpr int kUnrollCompatLut = 4;
 constexpr int kDepthCompatLut = 3;
-// (U, D) of the table kernel this call runs: the defaults, or
-// DIPS_COMPAT_LUT_VARIANT = 22 / 23 / 42 / 43 for A/B runs
-int compat_lut_variant();
-int compat_lut_unroll();
 constexpr uint32_t kCompatLutWaves = 16;  // waves per workgroup of compat_batch_lut_kernel (one per CU)
 // the epilogue table of the current properties: lut[S * 256 + m]
 hipError_t launch_compat_lut(uint16_t* lut, uint32_t filter, float k, bool colorize, hipStream_t s);
@@ -160,15 +144,12 @@ hipError_t launch_compat_batch(const CompatBatchArgs& a, int chroma, int filter,
 // dips_alt DiPsCompute (alt_kernels.hip).
 constexpr int kAltMaxTextures = 16;  // MAX_TEMPORAL_ARRAY_SIZE (dips_alt pre_compute_shader.wgsl:12)
 constexpr int kUnrollAlt = 2;        // vecs (4 px) per lane of alt_batch_kernel
-// vecs per lane / frames of loads in flight of its epilogue-table form; A/B
-// variants by DIPS_ALT_LUT_VARIANT = 22 / 23 / 33 / 42 / 43.  In one process
+// vecs per lane / frames of loads in flight of its epilogue-table form.  In one process
 // over one batch (tools/alt_variant_ab.py, profiles/r02_alt_variant_ab.jsonl):
 // U = 4, D = 2 72.8 % of 8 TB/s read + write, U = 2, D = 2 72.1 %, the others
 // 71.2-72.3 % (8 groups of 256 threads per CU already keep enough in flight).
 constexpr int kUnrollAltLut = 4;
 constexpr int kDepthAltLut = 2;
-int alt_lut_variant();
-int alt_lut_unroll();
 
 struct AltArgs {                     // one send_frame dispatch
     const uint8_t* slots[kAltMaxTextures];  // RGBA8 contents of the N texture slots
@@ -245,35 +226,27 @@ inline bool alt_fast_epilogue_ok(uint32_t filter, float k) {
 int pixels_per_vec(int channels);
 int fast_unroll(int channels);
 // isi (series_v2, RGB8 / RGBA8): 0 the exact f64 intensity sum, 1 the
-// integer sum with a threshold select (ISI), 2 the integer sum from
-// sum |x - T| and sum x (SADI); 1 and 2 need tau >= 2^-5
+// integer sum with a threshold select (ISI; needs tau >= 2^-5)
 const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align = false,
                                    int isi = 0);
 const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align = false,
                                  int isi = 0);
 // whether tau admits the integer intensity sum of series_v2 (tau >= 2^-5)
 bool series_v2_isi(float tau);
-// whether tau admits SADI (2^-5 <= tau < 1)
-bool series_v2_sadi(float tau);
-// SeriesArgs::thr_int of the SADI kernel: tau * 2^28, at most 2^28
-uint32_t series_sadi_threshold(float tau);
 // threshold argument (SeriesArgs::thr) of the kernel series_fast_kernel_ptr picks
 float series_threshold(int channels, float tau, int isi = 0);
 hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, bool per_frame, bool map,
                               uint32_t blocks, hipStream_t s, bool align = false, int isi = 0);
-// record layout: 0 RGB(A), 1 gray (series_fast_kernel), 2 gray table kernel (series_gray_lut_kernel),
-// 3 RGB(A) SADI (thr_int: its T)
+// record layout: 0 RGB(A), 1 gray (series_fast_kernel), 2 gray table kernel (series_gray_lut_kernel)
 hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
-                                dips_series_entry* series, hipStream_t s, uint32_t thr_int = 0);
-// GRAY8 table kernel, table layout 1 (two byte tables), 2 (one u16 table) or
-// 3 (the u16 table keyed by (a ^ b, a), band clamp), 5 (the same unswizzled)
-// or 4 (5 or 2 per workgroup from a sample of its items: the default)
-const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs = 0, uint32_t waves = 16);
-int gray_alu_vecs(float tau);          // arithmetic vecs of this call's table kernel (0 for tau < 2^-5)
-uint32_t gray_lut_waves(int layout, int alu_vecs);  // waves per group of the table kernel
+                                dips_series_entry* series, hipStream_t s);
+// GRAY8 table kernel: table layout 4, i.e. layout 5 (the u16 table keyed by
+// (a ^ b, a) with the band clamp) or 2 (the u16 table keyed by (a, b),
+// swizzled) per workgroup from a sample of its items
+const void* series_gray_lut_kernel_ptr(bool per_frame, bool map);
+// the tables of layout 4 (5, then 2 kGrayLutAllocBytes after it), or of one layout
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s);
-hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
-                                  hipStream_t s, int alu_vecs = 0);
+hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, uint32_t blocks, hipStream_t s);
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
 hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, hipStream_t s);

@@ -14,32 +14,26 @@
 // difference leaves a non-negative power-of-two remainder).  So per selected pixel the
 // kernel needs d and corr, each one byte, and per frame
 //     SI_fixed = 2 (8421504 * sum d + sum corr),   count = #selected.
-// gray_lut_kernel writes two byte tables for the current tau,
-//     T_d[a * 256 + b] = selected ? d : 0,   T_c[...] = selected ? corr : 0,
-// and the series kernel keeps them (128 KiB) in LDS, one 1024-thread group
-// per CU.  Layout 2 (the default): one u16 table e = d | corr << 8 (rows
-// swizzled against LDS bank conflicts, kGraySwizzle); per
-// pixel pair one v_perm_b32 builds the two indices a * 256 + b, two
-// ds_read_u16 fetch the entries (SDWA word-select shifts give the byte
-// addresses), one v_perm_b32 puts both in one register, and three SADs
-// (bytes, u16 halves, u16 halves minus 1) yield sum d, sum corr and the
-// count exactly.  Layout 1: two byte tables read into the halves of one
-// register (d | corr << 16) -- fewer VALU, but two random LDS reads per
-// pixel (LDS-bound).  No f32, no f64: the exact f32 arithmetic of the
-// reference is folded into the table.  SAD is the byte SAD as before and
-// SJ = 2 SAD.
+// gray_lut_kernel writes, for the current tau, a u16 table of the entries
+//     e(a, b) = selected ? d | corr << 8 : 0,
+// and the series kernel keeps it (128 KiB) in LDS, one 1024-thread group per
+// CU.  Per pixel pair one v_perm_b32 builds the two indices, two ds_read_u16
+// fetch the entries, one v_perm_b32 puts both in one register, and three
+// SADs (bytes, u16 halves, u16 halves minus 1) yield sum d, sum corr and the
+// count exactly.  No f32, no f64: the exact f32 arithmetic of the reference
+// is folded into the table.  SAD is the byte SAD and SJ = 2 SAD.  Two table
+// layouts (keyed by (a, b) -- layout 2 -- or by (a ^ b, a) with a band clamp
+// -- layout 5), chosen per workgroup from the content it walks (layout 4,
+// series_gray_lut_kernel below).
 //
 // Records: {SAD, sum d, sum corr, count} per (tile, frame); series_reduce
 // (mode 2) forms SI_fixed = 2 (8421504 sum d + sum corr) in 64 bits.
 #include "series_common.h"
 
-#include <cstdlib>
 #include <type_traits>
 
 namespace dips {
 
-constexpr uint32_t kGrayLutTcOffset = 65535u;  // T_c's byte offset in LDS (the ds offset field's maximum;
-                                               // T_d[65535] and T_c[0] share a byte: both are 0, a == b)
 constexpr uint32_t kGrayV = 8421504u;          // V = kGrayV * d + corr
 
 // Layout 2 stores the entry of (a, b) at u16 index a * 256 + (b ^ sw(a)),
@@ -55,83 +49,33 @@ constexpr uint32_t kGrayV = 8421504u;          // V = kGrayV * d + corr
 // reference dword is swizzled once before the index perms).
 constexpr uint32_t kGraySwizzle = 0x3Cu;
 
-// Layout 3 (the default): the entry of (a, b) at u16 index
-// x * 256 + (a ^ sw(x)), x = a ^ b, sw(x) = (x << 1) & 0x7E.  Rows x < 2^m
-// hold only pairs with |a - b| < 2^m; when every one of them is below the
-// threshold (2^m - 1 <= the largest |a - b| that is never selected for tau),
-// all their entries are 0, and the kernel clamps every index below
+// Layout 5: the entry of (a, b) at u16 index x * 256 + a, x = a ^ b.  Rows
+// x < 2^m hold only pairs with |a - b| < 2^m; when every one of them is below
+// the threshold (2^m - 1 <= the largest |a - b| that is never selected for
+// tau), all their entries are 0, and the kernel clamps every index below
 // K = 256 * 2^m - 1 up to K (one v_pk_max_u16 per pixel pair): all those
 // lanes read the one entry K, an LDS broadcast instead of a random gather.
 // Consecutive video frames put most pixels there -- the bench's synthetic
-// clips (+-4 noise per frame) ~63 % at tau = 8/255, flat content nearly all --
-// while the remaining lanes stay spread over the banks: bits 1-6 of the
-// column are bits 1-6 of a XOR bits 0-5 of x.  m comes from the band word the
-// table kernel leaves after the table (256 - the first row holding a selected
-// pair), so the clamp is exact by construction for any tau.
+// clips (+-4 noise per frame) ~63 % at tau = 8/255, flat content nearly all.
+// m comes from the band word the table kernel leaves after the table (256 -
+// the first row holding a selected pair), so the clamp is exact by
+// construction for any tau.  (An earlier layout 3 also swizzled the column
+// against bank conflicts; layout 5 without it measured faster on the bench
+// content, profiles/r04/d/gray_layout_ab.jsonl.)
 constexpr uint32_t kGrayBandOffset = 131072u;  // byte offset of the band word (after the table)
-__host__ __device__ constexpr uint32_t gray_band_swizzle(uint32_t x) { return (x << 1) & 0x7Eu; }
-
-// The arithmetic vecs (NA of the U vecs per lane, tau >= 2^-5 only).  The
-// table path is bound by its LDS gathers (profiles/r03/gray_lds_counters.json:
-// the LDS array busy 96 % of the kernel, 6.9 LDS cycles per wave-wide
-// ds_read_u16, 4.9 of them bank conflicts) while the VALU idles a third of
-// the time, so NA of the U vecs skip the table and compute the same numbers
-// from the spec: U'(c) = 2^28 u(c) = fma(c, 2^28 K_HI, c * 2^28 K_LO) exactly
-// (the unorm identity of series_common.h, scaled by a power of two),
-// D' = RN(U'(a) - U'(b)) = 2^28 RN(u(a) - u(b)) exactly, the pixel is
-// selected when |D'| > 2^28 tau, and then, dI >= tau >= 2^-5 having an ulp of
-// at least 2^-28, |D'| = dI 2^28 = V / 8 is an integer below 2^28 (v_cvt_u32
-// exact).  Per lane the selected |D'| of 8 pixels fit a u32 (< 2^31); their
-// sum S splits as S = 1052688 sum d + sum corr / 8 (8421504 = 8 * 1052688,
-// corr a multiple of 8, sum corr / 8 < 1052688), which lands in the record's
-// sum d / sum corr fields.  Per frame, a PF reference's U' is the previous
-// frame's, kept in registers.
-constexpr float kGrayAluHi = 0x1.010102p20f;   // kUnormHi * 2^28
-constexpr float kGrayAluLo = -0x1.fdfdfep-5f;  // kUnormLo * 2^28
-constexpr uint32_t kGrayAluDiv = 1052688u;     // 8421504 / 8
-constexpr float kGrayAluMinTau = 0.03125f;     // 2^-5
-
-__device__ __forceinline__ void gray_alu_unorm4(uint32_t w, f32x2& u01, f32x2& u23) {
-    const f32x2 c01 = {(float)(w & 0xFFu), (float)((w >> 8) & 0xFFu)};
-    const f32x2 c23 = {(float)((w >> 16) & 0xFFu), (float)(w >> 24)};
-    const f32x2 hi = {kGrayAluHi, kGrayAluHi}, lo = {kGrayAluLo, kGrayAluLo};
-    u01 = __builtin_elementwise_fma(c01, hi, c01 * lo);
-    u23 = __builtin_elementwise_fma(c23, hi, c23 * lo);
-}
-
-// Four pixels (frame dword f, reference dword r): the selected |D'| added to
-// sv, the number selected (wave-wide, on the scalar unit) to cnt.
-__device__ __forceinline__ void gray_alu_dword(uint32_t f, uint32_t r, float thr28, uint32_t& sv, uint32_t& cnt) {
-    // opaque copy: the reference's U' is derived again, not kept from the
-    // previous frame (that costs 16 VGPRs the table path needs)
-    asm volatile("" : "+v"(r));
-    f32x2 f01, f23, r01, r23;
-    gray_alu_unorm4(f, f01, f23);
-    gray_alu_unorm4(r, r01, r23);
-    const f32x2 d01 = f01 - r01, d23 = f23 - r23;
-    const float d[4] = {fabsf(d01.x), fabsf(d01.y), fabsf(d23.x), fabsf(d23.y)};
-#pragma unroll
-    for (int p = 0; p < 4; p += 2) {
-        const bool s0 = d[p] > thr28, s1 = d[p + 1] > thr28;
-        cnt += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(s0)) +
-               (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(s1));
-        sv = sv + (s0 ? (uint32_t)d[p] : 0u) + (s1 ? (uint32_t)d[p + 1] : 0u);
-    }
-}
 
 // The tables for threshold tau (65,536 spec evaluations), 131,072 bytes:
-// layout 1 -- T_d at byte 0 and T_c at byte kGrayLutTcOffset;
-// layout 2 -- one u16 table, entry d | corr << 8 at byte 2 idx;
-// layout 3 -- the same entries keyed by (x = a ^ b, a) (see kGrayBandOffset),
+// layout 2 -- one u16 table, entry d | corr << 8 at byte 2 idx (swizzled);
+// layout 5 -- the same entries keyed by (x = a ^ b, a) (see kGrayBandOffset),
 // plus the band word: max over the rows x holding a selected pair of 256 - x
 // (0 when none is), which the caller zeroes before the launch.  One block per
-// row x in layout 3.
+// row x in layout 5.
 __global__ __launch_bounds__(256) void gray_lut_kernel(uint8_t* __restrict__ tab, float tau, uint32_t layout) {
     const uint32_t idx = blockIdx.x * 256u + threadIdx.x;
     uint32_t a = idx >> 8, b = idx & 0xFFu;
-    if (layout == 3u || layout == 5u) {
+    if (layout == 5u) {
         const uint32_t x = idx >> 8;
-        a = (idx & 0xFFu) ^ (layout == 3u ? gray_band_swizzle(x) : 0u);
+        a = idx & 0xFFu;
         b = a ^ x;
     }
     const float di = fabsf(unorm_load(a) - unorm_load(b));
@@ -140,16 +84,13 @@ __global__ __launch_bounds__(256) void gray_lut_kernel(uint8_t* __restrict__ tab
     const uint32_t d = a > b ? a - b : b - a;
     const uint32_t corr = (uint32_t)(v - (uint64_t)kGrayV * d);  // in [0, 128] (exhaustive test)
     const uint16_t e = sel ? (uint16_t)(d | corr << 8) : (uint16_t)0;
-    if (layout == 3u || layout == 5u) {
+    if (layout == 5u) {
         reinterpret_cast<uint16_t*>(tab)[idx] = e;
         if (__syncthreads_or(sel) && threadIdx.x == 0u)
             atomicMax(reinterpret_cast<uint32_t*>(tab + kGrayBandOffset), 256u - blockIdx.x);
-    } else if (layout == 2u) {
+    } else {
         const uint32_t pos = (a << 8) | (b ^ ((a << 2) & kGraySwizzle));
         reinterpret_cast<uint16_t*>(tab)[pos] = e;
-    } else {
-        tab[idx] = sel ? (uint8_t)d : (uint8_t)0;
-        if (idx != 0u) tab[kGrayLutTcOffset + idx] = sel ? (uint8_t)corr : (uint8_t)0;
     }
 }
 
@@ -172,31 +113,15 @@ __device__ __forceinline__ void gstore_one(__amdgpu_buffer_rsrc_t rpart, uint32_
 }
 
 // One frame of one tile against the reference bytes rb: the 4 per-lane
-// values {SAD, sum d, sum corr, 0} and the wave-wide count.
-// NA > 0 (layout 2): vecs U - NA .. U - 1 take the arithmetic path.
-// LAYOUT 3: kk = the band clamp K in both u16 halves.
-template <int U, int NA, bool MAP, int LAYOUT>
+// values {SAD, sum d, sum corr, count}.
+// LAYOUT 5: kk = the band clamp K in both u16 halves.
+template <int U, bool MAP, int LAYOUT>
 __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* lds, const uint32_t (&rb)[U][4],
-                                           const uint32_t (&cur)[U][4], float thr28, uint32_t kk, uint32_t voff,
-                                           uint32_t t, uint32_t* vals, uint32_t& cnt) {
-    static_assert(NA == 0 || (LAYOUT == 2 && NA < U), "arithmetic vecs: layout 2, at least one table vec");
-    constexpr bool U16 = LAYOUT >= 2;  // one u16 entry per pixel (layouts 2, 3)
-    uint32_t sad = 0, acc = 0, accd = 0, accc = 0, c = 0;
+                                           const uint32_t (&cur)[U][4], uint32_t kk, uint32_t voff, uint32_t t,
+                                           uint32_t* vals, uint32_t& cnt) {
+    static_assert(LAYOUT == 2 || LAYOUT == 5, "table layouts 2 and 5");
+    uint32_t sad = 0, acc = 0, accd = 0, accc = 0;
     uint32_t map[U][4];
-    uint32_t alu_s[NA > 0 ? 2 * NA : 1], alu_c = 0;
-    if constexpr (NA > 0) {
-#pragma unroll
-        for (int x = 0; x < NA; ++x) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                uint32_t sv = 0;
-#pragma unroll
-                for (int k = 2 * h; k < 2 * h + 2; ++k)
-                    gray_alu_dword(cur[U - NA + x][k], rb[U - NA + x][k], thr28, sv, alu_c);
-                alu_s[2 * x + h] = sv;
-            }
-        }
-    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -204,26 +129,23 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
             const uint32_t f = cur[u][k], r = rb[u][k];
             sad = __builtin_amdgcn_sad_u8(f, r, sad);
             if constexpr (MAP) map[u][k] = absdiff_bytes(f, r);
-            if (u >= U - NA) continue;
             // table indices of pixels (0, 2) and (1, 3) as u16 pairs, per byte
-            // of the dword at once: layouts 1 / 2 f_i * 256 + r_i (layout 2:
-            // r_i ^ sw(f_i)); layout 3 x_i * 256 + (f_i ^ sw3(x_i)),
-            // x_i = f_i ^ r_i, the indices below the band clamp raised to it
+            // of the dword at once: layout 2 f_i * 256 + (r_i ^ sw(f_i));
+            // layout 5 x_i * 256 + f_i, x_i = f_i ^ r_i, the indices below
+            // the band clamp raised to it
             uint32_t i02, i13;
-            if constexpr (LAYOUT == 3 || LAYOUT == 5) {
+            if constexpr (LAYOUT == 5) {
                 const uint32_t x = f ^ r;
-                // layout 5: the column is a itself (no bank swizzle; A/B)
-                const uint32_t col = LAYOUT == 5 ? f : f ^ ((x << 1) & (gray_band_swizzle(0xFFu) * 0x01010101u));
-                i02 = as_u32(__builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x06020400u)),
+                i02 = as_u32(__builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, f, 0x06020400u)),
                                                        as_u16x2(kk)));
-                i13 = as_u32(__builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, col, 0x07030501u)),
+                i13 = as_u32(__builtin_elementwise_max(as_u16x2(__builtin_amdgcn_perm(x, f, 0x07030501u)),
                                                        as_u16x2(kk)));
             } else {
-                const uint32_t rs = LAYOUT == 2 ? r ^ ((f << 2) & (kGraySwizzle * 0x01010101u)) : r;
+                const uint32_t rs = r ^ ((f << 2) & (kGraySwizzle * 0x01010101u));
                 i02 = __builtin_amdgcn_perm(f, rs, 0x06020400u);
                 i13 = __builtin_amdgcn_perm(f, rs, 0x07030501u);
             }
-            if constexpr (U16) {
+            {
                 // one u16 entry e = d | corr << 8 per pixel (0: not selected,
                 // else d >= 1), two pixels' entries in one register.  Three
                 // SAD sums per pixel pair carry everything:
@@ -242,36 +164,17 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
                 accd = __builtin_amdgcn_sad_u16(r13, 0u, accd);
                 acc = __builtin_amdgcn_sad_u16(r02, 0x00010001u, acc);
                 acc = __builtin_amdgcn_sad_u16(r13, 0x00010001u, acc);
-            } else {
-                const uint32_t ix[4] = {i02 & 0xFFFFu, i13 & 0xFFFFu, i02 >> 16, i13 >> 16};
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-                    const uint32_t e = (uint32_t)lds[ix[p]] | ((uint32_t)lds[kGrayLutTcOffset + ix[p]] << 16);
-                    acc += e;
-                    c += (uint32_t)__builtin_popcountll(__ballot(e != 0u));
-                }
             }
         }
     }
-    if constexpr (U16) {
-        // sb = accc, s0 = accd, s1 = acc (all < 2^22 for 64 px per lane):
-        // sum corr = (s0 - sb) / 255, sum d = sb - sum corr,
-        // count = (s0 + n - s1) / 2
-        constexpr uint32_t n = (uint32_t)(U - NA) * 16u;
-        uint32_t sc = (accd - accc) / 255u;
-        uint32_t sd = accc - sc;
-        c = (accd + n - acc) >> 1;
-        if constexpr (NA > 0) {
-#pragma unroll
-            for (int g = 0; g < 2 * NA; ++g) {
-                const uint32_t q = alu_s[g] / kGrayAluDiv;
-                sd += q;
-                sc += (alu_s[g] - q * kGrayAluDiv) << 3;
-            }
-            c += (threadIdx.x & 63u) == 0u ? alu_c : 0u;  // alu_c is wave-wide
-        }
-        acc = sd | (sc << 16);  // sum d < 2^15, sum corr < 2^14
-    }
+    // sb = accc, s0 = accd, s1 = acc (all < 2^22 for 64 px per lane):
+    // sum corr = (s0 - sb) / 255, sum d = sb - sum corr,
+    // count = (s0 + n - s1) / 2
+    constexpr uint32_t n = (uint32_t)U * 16u;
+    const uint32_t sc = (accd - accc) / 255u;
+    const uint32_t sd = accc - sc;
+    const uint32_t c = (accd + n - acc) >> 1;
+    acc = sd | (sc << 16);  // sum d < 2^15, sum corr < 2^14
     if constexpr (MAP) {
         const __amdgpu_buffer_rsrc_t rm = make_rsrc(a.dmap + (uint64_t)t * a.frame_bytes, a.vec_bytes);
 #pragma unroll
@@ -280,18 +183,13 @@ __device__ __forceinline__ void gray_frame(const SeriesArgs& a, const uint8_t* l
     vals[0] = sad;
     vals[1] = acc & 0xFFFFu;
     vals[2] = acc >> 16;
-    if constexpr (U16) {
-        vals[3] = c;  // per-lane count, summed with the other values
-        cnt = 0u;
-    } else {
-        vals[3] = 0u;
-        cnt = c;  // wave-wide (scalar popcounts)
-    }
+    vals[3] = c;  // per-lane count, summed with the other values
+    cnt = 0u;
 }
 
 // The item walk of the table kernel over its table in LDS (`lds`; `lut` =
-// the table's global copy, whose band word layout 3 reads).
-template <int U, bool PF, bool MAP, int LAYOUT, int NA, int GW>
+// the table's global copy, whose band word layout 5 reads).
+template <int U, bool PF, bool MAP, int LAYOUT, int GW>
 __device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* lds, const uint8_t* lut) {
     static_assert(U * 64 * 16 <= 4096, "vec offsets must fit the 12-bit immediate");
     const uint32_t lane = threadIdx.x & 63u;
@@ -300,9 +198,8 @@ __device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* ld
     const uint32_t fb = a.frame_bytes, vb = a.vec_bytes;
     const uint32_t rec_off8 = (lane & 7u) == 0u ? (lane >> 5) * 16u + ((lane >> 3) & 3u) * 4u : 0x80000000u;
     const uint32_t rec_off4 = (lane & 15u) == 0u ? (lane >> 4) * 4u : 0x80000000u;
-    const float thr28 = a.thr * 268435456.0f;  // 2^28 tau (exact)
     uint32_t kk = 0u;
-    if constexpr (LAYOUT == 3 || LAYOUT == 5) {
+    if constexpr (LAYOUT == 5) {
         // the band clamp from the word after the table: rows x < 2^m hold no
         // selected pair, m = floor(log2(the first row that does)), K = 256 * 2^m - 1
         const uint32_t w = *reinterpret_cast<const uint32_t*>(lut + kGrayBandOffset);
@@ -381,13 +278,12 @@ __device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* ld
                     const int j = 2 * h + q;
                     const uint32_t tf = t0 + k + (uint32_t)j;
                     if constexpr (PF) {
-                        gray_frame<U, NA, MAP, LAYOUT>(a, lds, buf[j], buf[(j + 1) & 3], thr28, kk, voff, tf,
-                                                       v + 4 * q, q ? c1 : c0);
+                        gray_frame<U, MAP, LAYOUT>(a, lds, buf[j], buf[(j + 1) & 3], kk, voff, tf, v + 4 * q,
+                                                   q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 3, buf[j]);
                     } else {
-                        gray_frame<U, NA, MAP, LAYOUT>(a, lds, rb, buf[j], thr28, kk, voff, tf, v + 4 * q,
-                                                       q ? c1 : c0);
+                        gray_frame<U, MAP, LAYOUT>(a, lds, rb, buf[j], kk, voff, tf, v + 4 * q, q ? c1 : c0);
                         __builtin_amdgcn_sched_barrier(0);
                         load_frame(tf + 4, buf[j]);
                     }
@@ -405,9 +301,9 @@ __device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* ld
                 uint32_t v[4], c;
                 const uint32_t tf = t0 + k + (uint32_t)j;
                 if constexpr (PF)
-                    gray_frame<U, NA, MAP, LAYOUT>(a, lds, buf[j], buf[j + 1], thr28, kk, voff, tf, v, c);
+                    gray_frame<U, MAP, LAYOUT>(a, lds, buf[j], buf[j + 1], kk, voff, tf, v, c);
                 else
-                    gray_frame<U, NA, MAP, LAYOUT>(a, lds, rb, buf[j], thr28, kk, voff, tf, v, c);
+                    gray_frame<U, MAP, LAYOUT>(a, lds, rb, buf[j], kk, voff, tf, v, c);
                 const uint32_t y = wave_sum4_lanes(v);
                 gstore_one(rpart, tf, rec_off4, lane, y, c);
             }
@@ -496,9 +392,9 @@ __device__ __forceinline__ void gray_sample(const SeriesArgs& a, uint32_t wave, 
     px = n;
 }
 
-template <int U, bool PF, bool MAP, int LAYOUT, int NA = 0, int GW = kGrayWaves>
+template <int U, bool PF, bool MAP, int LAYOUT, int GW = kGrayWaves>
 __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) {
-    __shared__ uint32_t lds32[32768];  // T_d at byte 0, T_c at byte kGrayLutTcOffset
+    __shared__ uint32_t lds32[32768];  // the u16 table of the chosen layout
     zero_series(a);
     bool use5 = true;
     if constexpr (LAYOUT == 4) {
@@ -526,9 +422,9 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
         sp = __builtin_amdgcn_readfirstlane(sp);
         nw = __builtin_amdgcn_readfirstlane(nw);
         if (a.probe_min == 0u)
-            use5 = true;
+            use5 = true;  // pinned (DIPS_FLAG_GRAY_BAND_TABLE)
         else if (a.probe_min > 1024u)
-            use5 = false;
+            use5 = false;  // pinned (DIPS_FLAG_GRAY_PAIR_TABLE)
         else
             use5 = sb * 1024u >= a.probe_min * sp && (sb * 1024u >= a.probe_hi * sp || ss >= a.probe_spread * nw);
     }
@@ -542,83 +438,26 @@ __global__ __launch_bounds__(64 * GW) void series_gray_lut_kernel(SeriesArgs a) 
     const uint8_t* lds = reinterpret_cast<const uint8_t*>(lds32);
     if constexpr (LAYOUT == 4) {
         if (use5)
-            gray_walk<U, PF, MAP, 5, NA, GW>(a, lds, lut);
+            gray_walk<U, PF, MAP, 5, GW>(a, lds, lut);
         else
-            gray_walk<U, PF, MAP, 2, NA, GW>(a, lds, lut);
+            gray_walk<U, PF, MAP, 2, GW>(a, lds, lut);
     } else {
-        gray_walk<U, PF, MAP, LAYOUT, NA, GW>(a, lds, lut);
+        gray_walk<U, PF, MAP, LAYOUT, GW>(a, lds, lut);
     }
 }
 
 }  // namespace
 
-template <int U, int L, int NA = 0, int GW = kGrayWaves>
+template <int L>
 static const void* gray_ptr(bool per_frame, bool map) {
-    return per_frame ? (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<U, true, true, L, NA, GW>)
-                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<U, true, false, L, NA, GW>))
-                     : (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<U, false, true, L, NA, GW>)
-                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<U, false, false, L, NA, GW>));
+    return per_frame ? (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, true, true, L>)
+                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, true, false, L>))
+                     : (map ? reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, false, true, L>)
+                            : reinterpret_cast<const void*>(&series_gray_lut_kernel<kUnrollGrayLut, false, false, L>));
 }
 
-bool gray_alu_allowed(float tau) { return tau >= kGrayAluMinTau; }
-
-uint32_t gray_lut_waves(int layout, int alu_vecs) {
-    // waves per group of the table kernel: 16, or with arithmetic vecs
-    // kGrayAluWaves; DIPS_GRAY_ALU_WAVES = 12 / 16 for A/B runs of the u16
-    // table at U = 4 (12 waves leave 168 VGPRs; the arithmetic vecs spill at 16)
-    if (layout != 2) return (uint32_t)kGrayWaves;  // layouts 1, 3: 16 waves, no arithmetic vecs
-    if (alu_vecs == 0 && gray_lut_unroll() != 4) return (uint32_t)kGrayWaves;
-    if (const char* e = std::getenv("DIPS_GRAY_ALU_WAVES")) {
-        const int w = std::atoi(e);
-        if (w == 12 || w == 16) return (uint32_t)w;
-    }
-    return alu_vecs == 0 ? (uint32_t)kGrayWaves : kGrayAluWaves;
-}
-
-int gray_alu_vecs(float tau) {
-    // DIPS_GRAY_ALU = 0 / 1 / 2 arithmetic vecs of the U = 4 table kernel
-    // (A/B runs), else the default; only for tau >= 2^-5
-    if (!gray_alu_allowed(tau)) return 0;
-    int na = kGrayAluVecs;
-    if (const char* e = std::getenv("DIPS_GRAY_ALU")) {
-        const int v = std::atoi(e);
-        if (v >= 0 && v <= 2) na = v;
-    }
-    return na;
-}
-
-int gray_lut_unroll() {
-    // DIPS_GRAY_LUT_U = 2 / 3 / 4 (A/B runs; layout 2 only), else the default
-    if (const char* e = std::getenv("DIPS_GRAY_LUT_U")) {
-        const int u = std::atoi(e);
-        if (u == 2 || u == 3 || u == 4) return u;
-    }
-    return kUnrollGrayLut;
-}
-
-const void* series_gray_lut_kernel_ptr(bool per_frame, bool map, int layout, int alu_vecs, uint32_t waves) {
-    if (layout == 1) return gray_ptr<kUnrollGrayLut, 1>(per_frame, map);
-    if (layout == 4) return (alu_vecs != 0 || waves != 16u) ? nullptr : gray_ptr<4, 4>(per_frame, map);
-    if (layout == 5) return (alu_vecs != 0 || waves != 16u) ? nullptr : gray_ptr<4, 5>(per_frame, map);
-    if (layout == 3) {
-        if (alu_vecs != 0 || waves != 16u) return nullptr;
-        switch (gray_lut_unroll()) {
-            case 2: return gray_ptr<2, 3>(per_frame, map);
-            case 3: return gray_ptr<3, 3>(per_frame, map);
-            default: return gray_ptr<4, 3>(per_frame, map);
-        }
-    }
-    if (layout != 2) return nullptr;
-    if (waves != 12u && waves != 16u) return nullptr;
-    if (alu_vecs == 0 && waves == 12u) return gray_lut_unroll() == 4 ? gray_ptr<4, 2, 0, 12>(per_frame, map) : nullptr;
-    if (alu_vecs == 1) return waves == 12u ? gray_ptr<4, 2, 1, 12>(per_frame, map) : gray_ptr<4, 2, 1, 16>(per_frame, map);
-    if (alu_vecs == 2) return waves == 12u ? gray_ptr<4, 2, 2, 12>(per_frame, map) : gray_ptr<4, 2, 2, 16>(per_frame, map);
-    switch (gray_lut_unroll()) {
-        case 2: return gray_ptr<2, 2>(per_frame, map);
-        case 3: return gray_ptr<3, 2>(per_frame, map);
-        default: return gray_ptr<4, 2>(per_frame, map);
-    }
-}
+// The shipped table kernel: layout 4, layout 5 or 2 per workgroup.
+const void* series_gray_lut_kernel_ptr(bool per_frame, bool map) { return gray_ptr<4>(per_frame, map); }
 
 hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
     if (layout == 4) {  // auto: layout 5 (+ band word), then layout 2 after it
@@ -633,15 +472,12 @@ hipError_t launch_gray_lut(uint8_t* tab, float tau, int layout, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, int layout, uint32_t blocks,
-                                  hipStream_t s, int alu_vecs) {
-    if (alu_vecs != 0 && (layout != 2 || !gray_alu_allowed(a.thr))) return hipErrorInvalidValue;
-    const uint32_t waves = gray_lut_waves(layout, alu_vecs);
-    const void* k = series_gray_lut_kernel_ptr(per_frame, map, layout, alu_vecs, waves);
+hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map, uint32_t blocks, hipStream_t s) {
+    const void* k = series_gray_lut_kernel_ptr(per_frame, map);
     if (!k || !a.lut || blocks == 0) return hipErrorInvalidValue;
     SeriesArgs args = a;
     void* params[] = {&args};
-    return hipLaunchKernel(k, dim3(blocks), dim3(64 * waves), params, 0, s);
+    return hipLaunchKernel(k, dim3(blocks), dim3(64 * kGrayWaves), params, 0, s);
 }
 
 }  // namespace dips

@@ -303,9 +303,6 @@ __global__ __launch_bounds__(256, DIPS_MIN_WAVES_PER_SIMD) void series_fast_kern
 //   gray:   {SAD + count << 20, H, L, 0}      SI_fixed = H << 16 + L, SJ = 2 SAD
 //   gray table kernel: {SAD, sum d, sum corr, count}
 //                                             SI_fixed = 2 (8421504 sum d + sum corr), SJ = 2 SAD
-//   RGB(A) SADI (series_v2.hip ISI = 2): {SAD + count << 20, sum u, H, L}
-//                                             SJ = sum over tiles of (sum u * 510 + 2^19) >> 20,
-//                                             SI_fixed = H << 15 + L + 16 T count
 // (H, L: the split of the exact per-lane fixed-point intensity sum).
 struct ReduceAcc {
     uint64_t sad = 0, sj = 0, cnt = 0, h = 0;
@@ -324,12 +321,6 @@ __device__ __forceinline__ void reduce_add(ReduceAcc& s, const u32x4 rec) {
         s.cnt += rec.x >> 20;
         s.h += rec.y;
         s.l += (int64_t)(int32_t)rec.z;
-    } else if constexpr (LAYOUT == 3u) {
-        s.sad += rec.x & 0xFFFFFu;
-        s.cnt += rec.x >> 20;
-        s.sj += ((uint64_t)rec.y * 510u + (1u << 19)) >> 20;  // one tile's SJ, rounded
-        s.h += rec.z;
-        s.l += rec.w;
     } else {
         s.sad += rec.x;
         s.sj += rec.y & 0xFFFFFu;
@@ -359,7 +350,7 @@ __device__ __forceinline__ void reduce_tiles(ReduceAcc& s, const uint64_t* __res
 
 __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __restrict__ partials, uint32_t n_frames,
                                                             uint32_t n_tiles, uint32_t tiles_per_block, uint32_t layout,
-                                                            uint32_t thr_int, dips_series_entry* __restrict__ series) {
+                                                            dips_series_entry* __restrict__ series) {
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
     if (t >= n_frames) return;
     const uint32_t tile0 = blockIdx.y * tiles_per_block;
@@ -367,8 +358,6 @@ __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __re
     ReduceAcc s;
     if (layout == 2u)
         reduce_tiles<2u>(s, partials, n_frames, t, tile0, tile1);
-    else if (layout == 3u)
-        reduce_tiles<3u>(s, partials, n_frames, t, tile0, tile1);
     else if (layout == 1u)
         reduce_tiles<1u>(s, partials, n_frames, t, tile0, tile1);
     else
@@ -376,8 +365,8 @@ __global__ __launch_bounds__(256) void series_reduce_kernel(const uint64_t* __re
     const uint64_t sad = s.sad, cnt = s.cnt, h = s.h;
     const int64_t l = s.l;
     const uint64_t sj = (layout == 1u || layout == 2u) ? 2u * sad : s.sj;
-    uint64_t sif = layout == 2u ? 2u * (8421504u * h + (uint64_t)l) : (h << (layout == 1u ? 16 : 15)) + (uint64_t)l;
-    if (layout == 3u) sif += 16u * (uint64_t)thr_int * cnt;  // the c T of every tile (series_v2.hip SADI)
+    const uint64_t sif =
+        layout == 2u ? 2u * (8421504u * h + (uint64_t)l) : (h << (layout == 1u ? 16 : 15)) + (uint64_t)l;
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].sad), (unsigned long long)sad);
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].sj), (unsigned long long)sj);
     atomicAdd(reinterpret_cast<unsigned long long*>(&series[t].count), (unsigned long long)cnt);
@@ -665,7 +654,7 @@ hipError_t launch_series_fast(const SeriesArgs& a, int channels, int chroma, boo
 }
 
 hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uint32_t n_tiles, int layout,
-                                dips_series_entry* series, hipStream_t s, uint32_t thr_int) {
+                                dips_series_entry* series, hipStream_t s) {
     // 64 tiles per thread (eight rounds of eight loads) when that still
     // gives >= 2048 groups (4K: 20 x 127), else down to 8 (one round): small
     // batches are latency-bound here (640x480 x 300 frames: 4 groups, 6 us)
@@ -674,7 +663,7 @@ hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uin
     while (tpb > 8u && (uint64_t)gx * ((n_tiles + tpb - 1u) / tpb) < 2048u && n_tiles / (tpb >> 1) < 65535u) tpb >>= 1;
     dim3 grid(gx, (n_tiles + tpb - 1u) / tpb);
     hipLaunchKernelGGL(series_reduce_kernel, grid, dim3(256), 0, s, partials, n_frames, n_tiles, tpb, (uint32_t)layout,
-                       thr_int, series);
+                       series);
     return hipGetLastError();
 }
 

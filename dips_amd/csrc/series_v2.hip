@@ -48,36 +48,6 @@ constexpr float kSjMul = 255.0f / 4194304.0f;
 // L = n mod 2^15, exactly as the f64 form.
 constexpr float kIsiMinTau = 0.03125f;  // 2^-5
 
-// ISI = 2 (SADI): the same integer intensities, with the threshold select of
-// the sum and the f32 SJ accumulation replaced by two integer sums per
-// pixel.  With x = trunc(|dI| * 2^28) for EVERY pixel (v_cvt_u32_f32; the
-// selected ones exact, an unselected one has x <= T) and T = tau * 2^28 (an
-// integer for tau >= 2^-5, clamped to 2^28):
-//   Sa = sum |x - T| (one v_sad_u32, accumulate included),
-//   Sx = sum x       (one v_add3_u32 per pixel pair),
-// and over n pixels with c of them selected
-//   sum_selected x = (Sa + Sx - n T) / 2 + c T.
-// Per lane the record carries Q = (Sa + Sx - n T) / 2 = sum_selected x - c T
-// as H, L (as ISI = 1 carries sum_selected x); series_reduce (layout 3) adds
-// 16 T count per frame.  SJ comes from Sx: 510 |dI| = |dJ| + e with
-// |e| < 1.1e-4 (the SJ identity above) and x * 2^-28 <= |dI| < (x + 1) * 2^-28,
-// so over a tile's 1024 pixels SJ = round(510 * 2^-28 * Sx) with an error
-// below 0.12; each lane keeps u = (Sx_0 >> 8) + (Sx_1 >> 8) (its two 8-pixel
-// halves, each < 2^31; the dropped bits cost < 0.063 per tile), and
-// series_reduce forms SJ_tile = (sum u * 510 + 2^19) >> 20 per record.  The
-// count moves into the SAD word (SAD < 2^20 per tile for RGB8 and RGBA8).
-// Per pixel: cvt, compare, SAD and half an add, against cvt, compare,
-// select, an f32 fma and half an add.
-constexpr float kSadiMaxT = 268435456.0f;  // 2^28
-
-// |a - b| + c in one v_sad_u32 (b wave-uniform; hipcc's own pattern match
-// leaves some of them as v_max / v_min / v_sub)
-__device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t r;
-    asm("v_sad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
-    return r;
-}
-
 // One frame of one tile: accumulate against the reference state `st`
 // (updated to this frame's state in per-frame mode) and the reference bytes
 // `rb`; produce the 4 per-lane values {SAD, SJ, H, L} and the wave-wide count.
@@ -97,7 +67,6 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
     // = 2^-9, the a_s granularity; n < 2^35 keeps every add exact)
     double si = 0x1p43;
     uint32_t si0 = 0, si1 = 0;  // ISI: sum of a over vecs 0 .. U/2-1 and U/2 .. U-1
-    uint32_t sx0 = 0, sx1 = 0;  // SADI: sum x over the same halves (si0: sum |x - T| over all 16 px)
     uint32_t map[U][F::NDW];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -117,10 +86,8 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
         for (int k = 0; k < 2; ++k) {
             const f32x2 d = n.i[k] - st[u].i[k];
             const float a0 = fabsf(d.x), a1 = fabsf(d.y);
-            if constexpr (ISI != 2) {
-                sj = __builtin_fmaf(a0, sj_mul, sj);
-                sj = __builtin_fmaf(a1, sj_mul, sj);
-            }
+            sj = __builtin_fmaf(a0, sj_mul, sj);
+            sj = __builtin_fmaf(a1, sj_mul, sj);
             const bool s0 = a0 > a.thr, s1 = a1 > a.thr;
             const uint64_t m0 = __ballot(s0), m1 = __ballot(s1);
             c += (uint32_t)__builtin_popcountll(m0) + (uint32_t)__builtin_popcountll(m1);
@@ -129,16 +96,7 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
             // as a forced branch it costs registers and occupancy)
             // (the lane-predicated form `if (s0) si += a0` compiles to an
             // unconditional add and two 32-bit selects of the f64: slower)
-            if constexpr (ISI == 2) {
-                const uint32_t x0 = (uint32_t)a0, x1 = (uint32_t)a1;
-                // |x - T| < 2^28 (T >= 2^23), so 16 of them fit one u32
-                si0 = sad_u32(x0, a.thr_int, si0);
-                si0 = sad_u32(x1, a.thr_int, si0);
-                if (u < U / 2)
-                    sx0 = sx0 + x0 + x1;
-                else
-                    sx1 = sx1 + x0 + x1;
-            } else if constexpr (ISI == 1) {
+            if constexpr (ISI == 1) {
                 const uint32_t v = (uint32_t)(s0 ? a0 : 0.0f) + (uint32_t)(s1 ? a1 : 0.0f);
                 if (u < U / 2)
                     si0 += v;
@@ -157,16 +115,7 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
     }
     vals[0] = sad;
     vals[1] = (uint32_t)sj;
-    if constexpr (ISI == 2) {
-        static_assert(U == 4, "SADI: two halves of 8 pixels per lane");
-        // Q = (Sa + Sx - 16 T) / 2 = sum_selected x - c T, in [0, 2^32)
-        // (Sa + Sx < 2^33: 64-bit, per lane and frame)
-        const uint64_t q2 = (uint64_t)si0 + sx0 + sx1 - 16u * (uint64_t)a.thr_int;
-        const uint32_t q = (uint32_t)(q2 >> 1);
-        vals[1] = (sx0 >> 8) + (sx1 >> 8);
-        vals[2] = q >> 11;
-        vals[3] = (q & 0x7FFu) << 4;
-    } else if constexpr (ISI == 1) {
+    if constexpr (ISI == 1) {
         // n = 16 (si0 + si1): H = n >> 15, L = n mod 2^15 without forming
         // the 33-bit sum
         const uint32_t low = (si0 & 0x7FFu) + (si1 & 0x7FFu);
@@ -181,19 +130,17 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
     cnt = c;
 }
 
-// Records of frames t, t+1 from their 8 reduced values (lanes 8v hold v).
-// CW: the record word that carries count << 20 (1: SJ; 0: SAD, SADI).
-template <int CW = 1>
+// Records of frames t, t+1 from their 8 reduced values (lanes 8v hold v);
+// the SJ word (1) carries count << 20.
 __device__ __forceinline__ void store_pair(__amdgpu_buffer_rsrc_t rpart, uint32_t t, uint32_t rec_off8,
                                            uint32_t lane, uint32_t y, uint32_t cnt0, uint32_t cnt1) {
-    const uint32_t add = lane == 8u * CW ? (cnt0 << 20) : (lane == 32u + 8u * CW ? (cnt1 << 20) : 0u);
+    const uint32_t add = lane == 8u ? (cnt0 << 20) : (lane == 40u ? (cnt1 << 20) : 0u);
     __builtin_amdgcn_raw_buffer_store_b32(y + add, rpart, rec_off8, t * 16u, 0);
 }
 
-template <int CW = 1>
 __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t t, uint32_t rec_off4,
                                           uint32_t lane, uint32_t y, uint32_t cnt) {
-    const uint32_t add = lane == 16u * CW ? (cnt << 20) : 0u;
+    const uint32_t add = lane == 16u ? (cnt << 20) : 0u;
     __builtin_amdgcn_raw_buffer_store_b32(y + add, rpart, rec_off4, t * 16u, 0);
 }
 
@@ -201,12 +148,9 @@ __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t
 // per-frame kernel fits 64 VGPRs (8 waves) without spilling; the other
 // variants hold more state (fixed reference bytes, RGBA vecs, map stores) and
 // keep their natural allocation (5-7 waves).
-// SADI (ISI = 2) holds one more accumulator and is given 4 waves (128
-// VGPRs; 4 and 5 waves per SIMD run the ISI kernel at the same speed).
-template <int C, int U, bool PF, bool MAP, bool ALIGN = false, int ISI = 0>
+template <int C, int U, bool PF, bool MAP, bool ALIGN = false>
 constexpr int v2_min_waves() {
-    return ALIGN ? (MAP ? 1 : 4)
-                 : ((C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : (ISI == 2 ? 4 : 5))) : 1);
+    return ALIGN ? (MAP ? 1 : 4) : ((C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : 5)) : 1);
 }
 
 // The aligned-load form of an RGB8 vec (ALIGN): a frame whose base address
@@ -248,7 +192,6 @@ __device__ __forceinline__ void funnel(uint32_t (&v)[L], uint32_t sh) {
 template <int C, int CH, int U, bool PF, bool MAP, int AUX, int SAUX, int SCHED = 0, bool ALIGN = false,
           int ISI = 0>
 __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
-    constexpr int CW = ISI == 2 ? 0 : 1;  // record word of the count
     using F = Fmt<C>;
     static_assert(!ALIGN || C == 3 || C == 4, "the aligned-load form is the RGB8 / RGBA8 one");
     constexpr bool A4 = ALIGN && C == 4;  // RGBA8: the fifth dword from the next lane
@@ -422,7 +365,7 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
                     }
                 }
                 const uint32_t y = wave_sum8_lanes(v, lane);
-                store_pair<CW>(rpart, t0 + k + 2 * h, rec_off8, lane, y, c0, c1);
+                store_pair(rpart, t0 + k + 2 * h, rec_off8, lane, y, c0, c1);
             }
         }
         // tail: up to 3 frames, already in flight in their slots
@@ -439,14 +382,14 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
                     frame_v2<C, CH, U, PF, MAP, SAUX, LW, LW, ISI>(a, st, rb, buf[j], voff, tf, v, c);
                 }
                 const uint32_t y = wave_sum4_lanes(v);
-                store_one<CW>(rpart, tf, rec_off4, lane, y, c);
+                store_one(rpart, tf, rec_off4, lane, y, c);
             }
         }
     }
 }
 
 template <int C, int CH, int U, bool PF, bool MAP, bool ALIGN = false, int ISI = 0>
-__global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP, ALIGN, ISI>())) void series_v2_kernel(SeriesArgs a) {
+__global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP, ALIGN>())) void series_v2_kernel(SeriesArgs a) {
     series_v2_body<C, CH, U, PF, MAP, kAuxNT, kAuxNT, 0, ALIGN, ISI>(a);
 }
 
@@ -478,14 +421,10 @@ static const void* pick_v2(int chroma, bool pf, bool map) {
 const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align, int isi) {
     switch (channels) {
         case 3:
-            if (isi == 2)
-                return align ? pick_v2<3, true, 2>(chroma, per_frame, map) : pick_v2<3, false, 2>(chroma, per_frame, map);
             if (isi == 1)
                 return align ? pick_v2<3, true, 1>(chroma, per_frame, map) : pick_v2<3, false, 1>(chroma, per_frame, map);
             return align ? pick_v2<3, true, 0>(chroma, per_frame, map) : pick_v2<3, false, 0>(chroma, per_frame, map);
         case 4:
-            if (isi == 2)
-                return align ? pick_v2<4, true, 2>(chroma, per_frame, map) : pick_v2<4, false, 2>(chroma, per_frame, map);
             if (isi == 1)
                 return align ? pick_v2<4, true, 1>(chroma, per_frame, map) : pick_v2<4, false, 1>(chroma, per_frame, map);
             return align ? pick_v2<4, true, 0>(chroma, per_frame, map) : pick_v2<4, false, 0>(chroma, per_frame, map);
@@ -494,15 +433,5 @@ const void* series_v2_kernel_ptr(int channels, int chroma, bool per_frame, bool 
 }
 
 bool series_v2_isi(float tau) { return tau >= kIsiMinTau; }
-
-// SADI needs T = tau * 2^28 < 2^28 (with T = 2^28, 16 equal pixels would
-// make sum |x - T| = 2^32); for tau >= 1 nothing is ever selected and ISI = 1
-// runs
-bool series_v2_sadi(float tau) { return tau >= kIsiMinTau && tau < 1.0f; }
-
-uint32_t series_sadi_threshold(float tau) {
-    const float t = tau * 268435456.0f;  // exact for tau >= 2^-5 (an integer)
-    return (uint32_t)(t < kSadiMaxT ? t : kSadiMaxT);
-}
 
 }  // namespace dips

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define DIPS_ABI_VERSION 1
+#define DIPS_ABI_VERSION 2
 
 typedef enum dips_status {
     DIPS_OK = 0,
@@ -33,7 +33,10 @@ typedef enum dips_status {
     DIPS_ERR_STATE = -3,    /* call not valid in the handle's state */
     DIPS_ERR_NOMEM = -4,    /* device or host allocation failed */
     DIPS_ERR_CAPACITY = -5, /* caller's output buffer too small */
-    DIPS_ERR_NODEVICE = -6  /* no HIP device / device index out of range */
+    DIPS_ERR_NODEVICE = -6, /* no HIP device / device index out of range */
+    DIPS_ERR_INTERNAL = -7  /* a C++ exception inside the library, caught at the
+                               boundary (see dips_last_error); the handle may
+                               be left mid-call and should be destroyed */
 } dips_status;
 
 /* DiPsFilter -> override id 3 (dips/src/lib.rs:25-41, dips_shader.wgsl:20). */
@@ -60,6 +63,22 @@ typedef enum dips_status {
 #define DIPS_FLAG_DEVICE_PTRS 0x1u /* series pointers are device (HBM) pointers */
 #define DIPS_FLAG_TIME_KERNEL 0x2u /* record hipEvents around the series kernel */
 #define DIPS_FLAG_FORCE_GENERIC 0x4u /* use the generic (any-shape) series kernel */
+/* Cross-check forms: the same results through the plain kernels instead of
+ * the specialised ones -- GRAY8 series: the f32 kernel, not the table kernel;
+ * RGB8 / RGBA8 series: the exact f64 intensity sum at every tau, not the
+ * integer sum of tau >= 2^-5; dips-compat / dips_alt batches: the per-pixel
+ * arithmetic epilogue, not the epilogue table; the per-frame calls: whole
+ * RGBA8 frames through the DMA staging (add_texture + dispatch), not the
+ * striped zero-copy pipeline with compact transfers.  For tests and
+ * A/B checks; slower. */
+#define DIPS_FLAG_CROSSCHECK 0x8u
+/* GRAY8 series: pin the table kernel's layout instead of its per-workgroup
+ * choice from the content it walks (series_gray.hip layout 4) -- the table
+ * keyed by (a ^ b, a) with the band clamp (BAND: fastest on consecutive video
+ * frames) or by (a, b) (PAIR: fastest on flat or i.i.d. random content).
+ * Same results either way; both set = BAND. */
+#define DIPS_FLAG_GRAY_BAND_TABLE 0x10u
+#define DIPS_FLAG_GRAY_PAIR_TABLE 0x20u
 
 /* Operator parameters.  The first five mirror ComputeState::new's arguments
  * (dips/src/gpu/mod.rs:59-65) and DiPsProperties (dips/src/lib.rs:63-86);
@@ -151,7 +170,7 @@ dips_status dips_synchronize(dips_handle *h);
  * (window 1, host pointers) the call also starts the compute of the
  * dispatch that normally follows on the staged frame; that dispatch then
  * only collects it, and any other call first lets it finish, keeping the
- * reference's state (DIPS_DEFER_UPLOAD=0 turns this off). */
+ * reference's state (DIPS_FLAG_CROSSCHECK turns this off). */
 dips_status dips_add_texture(dips_handle *h, uint32_t width, uint32_t height,
                              const uint8_t *frame_rgba, size_t len);
 

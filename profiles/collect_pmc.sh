@@ -13,12 +13,12 @@ mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o run -- \
     python3 bench.py --frames-per-gpu $F --steps 2 --warmup 1 --mode $MODE --no-cpu-baseline --no-pcie \
-    --map-frames 2500 > $OUT/$c.log 2>&1
+    --no-tau0 --no-legs --no-per-frame-call --map-frames 2500 > $OUT/$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 PF=$([ "$MODE" = per-frame ] && echo true || echo false)
 python3 tools/pmc_to_json.py $OUT $F $MODE gpurun_out/pmc_traffic.json \
-  "series_v2_kernel<3, 0, 4, $PF, false, false" && \
+  "series_v2_kernel<3, 0, 4, $PF, false, false, 1>" && \
 python3 tools/pmc_to_json.py $OUT 2500 $MODE gpurun_out/pmc_traffic_map.json \
-  "series_v2_kernel<3, 0, 4, $PF, true, false" $((3840 * 2160 * 3 * 2))
+  "series_v2_kernel<3, 0, 4, $PF, true, false, 1>" $((3840 * 2160 * 3 * 2))
 # copy gpurun_out/pmc_traffic*.json into profiles/ after merge-back

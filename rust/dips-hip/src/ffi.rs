@@ -18,8 +18,9 @@ pub const DIPS_ERR_STATE: DipsStatus = -3;
 pub const DIPS_ERR_NOMEM: DipsStatus = -4;
 pub const DIPS_ERR_CAPACITY: DipsStatus = -5;
 pub const DIPS_ERR_NODEVICE: DipsStatus = -6;
+pub const DIPS_ERR_INTERNAL: DipsStatus = -7;
 
-pub const DIPS_ABI_VERSION: c_int = 1;
+pub const DIPS_ABI_VERSION: c_int = 2;
 
 pub const DIPS_FILTER_SIGMOID: u32 = 0;
 pub const DIPS_FILTER_INVERSE_SIGMOID: u32 = 1;
@@ -36,6 +37,9 @@ pub const DIPS_MODE_PER_FRAME: u32 = 1;
 pub const DIPS_FLAG_DEVICE_PTRS: u32 = 0x1;
 pub const DIPS_FLAG_TIME_KERNEL: u32 = 0x2;
 pub const DIPS_FLAG_FORCE_GENERIC: u32 = 0x4;
+pub const DIPS_FLAG_CROSSCHECK: u32 = 0x8;
+pub const DIPS_FLAG_GRAY_BAND_TABLE: u32 = 0x10;
+pub const DIPS_FLAG_GRAY_PAIR_TABLE: u32 = 0x20;
 pub const DIPS_CALLBACK_PHASES: u32 = 11;
 
 /// `dips_params`: ComputeState::new's arguments (dips/src/gpu/mod.rs:59-65,

@@ -9,8 +9,15 @@
 //! north star's per-frame difference series (`DiffSeries`) and the dips_alt
 //! operator (`DiPsCompute`, dips_alt/src/dips_compute/mod.rs:243-647).
 //!
-//! Every call goes through `ffi` (include/dips_hip.h); nothing panics across
-//! the boundary and no CPU fallback exists.
+//! Every call goes through `ffi` (include/dips_hip.h); no CPU fallback
+//! exists.  Failure contract: the library never unwinds into Rust (every C++
+//! exception is caught at the boundary and returned as a status,
+//! `DIPS_ERR_INTERNAL` / `DIPS_ERR_NOMEM`); this crate never unwinds into
+//! the library.  The `try_*` methods return every failure as a `DipsError`;
+//! the reference-shaped methods keep the reference's signatures and panic
+//! where its wgpu path panics (a device error), so `None` from `dispatch`
+//! means the warm-up only and `frame_callback` never passes the input
+//! through on an error.
 
 pub mod ffi;
 
@@ -176,13 +183,25 @@ impl ComputeState {
         Ok(())
     }
 
-    /// gpu/mod.rs:306-397: `None` while the ring warms up (frames 0..2).
-    pub fn dispatch(&mut self) -> Option<Vec<u8>> {
+    /// gpu/mod.rs:306-397: `Ok(None)` while the ring warms up (frames 0..2),
+    /// `Ok(Some(frame))` after, `Err` on any failure.
+    pub fn try_dispatch(&mut self) -> Result<Option<Vec<u8>>, DipsError> {
         let mut out = vec![0u8; self.frame_bytes()];
         // SAFETY: out has cap bytes.
-        match unsafe { ffi::dips_dispatch(self.h.as_ptr(), out.as_mut_ptr(), out.len()) } {
-            1 => Some(out),
-            _ => None,
+        let r = unsafe { ffi::dips_dispatch(self.h.as_ptr(), out.as_mut_ptr(), out.len()) };
+        match check(r, self.h.as_ptr())? {
+            1 => Ok(Some(out)),
+            _ => Ok(None),
+        }
+    }
+
+    /// gpu/mod.rs:306-397 with the reference's signature: `None` only while
+    /// the ring warms up (:394-396).  Panics on a device or argument error,
+    /// as the reference's wgpu calls do; use `try_dispatch` to handle it.
+    pub fn dispatch(&mut self) -> Option<Vec<u8>> {
+        match self.try_dispatch() {
+            Ok(v) => v,
+            Err(e) => panic!("ComputeState::dispatch: {e}"),
         }
     }
 
@@ -233,13 +252,23 @@ impl ComputeState {
         if st == ffi::DIPS_OK { Some(v) } else { None }
     }
 
-    /// The start texture S (pre_compute_shader.wgsl:92-132), once built.
-    pub fn start_texture(&mut self) -> Option<Vec<u8>> {
+    /// The start texture S (pre_compute_shader.wgsl:92-132): `Ok(None)`
+    /// until the 4th frame has built it.
+    pub fn try_start_texture(&mut self) -> Result<Option<Vec<u8>>, DipsError> {
         let mut out = vec![0u8; self.frame_bytes()];
         // SAFETY: out has cap bytes.
-        match unsafe { ffi::dips_start_texture(self.h.as_ptr(), out.as_mut_ptr(), out.len()) } {
-            1 => Some(out),
-            _ => None,
+        let r = unsafe { ffi::dips_start_texture(self.h.as_ptr(), out.as_mut_ptr(), out.len()) };
+        match check(r, self.h.as_ptr())? {
+            1 => Ok(Some(out)),
+            _ => Ok(None),
+        }
+    }
+
+    /// `try_start_texture`, panicking on an error (`None`: not built yet).
+    pub fn start_texture(&mut self) -> Option<Vec<u8>> {
+        match self.try_start_texture() {
+            Ok(v) => v,
+            Err(e) => panic!("ComputeState::start_texture: {e}"),
         }
     }
 
@@ -271,15 +300,16 @@ impl Drop for ComputeState {
 
 /// dips/src/lib.rs:233-246, the `CallbackFunction` the GStreamer appsink
 /// closure calls (frame_extractor.rs:232-240): add_texture, then dispatch
-/// or the input passed through.  One ABI call per frame (dips_frame_callback
-/// overlaps the upload, the kernel and the readback in row stripes).
+/// or the input passed through while the ring warms up.  One ABI call per
+/// frame (dips_frame_callback overlaps the upload, the kernel and the
+/// readback in row stripes).  An error panics, as the reference's wgpu path
+/// does -- it is never disguised as the warm-up passthrough; callers that
+/// handle errors use `ComputeState::frame_callback_into`.
 pub fn frame_callback(width: u32, height: u32, frame_data: &[u8], compute: &mut ComputeState) -> Vec<u8> {
     let mut out = vec![0u8; frame_data.len()];
     match compute.frame_callback_into(width, height, frame_data, &mut out) {
         Ok(_) => out,
-        // the reference's wgpu path panics on a device error; keep the
-        // caller's contract (a frame back) and pass the input through
-        Err(_) => frame_data.to_vec(),
+        Err(e) => panic!("frame_callback: {e}"),
     }
 }
 

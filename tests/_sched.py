@@ -1,25 +1,16 @@
 """Test helper: the part-major schedule the library picks for a 'per-frame'
-RGB8 / RGBA8 batch, restated from dips_abi.hip part_geometry so that a test
+RGB8 / RGBA8 batch, restated from series_abi.hip part_geometry so that a test
 can assert which schedule a launch runs (and that the library agrees: the
 wave count it reports must equal the restatement's)."""
 from __future__ import annotations
 
-import os
-
 
 def resident_waves(op, width: int, height: int, n_frames: int) -> int:
     """Wave slots of the series kernel for this shape: the library's wave
-    count with the part-major schedule off and more items than slots."""
-    old = os.environ.get("DIPS_SERIES_PARTS")
-    os.environ["DIPS_SERIES_PARTS"] = "0"
-    try:
-        waves, tiles, _ = op.geometry(width, height, n_frames)
-    finally:
-        if old is None:
-            del os.environ["DIPS_SERIES_PARTS"]
-        else:
-            os.environ["DIPS_SERIES_PARTS"] = old
-    assert tiles * n_frames > waves, "batch too small to fill the wave slots"
+    count for a batch of < 256 frames (the contiguous ranges, part_geometry
+    starts at 256) that has more items than slots."""
+    waves, tiles, _ = op.geometry(width, height, min(n_frames, 255))
+    assert tiles * min(n_frames, 255) > waves, "batch too small to fill the wave slots"
     return int(waves)
 
 

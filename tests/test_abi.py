@@ -28,7 +28,7 @@ def test_header_functions_exported():
     assert len(names) >= 18
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.dips_abi_version() == 1
+    assert lib.dips_abi_version() == 2
 
 
 def test_rust_crate_binds_every_entry_point():

@@ -250,48 +250,48 @@ def test_rejects_bad_input():
         c.close()
 
 
-@pytest.mark.parametrize("chunk_frames", [1, 4, 9])
-@pytest.mark.parametrize("copies", ["", "1"])  # default (DMA) / copy kernels both ways
-def test_run_host_feed_chunks(monkeypatch, chunk_frames, copies):
-    """Host frames go through the pipelined feed in chunks; with a few frames
-    per chunk (ragged last chunk, refresh markers and snapshots falling on
-    chunk edges) the loop's outputs equal the oracle's."""
+@pytest.mark.parametrize("pieces", [[13, 37], [1, 4, 45], [50], [7, 7, 7, 29]])
+def test_run_host_feed_chunks(pieces):
+    """Host frames go through the pipelined feed in chunks of at most a
+    quarter of each call's batch (host_stream.h feed_chunk_frames); calls of
+    1 to 50 frames (ragged last chunks, refresh markers and snapshots falling
+    on chunk and call edges) give the loop's outputs equal to the oracle's."""
     from dips_amd.alt import DiPsRunner
     w, h = 32, 24
-    monkeypatch.setenv("DIPS_PIPE_KERNEL_COPY", copies)
-    monkeypatch.setenv("DIPS_FEED_CHUNK_BYTES", str(chunk_frames * w * h * 4))
-    frames = _frames(w, h, 50, 40 + chunk_frames)
+    frames = _frames(w, h, 50, 40 + len(pieces))
     markers = [4, 9, 10, 27, 36]
     want = oracle.AltCompute(2, w, h, True, 1, 5.0, 0, 0).run(frames, markers)
     r = DiPsRunner(h, w, _props(True, 1, 5.0, 0, 0), markers)
     try:
-        got = np.concatenate([r(frames[:13]), r(frames[13:])])
+        bounds = np.cumsum([0] + pieces)
+        got = np.concatenate([r(frames[a:b]) for a, b in zip(bounds[:-1], bounds[1:])])
     finally:
         r.close()
     assert np.array_equal(got, want), np.argwhere(got != want)[:4]
 
 
+# frame shapes whose per-frame pipeline cuts several row stripes with a
+# ragged last one (host_stream.h piece_bytes / DirectGeom): 40 x 200 -- 5
+# stripes of 50 rows (the first 12); 41 x 157 (odd row bytes) -- 5 stripes
+STRIPE_SHAPES = [(40, 200), (41, 157)]
+
+
 @pytest.mark.parametrize("n_tex,filt,colorize", [(2, 0, True), (3, 255, False), (1, 1, True), (16, 0, False)])
-@pytest.mark.parametrize("piece", ["rows3", "odd"])
-@pytest.mark.parametrize("form", ["direct", "direct-1stream", "dma"])
-def test_send_frame_striped_matches_oracle(monkeypatch, n_tex, filt, colorize, piece, form):
-    """send_frame with W = 1 goes through the striped path -- the zero-copy
-    form (the kernel reads the frame from pinned host memory, stores it into
-    its slot and writes the output to pinned host memory; stripes on two
-    streams or one) or the DMA form (upload / kernel / readback); with
-    stripes of a few rows (ragged last stripe), more frames than slots and
-    snapshots on some frames (read back by the frames after them), every
-    output equals the oracle's."""
+@pytest.mark.parametrize("shape", STRIPE_SHAPES)
+@pytest.mark.parametrize("crosscheck", [False, True])
+def test_send_frame_striped_matches_oracle(n_tex, filt, colorize, shape, crosscheck):
+    """send_frame with W = 1 goes through the zero-copy striped path (the
+    kernel reads the frame from pinned host memory, stores it into its slot
+    and writes the output to pinned host memory, stripes alternating over two
+    streams) or, with DIPS_FLAG_CROSSCHECK, whole-frame DMA transfers; with
+    several ragged stripes, more frames than slots and snapshots on some
+    frames (read back by the frames after them), every output equals the
+    oracle's."""
     from dips_amd.alt import DiPsCompute
-    w, h = 40, 27
-    row = w * 4
-    monkeypatch.setenv("DIPS_PIECE_BYTES", str({"rows3": 3 * row, "odd": 5 * row + 9}[piece]))
-    monkeypatch.setenv("DIPS_CALLBACK_DIRECT", "0" if form == "dma" else "1")
-    monkeypatch.setenv("DIPS_DIRECT_STREAMS", "1" if form == "direct-1stream" else "2")
-    monkeypatch.setenv("DIPS_DIRECT_SPLIT", "3" if form == "direct-1stream" else "4")  # copy-pool pieces per stripe
+    w, h = shape
     frames = _frames(w, h, 20, 60 + n_tex)
     snaps = [False, True, False, False, True, False, False, False, False, True, False, False] + [False] * 8
-    c = DiPsCompute(n_tex, h, w, _props(colorize, 1, 5.0, filt, 0))
+    c = DiPsCompute(n_tex, h, w, _props(colorize, 1, 5.0, filt, 0), crosscheck=crosscheck)
     ref = oracle.AltCompute(n_tex, w, h, colorize, 1, 5.0, filt, 0)
     try:
         for t in range(20):
@@ -362,44 +362,40 @@ def test_lut_selfcheck_exhaustive(filt, colorize):
 
 @pytest.mark.parametrize("filt,colorize", list(itertools.product([0, 1, 255], [False, True])))
 @pytest.mark.parametrize("window,chroma", [(1, 0), (1, 2), (1, 3), (3, 0), (5, 1)])
-def test_batch_lut_equals_arithmetic_and_oracle(filt, colorize, window, chroma, monkeypatch):
+def test_batch_lut_equals_arithmetic_and_oracle(filt, colorize, window, chroma):
     """alt_batch_kernel with the epilogue table (default) against its
-    per-pixel arithmetic form (DIPS_ALT_LUT=0) and the oracle's run loop, on
-    random frames with snapshots, W = 1 (RGBA8 frames) and W > 1
+    per-pixel arithmetic form (DIPS_FLAG_CROSSCHECK) and the oracle's run
+    loop, on random frames with snapshots, W = 1 (RGBA8 frames) and W > 1
     (prefiltered intensities)."""
     from dips_amd.alt import DiPsRunner
     w, h = 72, 40
     frames = _frames(w, h, 36, 500 + filt + 7 * chroma + window)
     markers = [4, 5, 20]
     outs = {}
-    for lut in ("1", "0"):
-        monkeypatch.setenv("DIPS_ALT_LUT", lut)
-        r = DiPsRunner(h, w, _props(colorize, window, 4.0, filt, chroma), markers)
+    for xc in (False, True):
+        r = DiPsRunner(h, w, _props(colorize, window, 4.0, filt, chroma), markers, crosscheck=xc)
         try:
-            outs[lut] = r(frames)
+            outs[xc] = r(frames)
         finally:
             r.close()
-    assert np.array_equal(outs["1"], outs["0"]), np.argwhere(outs["1"] != outs["0"])[:4]
+    assert np.array_equal(outs[False], outs[True]), np.argwhere(outs[False] != outs[True])[:4]
     want = oracle.AltCompute(2, w, h, colorize, window, 4.0, filt, chroma).run(frames, markers)
-    assert np.array_equal(outs["1"], want), np.argwhere(outs["1"] != want)[:4]
+    assert np.array_equal(outs[False], want), np.argwhere(outs[False] != want)[:4]
 
 
 @pytest.mark.parametrize("window", [3, 6])
-@pytest.mark.parametrize("form", ["direct", "dma"])
-@pytest.mark.parametrize("piece", ["rows3", "odd"])
-def test_send_frame_window_stripes_match_oracle(monkeypatch, window, form, piece):
+@pytest.mark.parametrize("crosscheck", [False, True])
+@pytest.mark.parametrize("shape", STRIPE_SHAPES)
+def test_send_frame_window_stripes_match_oracle(window, crosscheck, shape):
     """send_frame with W > 1: the zero-copy form uploads the stripes into the
     slot by copy kernels, runs the frame kernel on the whole frame and brings
     the output back by copy kernels, stripe by stripe (several ragged stripes
-    here); the DMA form moves whole frames.  Every output equals the
-    oracle's, snapshots included."""
+    here); the cross-check form (DIPS_FLAG_CROSSCHECK) moves whole frames by
+    DMA.  Every output equals the oracle's, snapshots included."""
     from dips_amd.alt import DiPsCompute
-    w, h = 41, 23
-    row = w * 4
-    monkeypatch.setenv("DIPS_PIECE_BYTES", str({"rows3": 3 * row, "odd": 5 * row + 9}[piece]))
-    monkeypatch.setenv("DIPS_CALLBACK_DIRECT", "0" if form == "dma" else "1")
+    w, h = shape
     frames = _frames(w, h, 10, 300 + window)
-    gpu = DiPsCompute(3, h, w, _props(True, window, 3.0, 0, 0))
+    gpu = DiPsCompute(3, h, w, _props(True, window, 3.0, 0, 0), crosscheck=crosscheck)
     ref = oracle.AltCompute(3, w, h, True, window, 3.0, 0, 0)
     try:
         for t in range(10):

@@ -252,46 +252,48 @@ def test_frame_callback_batch_device_4k():
         cs2.close()
 
 
-@pytest.mark.parametrize("chunk_frames", [1, 3, 7])
-@pytest.mark.parametrize("copies", ["", "1"])  # default (DMA) / copy kernels both ways
-def test_frame_callback_batch_host_feed_chunks(monkeypatch, chunk_frames, copies):
+@pytest.mark.parametrize("pieces", [[5, 56], [1, 2, 58], [61], [9, 9, 9, 34]])
+def test_frame_callback_batch_host_feed_chunks(pieces):
     """The host-pointer batch is fed through the pipelined upload / kernel /
-    download in chunks (two in flight); forced down to a few frames per chunk
-    with a ragged last chunk, the outputs stay those of the oracle."""
+    download in chunks of at most a quarter of the call's batch (two in
+    flight; host_stream.h feed_chunk_frames); calls of 1 to 61 frames (ragged
+    last chunks, the warm-up frames split over calls) give the oracle's
+    outputs."""
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter
     w, h = 64, 48
-    monkeypatch.setenv("DIPS_PIPE_KERNEL_COPY", copies)
-    monkeypatch.setenv("DIPS_FEED_CHUNK_BYTES", str(chunk_frames * w * h * 4))
-    frames = _frames(w, h, 61, 5 + chunk_frames)
+    frames = _frames(w, h, 61, 5 + len(pieces))
     params = (True, 1, 5.0, 0, 0)
     want = _oracle_callbacks(frames, params)
     cs = ComputeState(True, 1, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
     try:
-        got = np.concatenate([cs.frame_callback_batch(w, h, frames[:5]), cs.frame_callback_batch(w, h, frames[5:])])
+        bounds = np.cumsum([0] + pieces)
+        got = np.concatenate([cs.frame_callback_batch(w, h, frames[a:b]) for a, b in zip(bounds[:-1], bounds[1:])])
     finally:
         cs.close()
     assert np.array_equal(got, want), np.argwhere(got != want)[:4]
 
 
+# frame shapes of the per-frame pipeline (host_stream.h piece_bytes /
+# DirectGeom): 40 x 200 -- 5 row stripes of 50 (the first 12); 41 x 157 (odd
+# row bytes) -- 5 stripes, the last ragged; 16 x 8 -- one stripe
+STRIPE_SHAPES = [(40, 200), (41, 157), (16, 8)]
+
+
 @pytest.mark.parametrize("colorize,sens,filt,chroma", [(False, 5.0, 255, 0), (True, 5.0, 0, 0), (True, 0.7, 1, 2)])
-@pytest.mark.parametrize("piece", ["rows3", "odd", "whole"])
-@pytest.mark.parametrize("form", ["direct", "direct-1stream", "dma"])
-def test_frame_callback_striped_matches_oracle(monkeypatch, colorize, sens, filt, chroma, piece, form):
-    """Steady-state frame_callback goes through the striped path -- the
-    zero-copy form (the kernel reads and writes pinned host memory, stripes
-    on two streams or one) or the DMA form (upload, per-stripe kernel and
-    readback overlapped); with stripes of a few rows, a ragged last stripe or
-    one stripe, every output and the ring state equal the oracle's
-    add_texture + dispatch."""
+@pytest.mark.parametrize("shape", STRIPE_SHAPES)
+@pytest.mark.parametrize("crosscheck", [False, True])
+def test_frame_callback_striped_matches_oracle(colorize, sens, filt, chroma, shape, crosscheck):
+    """Steady-state frame_callback goes through the zero-copy striped path
+    (the copy pool packs each row stripe into pinned memory, the kernel reads
+    it over PCIe and writes the output keys back, stripes alternating over
+    two streams) or, with DIPS_FLAG_CROSSCHECK, through add_texture +
+    dispatch with whole-frame DMA transfers; with several ragged stripes or
+    one, every output and the ring state equal the oracle's add_texture +
+    dispatch."""
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
-    w, h = 40, 29
-    row = w * 4
-    monkeypatch.setenv("DIPS_PIECE_BYTES", str({"rows3": 3 * row, "odd": 7 * row + 5, "whole": 1 << 22}[piece]))
-    monkeypatch.setenv("DIPS_CALLBACK_DIRECT", "0" if form == "dma" else "1")
-    monkeypatch.setenv("DIPS_DIRECT_STREAMS", "1" if form == "direct-1stream" else "2")
-    monkeypatch.setenv("DIPS_DIRECT_SPLIT", "3" if form == "direct-1stream" else "4")  # copy-pool pieces per stripe
+    w, h = shape
     frames = _frames(w, h, 16, 90 + filt)
-    cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter(chroma))
+    cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter(chroma), crosscheck=crosscheck)
     ref = oracle.ComputeState(colorize, 1, sens, filt, chroma)
     try:
         for k in range(16):
@@ -370,13 +372,13 @@ def test_resume_window_matches_continuous_run(window):
 
 
 @pytest.mark.parametrize("window", [1, 3])
-def test_resume_after_deferred_add_texture(monkeypatch, window):
+def test_resume_after_deferred_add_texture(window):
     """dips_compat_resume on a handle whose last call was a deferred
-    add_texture (W = 1: its speculative stripes still in flight on two
-    streams): resume waits for them before rewriting the ring, so the resumed
-    handle gives the outputs of a fresh resumed one."""
+    add_texture (W = 1: its speculative stripes -- 5 of them at 96 x 64 --
+    still in flight on two streams): resume waits for them before rewriting
+    the ring, so the resumed handle gives the outputs of a fresh resumed one
+    (ADVICE r2)."""
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
-    monkeypatch.setenv("DIPS_PIECE_BYTES", str(3 * 96 * 4 + 4))  # many stripes on both streams
     w, h, n = 96, 64, 30
     frames = _frames(w, h, n, 900 + window)
     params = (True, window, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
@@ -409,7 +411,7 @@ def test_resume_rejects_bad_arguments():
         cs.close()
 
 
-def test_handles_on_concurrent_threads(monkeypatch):
+def test_handles_on_concurrent_threads():
     """The ABI's threading contract: a handle is not internally synchronised,
     but distinct handles may be driven from different threads at the same
     time (ctypes drops the GIL during the calls; the staging copies share
@@ -418,8 +420,7 @@ def test_handles_on_concurrent_threads(monkeypatch):
     import threading
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
     from dips_amd.alt import DiPsCompute
-    w, h, n = 256, 192, 14
-    monkeypatch.setenv("DIPS_PIECE_BYTES", str(64 * 1024))  # several stripes: the copy pool runs
+    w, h, n = 256, 192, 14  # 5 stripes per frame: the copy pool runs
     clips = [_frames(w, h, n, 500 + k) for k in range(4)]
     results, errors = {}, []
 
@@ -464,10 +465,10 @@ def test_handles_on_concurrent_threads(monkeypatch):
 @pytest.mark.parametrize("colorize", [False, True])
 @pytest.mark.parametrize("filt", [0, 1, 255])
 @pytest.mark.parametrize("sens", [5.0, -3.0, 0.0, 200.0, 1e-30])
-def test_batch_epilogue_table_equals_arithmetic_and_oracle(colorize, filt, sens, monkeypatch):
+def test_batch_epilogue_table_equals_arithmetic_and_oracle(colorize, filt, sens):
     """compat_batch_lut_kernel (the epilogue as a 65536-entry (S, m) table in
     LDS, the default) against compat_batch_kernel (the per-pixel arithmetic,
-    DIPS_COMPAT_LUT=0) and the oracle, on random frames that reach many (S, m)
+    DIPS_FLAG_CROSSCHECK) and the oracle, on random frames that reach many (S, m)
     pairs, for every filter, negative / zero / huge / tiny sensitivities (the
     inverse sigmoid's inf and NaN texels included) and both colour modes."""
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter
@@ -477,34 +478,32 @@ def test_batch_epilogue_table_equals_arithmetic_and_oracle(colorize, filt, sens,
     params = (colorize, 1, sens, filt, 0)
     want = _oracle_callbacks(frames, params)
     outs = {}
-    for lut in ("1", "0"):
-        monkeypatch.setenv("DIPS_COMPAT_LUT", lut)
-        cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter.None_)
+    for xc in (False, True):
+        cs = ComputeState(colorize, 1, sens, DiPsFilter(filt), ChromaFilter.None_, crosscheck=xc)
         try:
-            outs[lut] = cs.frame_callback_batch(w, h, frames)
+            outs[xc] = cs.frame_callback_batch(w, h, frames)
         finally:
             cs.close()
-    assert np.array_equal(outs["1"], outs["0"]), np.argwhere(outs["1"] != outs["0"])[:4]
-    assert np.array_equal(outs["1"], want), np.argwhere(outs["1"] != want)[:4]
+    assert np.array_equal(outs[False], outs[True]), np.argwhere(outs[False] != outs[True])[:4]
+    assert np.array_equal(outs[False], want), np.argwhere(outs[False] != want)[:4]
 
 
-@pytest.mark.parametrize("defer", ["1", "0"])
+@pytest.mark.parametrize("crosscheck", [False, True])
 @pytest.mark.parametrize("colorize,sens,filt,chroma,window", [(False, 5.0, 255, 0, 1), (True, 0.7, 0, 3, 1),
                                                              (False, 5.0, 255, 0, 4), (True, 5.0, 1, 2, 7)])
-def test_deferred_add_texture_sequences_match_oracle(monkeypatch, defer, colorize, sens, filt, chroma, window):
+def test_deferred_add_texture_sequences_match_oracle(crosscheck, colorize, sens, filt, chroma, window):
     """add_texture in steady state (host frame) stages the frame and starts
     the dispatch that normally follows on it (zero-copy; W > 1: upload,
     spatial filter, then the main kernel); that dispatch collects it, every
     other call first lets it finish and keeps the slot raw.  Mixed call sequences -- add + dispatch,
     two adds without a dispatch, dispatch twice, add then start_texture, add
     then a striped frame_callback, add then a host batch -- give the oracle's
-    outputs and ring state, with the deferral on and off."""
+    outputs and ring state, with the deferral on and off (DIPS_FLAG_CROSSCHECK:
+    no deferral, no zero-copy stripes).  44 x 61 frames: 4 ragged stripes."""
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
-    monkeypatch.setenv("DIPS_DEFER_UPLOAD", defer)
-    monkeypatch.setenv("DIPS_PIECE_BYTES", str(5 * 44 * 4 + 12))  # several ragged stripes
-    w, h = 44, 31
+    w, h = 44, 61
     frames = _frames(w, h, 40, 140 + filt)
-    cs = ComputeState(colorize, window, sens, DiPsFilter(filt), ChromaFilter(chroma))
+    cs = ComputeState(colorize, window, sens, DiPsFilter(filt), ChromaFilter(chroma), crosscheck=crosscheck)
     ref = oracle.ComputeState(colorize, window, sens, filt, chroma)
     t = 0
 

@@ -40,19 +40,20 @@ def _frame(rng, w, h, prev):
 
 
 @pytest.mark.parametrize("size", [(37, 23), (131, 61)])
-@pytest.mark.parametrize("defer", ["1", "0"])
+@pytest.mark.parametrize("crosscheck", [False, True])
 @pytest.mark.parametrize("window", [1, 3])
-def test_random_call_sequences_match_oracle(window, defer, size, monkeypatch):
+def test_random_call_sequences_match_oracle(window, crosscheck, size):
     import torch
     from dips_amd import ChromaFilter, ComputeState, DiPsFilter, frame_callback
     w, h = size
-    monkeypatch.setenv("DIPS_DEFER_UPLOAD", defer)
-    # ragged row stripes (several per frame at 131x61) for the per-frame paths
-    monkeypatch.setenv("DIPS_PIECE_BYTES", str(7 * w * 4 + 12))
-    seed = 1000 * window + 10 * int(defer) + w
+    # ragged row stripes for the per-frame paths: 2 per frame at 37x23, 5 at
+    # 131x61 (host_stream.h piece_bytes); DIPS_FLAG_CROSSCHECK: no deferral,
+    # no zero-copy stripes
+    seed = 1000 * window + 10 * int(crosscheck) + w
     rng = np.random.default_rng(seed)
     props = (True, window, 3.0, 0, 2)  # colorized, sigmoid, green chroma
-    gpu = ComputeState(props[0], window, props[2], DiPsFilter(props[3]), ChromaFilter(props[4]))
+    gpu = ComputeState(props[0], window, props[2], DiPsFilter(props[3]), ChromaFilter(props[4]),
+                       crosscheck=crosscheck)
     ora = oracle.ComputeState(*props)
     ora_dev = oracle.ComputeState(*props)
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]

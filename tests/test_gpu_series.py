@@ -130,10 +130,8 @@ def test_identical_frames_zero():
         assert not m.any()
 
 
-@pytest.mark.parametrize("copies", ["", "0"])  # default (copy kernel uploads) / DMA
-def test_streamed_equals_batch(monkeypatch, copies):
+def test_streamed_equals_batch():
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    monkeypatch.setenv("DIPS_PIPE_KERNEL_COPY", copies)
     frames = _frames(3, 64, 48, 23, 7, "synth")
     ref = _frames(3, 64, 48, 1, 8, "random")[0]
     for mode in (Mode.Overall, Mode.PerFrame):
@@ -374,21 +372,23 @@ def test_unaligned_device_batches(c, mode, offsets, with_map):
             assert (m[:mo] == 0xA5).all() and (m[mo + n * fb:] == 0xA5).all()
 
 
+GRAY_FORMS = [dict(), dict(gray_table="band"), dict(gray_table="pair"), dict(crosscheck=True)]
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.5, 1.0])
-def test_gray_kernels_agree(mode, tau, monkeypatch):
-    """GRAY8 on the table kernel (u16 table keyed by (a ^ b, a) with the band
-    clamp, the default; DIPS_GRAY_LUT=3), the u16 table keyed by (a, b) (=2),
-    its two-byte-table layout (=1) and the f32 series_fast_kernel (=0), with
-    and without the map, against the oracle -- random and synthetic frames,
-    ragged shape included."""
+def test_gray_kernels_agree(mode, tau):
+    """GRAY8 on the table kernel (layout chosen per workgroup from the content,
+    the default), its two tables pinned (DIPS_FLAG_GRAY_BAND_TABLE: keyed by
+    (a ^ b, a) with the band clamp; _PAIR_TABLE: keyed by (a, b)) and the f32
+    series_fast_kernel (DIPS_FLAG_CROSSCHECK), with and without the map,
+    against the oracle -- random and synthetic frames, ragged shape included."""
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     for (w, h), kind in [((256, 64), "random"), ((640, 48), "synth"), ((37, 23), "random")]:
         frames = _frames(1, w, h, 9, 40 + w, kind)
         out4, si, dmap = oracle.series(frames, mode=mode, tau=tau, want_map=True)
-        for layout in ("4", "5", "3", "2", "1", "0"):
-            monkeypatch.setenv("DIPS_GRAY_LUT", layout)
-            op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
+        for form in GRAY_FORMS:
+            op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau, **form)
             try:
                 got, gmap = op(frames, want_map=True)
                 got_nomap, _ = op(frames)
@@ -398,20 +398,19 @@ def test_gray_kernels_agree(mode, tau, monkeypatch):
             _check(got_nomap, out4, si)
 
 
-@pytest.mark.parametrize("layout", ["3", "2", "5"])
+@pytest.mark.parametrize("table", ["band", "pair", "auto"])
 @pytest.mark.parametrize("tau", [0.0, 1 / 255, 8 / 255, 0.1, 0.5, 1.0])
-def test_gray_table_every_byte_pair(tau, layout, monkeypatch):
-    """Every (frame byte a, reference byte b) through the swizzled GRAY8
-    table (layout 3: keyed by (a ^ b, a), indices below the band clamp raised
-    to it; layout 2: keyed by (a, b)), against the oracle: 'overall' against a
-    reference with b = x; frame t = 1..256 holds a = t - 1 everywhere (so each
-    a value is its own series entry), frame 257 holds a = y (all 65,536 pairs
-    in one frame); plus a flat low-noise clip (the content that piles LDS
-    reads onto few banks without a swizzle, and nearly all inside layout 3's
-    band) and a clip whose frames alternate between one flat frame and
-    random ones (a = const against varying b)."""
+def test_gray_table_every_byte_pair(tau, table):
+    """Every (frame byte a, reference byte b) through each GRAY8 table (band:
+    keyed by (a ^ b, a), indices below the band clamp raised to it; pair:
+    keyed by (a, b), swizzled; auto: per workgroup), against the oracle:
+    'overall' against a reference with b = x; frame t = 1..256 holds a = t - 1
+    everywhere (so each a value is its own series entry), frame 257 holds
+    a = y (all 65,536 pairs in one frame); plus a flat low-noise clip (the
+    content that piles LDS reads onto few banks without a swizzle, and nearly
+    all inside the band) and a clip whose frames alternate between one flat
+    frame and random ones (a = const against varying b)."""
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    monkeypatch.setenv("DIPS_GRAY_LUT", layout)
     x = np.arange(256, dtype=np.uint8)
     frames = np.empty((258, 256, 256), dtype=np.uint8)
     frames[0] = x[None, :]
@@ -421,49 +420,16 @@ def test_gray_table_every_byte_pair(tau, layout, monkeypatch):
     flat = np.clip(128 + rng.integers(-3, 4, (12, 64, 512)), 0, 255).astype(np.uint8)
     alt = rng.integers(0, 256, (9, 32, 256), dtype=np.uint8)
     alt[::2] = 77
-    for fr, mode in ((frames, 0), (frames, 1), (flat, 1), (alt, 1), (alt, 0)):
+    bw = np.zeros((7, 64, 256), dtype=np.uint8)
+    bw[1::2] = 255  # every pixel dI = 1: the largest per-lane sums
+    for fr, mode in ((frames, 0), (frames, 1), (flat, 1), (alt, 1), (alt, 0), (bw, 1)):
         out4, si, _ = oracle.series(fr, mode=mode, tau=tau)
-        op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
+        op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau, gray_table=table)
         try:
             got, _ = op(fr)
         finally:
             op.close()
         _check(got, out4, si)
-
-
-@pytest.mark.parametrize("alu,waves", [("1", "12"), ("1", "16"), ("2", "12"), ("2", "16")])
-def test_gray_alu_vecs_match_oracle(alu, waves, monkeypatch):
-    """The GRAY8 table kernel with 1 or 2 of its 4 vecs per lane on the
-    arithmetic path (series_gray.hip gray_alu_dword; DIPS_GRAY_ALU, tau >=
-    2^-5 only) at 12 and 16 waves per group, against the oracle: all 65,536
-    byte pairs, alternating black / white frames (every pixel dI = 1, the
-    largest per-lane sums), random and synthetic clips with a ragged shape,
-    both modes, with and without the map; tau below 2^-5 keeps the table."""
-    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    monkeypatch.setenv("DIPS_GRAY_LUT", "2")  # the arithmetic vecs are a layout-2 option
-    monkeypatch.setenv("DIPS_GRAY_ALU", alu)
-    monkeypatch.setenv("DIPS_GRAY_ALU_WAVES", waves)
-    x = np.arange(256, dtype=np.uint8)
-    pairs = np.empty((258, 256, 256), dtype=np.uint8)
-    pairs[0] = x[None, :]
-    pairs[1:257] = x[:, None, None]
-    pairs[257] = x[:, None]
-    bw = np.zeros((7, 64, 256), dtype=np.uint8)
-    bw[1::2] = 255
-    clips = [pairs, bw, _frames(1, 640, 48, 9, 77, "synth"), _frames(1, 256, 64, 9, 78, "random"),
-             _frames(1, 1000, 37, 6, 79, "random")]
-    for tau in (1 / 32, 8 / 255, 0.5, 1.0, 1 / 64):
-        for fr in clips:
-            for mode in (0, 1):
-                out4, si, dmap = oracle.series(fr, mode=mode, tau=tau, want_map=True)
-                op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau)
-                try:
-                    got, gmap = op(fr, want_map=True)
-                    got_nomap, _ = op(fr)
-                finally:
-                    op.close()
-                _check(got, out4, si, gmap, dmap)
-                _check(got_nomap, out4, si)
 
 
 @pytest.mark.parametrize("c", [1, 3])
@@ -529,20 +495,17 @@ def test_device_calls_ordered_with_torch_default_stream():
         op.close()
 
 
-@pytest.mark.parametrize("isi", ["0", "1", "2"])
+@pytest.mark.parametrize("crosscheck", [False, True])
 @pytest.mark.parametrize("c", [3, 4])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_series_intensity_sum_forms_match_oracle(isi, c, mode, monkeypatch):
-    """The three intensity-sum forms of series_v2 (DIPS_SERIES_ISI: 0 the
-    exact f64 sum, 1 the integer sum with a threshold select, 2 SADI: sums of
-    |x - T| and x, SJ rounded per tile in series_reduce) against the oracle,
-    for tau at and above 2^-5 up to just below 1 (SADI's range) and 1.0
-    (SADI falls back to 1): synthetic and random clips, black / white frames
-    (every pixel dI = 1: the largest per-lane sums), identical frames, a
-    ragged shape and an offset (aligned-load) batch, with and without the
-    map."""
+def test_series_intensity_sum_forms_match_oracle(crosscheck, c, mode):
+    """The two intensity-sum forms of series_v2 (ISI = 1, the integer sum
+    with a threshold select, the default for tau >= 2^-5; ISI = 0, the exact
+    f64 sum, DIPS_FLAG_CROSSCHECK) against the oracle for tau at and above
+    2^-5 up to 1.0: synthetic and random clips, black / white frames (every
+    pixel dI = 1: the largest per-lane sums), identical frames, a ragged shape
+    and an offset (aligned-load) batch, with and without the map."""
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    monkeypatch.setenv("DIPS_SERIES_ISI", isi)
     bw = np.zeros((6, 32, 96, c), dtype=np.uint8)
     bw[1::2] = 255
     same = np.repeat(_frames(c, 96, 32, 1, 5, "random"), 4, axis=0)
@@ -551,7 +514,7 @@ def test_series_intensity_sum_forms_match_oracle(isi, c, mode, monkeypatch):
     below_one = float(np.nextafter(np.float32(1), np.float32(0)))
     for tau in (1 / 32, 8 / 255, 0.3, below_one, 1.0):
         for chroma in (0, 2):
-            op = DiffSeriesOperator(PixelFormat(c), Mode(mode), tau, chroma)
+            op = DiffSeriesOperator(PixelFormat(c), Mode(mode), tau, chroma, crosscheck=crosscheck)
             try:
                 for fr in clips:
                     out4, si, dmap = oracle.series(fr, mode=mode, chroma=chroma, tau=tau, want_map=True)
@@ -569,57 +532,73 @@ def test_series_intensity_sum_forms_match_oracle(isi, c, mode, monkeypatch):
                     op.run_device(dev, ser)
                     torch.cuda.synchronize()
                     out4, _, _ = oracle.series(fr, mode=mode, chroma=chroma, tau=tau)
-                    assert np.array_equal(ser.cpu().numpy().view(np.uint64), out4), (isi, tau, chroma, off)
+                    assert np.array_equal(ser.cpu().numpy().view(np.uint64), out4), (crosscheck, tau, chroma, off)
             finally:
                 op.close()
 
 
+def _split_series(op, dev, parts, ref=None, map_out=None):
+    """The series of `dev` as consecutive batches of < 256 frames each (the
+    contiguous schedule; part_geometry applies from 256 frames), each against
+    its own reference: 'overall' the given one, 'per-frame' the frame before
+    the batch."""
+    import torch
+    from dips_amd import Mode
+    n = dev.shape[0]
+    out = torch.zeros((n, 4), dtype=torch.int64, device=dev.device)
+    bounds = np.linspace(0, n, parts + 1).astype(int)
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        assert b - a < 256
+        r = ref if op.mode == Mode.Overall else (dev[a - 1] if a > 0 else None)
+        op.run_device(dev[a:b], out[a:b], ref=r, map_out=None if map_out is None else map_out[a:b])
+    return out
+
+
 @pytest.mark.parametrize("mode", [0, 1])
-def test_4k_forms_agree_and_match_oracle(mode, monkeypatch):
-    """At the bench's full frame size (4K), the alternative forms of the two
-    series kernels give the same series over a 48-frame batch (a
-    size-independent property): GRAY8 layout 3 (band clamp) = layout 2, and
-    the RGB8 intensity-sum forms ISI = 1 = 2 (SADI) = 0 (f64); the first 4
-    frames of each against the oracle."""
+def test_4k_forms_agree_and_match_oracle(mode):
+    """At the bench's full frame size (4K), the forms of the two series
+    kernels give the same series over a 48-frame batch (a size-independent
+    property): GRAY8 auto = band table = pair table = f32 kernel, RGB8 ISI = 1
+    (integer sum) = ISI = 0 (f64, DIPS_FLAG_CROSSCHECK); the first 4 frames of
+    each against the oracle."""
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     w, h, n, tau = 3840, 2160, 48, 8 / 255
-    for fmt, env, forms in ((PixelFormat.Gray8, "DIPS_GRAY_LUT", ("4", "5", "3", "2")),
-                            (PixelFormat.RGB8, "DIPS_SERIES_ISI", ("1", "2", "0"))):
+    for fmt, forms in ((PixelFormat.Gray8, GRAY_FORMS), (PixelFormat.RGB8, [dict(), dict(crosscheck=True)])):
         c = int(fmt)
         shape = (n, h, w) if c == 1 else (n, h, w, c)
-        op = DiffSeriesOperator(fmt, Mode(mode), tau, 0)
-        try:
-            dev = torch.empty(shape, dtype=torch.uint8, device="cuda")
-            op.synth_device(dev, w, h, 0xD1B5, 7)
-            got = {}
-            for form in forms:
-                monkeypatch.setenv(env, form)
+        dev = torch.empty(shape, dtype=torch.uint8, device="cuda")
+        got = []
+        for k, form in enumerate(forms):
+            op = DiffSeriesOperator(fmt, Mode(mode), tau, 0, **form)
+            try:
+                if k == 0:
+                    op.synth_device(dev, w, h, 0xD1B5, 7)
                 ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
                 op.run_device(dev, ser)
                 torch.cuda.synchronize()
-                got[form] = ser.cpu().numpy().view(np.uint64)
-            monkeypatch.delenv(env)
-            for form in forms[1:]:
-                assert np.array_equal(got[form], got[forms[0]]), (fmt, form)
-            head = dev[:4].cpu().numpy()
-            out4, _, _ = oracle.series(head, mode=mode, tau=tau, nthreads=8)
-            assert np.array_equal(got[forms[0]][:4], out4), fmt
-        finally:
-            op.close()
+                got.append(ser.cpu().numpy().view(np.uint64))
+            finally:
+                op.close()
+        for k in range(1, len(forms)):
+            assert np.array_equal(got[k], got[0]), (fmt, forms[k])
+        head = dev[:4].cpu().numpy()
+        out4, _, _ = oracle.series(head, mode=mode, tau=tau, nthreads=8)
+        assert np.array_equal(got[0][:4], out4), fmt
 
 
 @pytest.mark.parametrize("fmt_name,w,h,n", [("RGB8", 1920, 1080, 523), ("RGBA8", 1920, 1080, 525),
                                              ("Gray8", 2048, 1536, 1000)])
-def test_part_major_schedule_matches_contiguous_and_oracle(fmt_name, w, h, n, monkeypatch):
+def test_part_major_schedule_matches_contiguous_and_oracle(fmt_name, w, h, n):
     """'Per-frame' batches of >= 256 frames run the part-major schedule
-    (dips_abi.hip part_geometry; series_v2.hip / series_gray.hip item loop).
+    (series_abi.hip part_geometry; series_v2.hip / series_gray.hip item loop).
     These shapes take it on a 256-CU MI355X: 1080p RGB8 4 parts of 131
     frames (the last 130), RGBA8 4 parts of 132 (the last 129), 2048x1536
     gray8 7 parts of 143 (the last 142), so items start mid-batch, segments
-    end in 0- to 3-frame tails and the last part is short.  The series (and the |F - R| map for RGB8)
-    must equal the contiguous schedule's (DIPS_SERIES_PARTS=0) bit for bit,
-    and every frame must match the oracle."""
+    end in 0- to 3-frame tails and the last part is short.  The series (and
+    the |F - R| map for RGB8) must equal the contiguous schedule's -- the same
+    frames as batches of < 256, each against the frame before it -- bit for
+    bit, and every frame must match the oracle."""
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     fmt = getattr(PixelFormat, fmt_name)
@@ -630,50 +609,41 @@ def test_part_major_schedule_matches_contiguous_and_oracle(fmt_name, w, h, n, mo
     try:
         dev = torch.empty(shape, dtype=torch.uint8, device="cuda")
         op.synth_device(dev, w, h, 0xA11CE, 3)
-        got, maps = {}, {}
-        for parts in ("1", "0"):
-            monkeypatch.setenv("DIPS_SERIES_PARTS", parts)
-            ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-            dmap = torch.empty_like(dev) if want_map else None
-            op.run_device(dev, ser, map_out=dmap)
-            torch.cuda.synchronize()
-            got[parts] = ser.cpu().numpy().view(np.uint64)
-            if want_map:
-                maps[parts] = dmap
-        monkeypatch.delenv("DIPS_SERIES_PARTS")
-        assert np.array_equal(got["1"], got["0"])
+        ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+        dmap = torch.empty_like(dev) if want_map else None
+        op.run_device(dev, ser, map_out=dmap)
+        cmap = torch.empty_like(dev) if want_map else None
+        cser = _split_series(op, dev, 5 if n < 1000 else 8, map_out=cmap)
+        torch.cuda.synchronize()
+        got = ser.cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, cser.cpu().numpy().view(np.uint64))
         if want_map:
-            assert torch.equal(maps["1"], maps["0"])
+            assert torch.equal(dmap, cmap)
         frames = dev.cpu().numpy()
         out4, _, omap = oracle.series(frames, mode=1, tau=tau, want_map=want_map, nthreads=16)
-        bad = np.nonzero(~np.all(got["1"] == out4, axis=1))[0]
+        bad = np.nonzero(~np.all(got == out4, axis=1))[0]
         assert bad.size == 0, f"frames differing from the oracle: {bad[:10]}"
         if want_map:
-            assert np.array_equal(maps["1"].cpu().numpy(), omap)
+            assert np.array_equal(dmap.cpu().numpy(), omap)
     finally:
         op.close()
 
 
-@pytest.mark.parametrize("frac", ["0", "2", None])
+@pytest.mark.parametrize("table", ["band", "pair", "auto"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_gray_auto_layout_branches_match_oracle(frac, mode, monkeypatch):
+def test_gray_auto_layout_branches_match_oracle(table, mode):
     """GRAY8 table layout 4 (the default): one kernel whose workgroups each
     take layout 5 (band clamp) or layout 2 from a sample of their own first
-    items.  DIPS_GRAY_AUTO_FRAC=0 forces the layout-5 branch, 2 the
-    layout-2 branch, unset the content's own choice -- every branch against
-    the oracle on synthetic, random, identical and ragged clips, tau 0 / 8/255
-    / 0.5, with and without the map, one-frame batches included."""
+    items; DIPS_FLAG_GRAY_BAND_TABLE / _PAIR_TABLE pin one branch -- every
+    branch against the oracle on synthetic, random, identical and ragged
+    clips, tau 0 / 8/255 / 0.5, with and without the map, one-frame batches
+    included."""
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    if frac is None:
-        monkeypatch.delenv("DIPS_GRAY_AUTO_FRAC", raising=False)
-    else:
-        monkeypatch.setenv("DIPS_GRAY_AUTO_FRAC", frac)
-    monkeypatch.delenv("DIPS_GRAY_LUT", raising=False)
     same = np.repeat(_frames(1, 256, 64, 1, 9, "random"), 5, axis=0)
     clips = [_frames(1, 256, 64, 9, 41, "synth"), _frames(1, 256, 64, 9, 42, "random"), same,
              _frames(1, 1000, 37, 6, 43, "random"), _frames(1, 512, 32, 1, 44, "synth")]
     for tau in (0.0, 8 / 255, 0.5):
-        op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau, 0)
+        op = DiffSeriesOperator(PixelFormat.Gray8, Mode(mode), tau, 0, gray_table=table)
         try:
             for fr in clips:
                 out4, si, dmap = oracle.series(fr, mode=mode, tau=tau, want_map=True)
@@ -686,15 +656,13 @@ def test_gray_auto_layout_branches_match_oracle(frac, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode,n", [(0, 40), (1, 300)])
-def test_gray_auto_mixed_content_per_workgroup(mode, n, monkeypatch):
+def test_gray_auto_mixed_content_per_workgroup(mode, n):
     """Layout 4 decides per workgroup, so one launch can run both tables: a
     2048 x 512 clip whose row bands are flat noise (128 +- 3: layout 2),
     slowly varying synthetic content and i.i.d. random bytes, 'overall' (40
     frames, contiguous ranges) and 'per-frame' (300 frames, the part-major
     schedule) -- every frame and the map equal to the oracle."""
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    monkeypatch.delenv("DIPS_GRAY_AUTO_FRAC", raising=False)
-    monkeypatch.delenv("DIPS_GRAY_LUT", raising=False)
     rng = np.random.default_rng(77 + mode)
     w, h = 2048, 512
     fr = oracle.synth(1, w, h, 0xD1B5, 0, n)
@@ -709,34 +677,29 @@ def test_gray_auto_mixed_content_per_workgroup(mode, n, monkeypatch):
         op.close()
 
 
-@pytest.mark.parametrize("fmt_name,env", [("RGB8", {}), ("RGBA8", {}), ("Gray8", {}), ("Gray8", {"DIPS_GRAY_LUT": "0"}),
-                                          ("RGB8", {"DIPS_SERIES_KZERO": "0"})])
-def test_series_starts_from_zero_on_a_dirty_buffer(fmt_name, env, monkeypatch):
+@pytest.mark.parametrize("fmt_name,form", [("RGB8", {}), ("RGBA8", {}), ("Gray8", {}),
+                                           ("Gray8", {"crosscheck": True}), ("RGB8", {"force_generic": True})])
+def test_series_starts_from_zero_on_a_dirty_buffer(fmt_name, form):
     """The RGB(A) and GRAY8 table kernels clear the caller's series
     themselves (SeriesArgs::zero, no fill launch); the f32 GRAY8 kernel
-    (DIPS_GRAY_LUT=0) and DIPS_SERIES_KZERO=0 after a fill.  A series tensor
-    full of garbage, twice in a row, must come out equal to the oracle -- at
-    300 frames (part-major, the adaptive reduce grid) and 3 frames."""
+    (DIPS_FLAG_CROSSCHECK) and the generic kernel after a fill.  A series
+    tensor full of garbage, twice in a row, must come out equal to the oracle
+    -- at 300 frames (part-major, the adaptive reduce grid) and 3 frames."""
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    for k in ("DIPS_GRAY_LUT", "DIPS_SERIES_KZERO"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    lut = env
     fmt = getattr(PixelFormat, fmt_name)
     c = int(fmt)
     for n, w, h in ((300, 256, 96), (3, 640, 480)):
         frames = _frames(c, w, h, n, 5 + n, "synth")
         want, _, _ = oracle.series(frames, mode=1, tau=8 / 255, nthreads=8)
-        op = DiffSeriesOperator(fmt, Mode.PerFrame, 8 / 255, 0)
+        op = DiffSeriesOperator(fmt, Mode.PerFrame, 8 / 255, 0, **form)
         try:
             dev = torch.from_numpy(frames).cuda()
             ser = torch.full((n, 4), 0x5A5A5A5A5A5A5A5A, dtype=torch.int64, device="cuda")
             for _ in range(2):
                 op.run_device(dev, ser)
                 torch.cuda.synchronize()
-                assert np.array_equal(ser.cpu().numpy().view(np.uint64), want), (fmt_name, lut, n)
+                assert np.array_equal(ser.cpu().numpy().view(np.uint64), want), (fmt_name, form, n)
                 ser.fill_(-1)
         finally:
             op.close()
@@ -767,12 +730,11 @@ def test_reduce_grid_for_few_large_frames(fmt_name, n):
 
 
 @pytest.mark.parametrize("fmt_name,w,h,n", [("RGB8", 1920, 1080, 523), ("RGBA8", 1920, 1080, 525)])
-def test_part_major_overall_matches_contiguous_and_oracle(fmt_name, w, h, n, monkeypatch):
-    """'Overall' batches on the part-major schedule (the default since round
-    4, DIPS_SERIES_PARTS=2 forces it: each item loads the fixed reference
-    tile at its part's first frame) --
-    series and map equal to the contiguous schedule's and every frame equal
-    to the oracle."""
+def test_part_major_overall_matches_contiguous_and_oracle(fmt_name, w, h, n):
+    """'Overall' batches on the part-major schedule (each item loads the
+    fixed reference tile at its part's first frame) -- series and map equal
+    to the contiguous schedule's (the same frames as batches of < 256 against
+    the same reference) and every frame equal to the oracle."""
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     fmt = getattr(PixelFormat, fmt_name)
@@ -782,19 +744,17 @@ def test_part_major_overall_matches_contiguous_and_oracle(fmt_name, w, h, n, mon
         dev = torch.empty((n, h, w, c), dtype=torch.uint8, device="cuda")
         op.synth_device(dev, w, h, 0xB0B, 11)
         ref = dev[0].clone()
-        got, maps = {}, {}
-        for parts in ("2", "0"):
-            monkeypatch.setenv("DIPS_SERIES_PARTS", parts)
-            ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
-            dmap = torch.empty_like(dev)
-            op.run_device(dev, ser, ref=ref, map_out=dmap)
-            torch.cuda.synchronize()
-            got[parts], maps[parts] = ser.cpu().numpy().view(np.uint64), dmap
-        monkeypatch.delenv("DIPS_SERIES_PARTS")
-        assert np.array_equal(got["2"], got["0"])
-        assert torch.equal(maps["2"], maps["0"])
+        ser = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+        dmap = torch.empty_like(dev)
+        op.run_device(dev, ser, ref=ref, map_out=dmap)
+        cmap = torch.empty_like(dev)
+        cser = _split_series(op, dev, 5, ref=ref, map_out=cmap)
+        torch.cuda.synchronize()
+        got = ser.cpu().numpy().view(np.uint64)
+        assert np.array_equal(got, cser.cpu().numpy().view(np.uint64))
+        assert torch.equal(dmap, cmap)
         out4, _, _ = oracle.series(dev.cpu().numpy(), mode=0, tau=tau, ref=ref.cpu().numpy(), nthreads=16)
-        bad = np.nonzero(~np.all(got["2"] == out4, axis=1))[0]
+        bad = np.nonzero(~np.all(got == out4, axis=1))[0]
         assert bad.size == 0, f"frames differing from the oracle: {bad[:10]}"
     finally:
         op.close()

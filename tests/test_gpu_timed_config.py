@@ -3,7 +3,7 @@ frame (BASELINE.json configs[2]: 3840x2160 RGB8, 'per-frame', tau = 8/255,
 the default intensity-sum form ISI = 1 -- series_v2_kernel<3, 0, 4, true,
 false, false, 1>).
 
-The bench's 5000-frame batch runs the part-major schedule (dips_abi.hip
+The bench's 5000-frame batch runs the part-major schedule (series_abi.hip
 part_geometry: 5 parts of 1000 frames); a 520-frame batch of the same frames
 runs it with 3 parts of 174 frames (the last 172) on a 256-CU MI355X, so
 items start mid-batch and the last part is short -- asserted through the
@@ -52,20 +52,16 @@ def _series_vs_oracle(fmt_name, mode, n, offset=0, t0=0):
 
 @pytest.mark.timeout(600)
 def test_timed_config_per_frame_part_major_every_frame(monkeypatch):
-    monkeypatch.delenv("DIPS_SERIES_ISI", raising=False)
-    monkeypatch.delenv("DIPS_SERIES_PARTS", raising=False)
     monkeypatch.delenv("DIPS_SERIES_WAVES_PER_SIMD", raising=False)
     sch = _series_vs_oracle("RGB8", 1, 520)
     assert sch is not None and sch[1] >= 3, sch  # part-major, >= 3 parts
 
 
 @pytest.mark.timeout(600)
-def test_timed_config_overall_every_frame(monkeypatch):
-    monkeypatch.delenv("DIPS_SERIES_ISI", raising=False)
+def test_timed_config_overall_every_frame():
     _series_vs_oracle("RGB8", 0, 300, t0=17)
 
 
 @pytest.mark.timeout(600)
-def test_timed_config_rgba8_offset2_every_frame(monkeypatch):
-    monkeypatch.delenv("DIPS_SERIES_ISI", raising=False)
+def test_timed_config_rgba8_offset2_every_frame():
     _series_vs_oracle("RGBA8", 1, 300, offset=2, t0=5)

@@ -66,14 +66,13 @@ int main() {
     for (auto& b : src) b = (uint8_t)rng();
     const size_t sizes[] = {0, 1, 31, 32, 127, 128, 129, 65535, 65536, 65537, 1u << 20, (4u << 20) + 77, 9u << 20};
     int bad = 0;
-    for (int nt = 0; nt < 2; ++nt) {
-        setenv("DIPS_NT_COPY", nt ? "1" : "0", 1);
+    for (int rep = 0; rep < 2; ++rep) {
         for (size_t n : sizes)
             for (size_t so = 0; so < 4; ++so)
                 for (size_t dof = 0; dof < 40; dof += 13) {
                     if (so + n > src.size() || dof + n + 8 > dst.size()) continue;
                     std::fill(dst.begin(), dst.end(), 0xA5);
-                    dips_host::host_copy(dst.data() + dof, src.data() + so, n, dips_host::nt_copy());
+                    dips_host::host_copy(dst.data() + dof, src.data() + so, n);
                     for (size_t i = 0; i < dof; ++i) bad += dst[i] != 0xA5;
                     bad += std::memcmp(dst.data() + dof, src.data() + so, n) != 0;
                     for (size_t i = dof + n; i < dof + n + 8; ++i) bad += dst[i] != 0xA5;
@@ -113,19 +112,24 @@ _GEOM_CHECK = r"""
 #include <string>
 int main() {
     int bad = 0, cases = 0;
-    const size_t pieces[] = {64, 1000, 4096, 1u << 20, 4u << 20, 8u << 20};
-    const uint32_t heights[] = {1, 2, 3, 7, 29, 1080, 2160};
-    const size_t rows[] = {4, 160, 164, 7680, 15360};
-    const char* splits[] = {"1", "3", "8", "64"};
-    const char* firsts[] = {"0", "1"};
-    for (size_t pb : pieces) for (uint32_t hgt : heights) for (size_t row : rows) for (const char* sp : splits)
-    for (const char* fr : firsts) {
-        setenv("DIPS_PIECE_BYTES", std::to_string(pb).c_str(), 1);
-        setenv("DIPS_DIRECT_SPLIT", sp, 1);
-        setenv("DIPS_DIRECT_FIRST", fr, 1);
+    const uint32_t heights[] = {1, 2, 3, 7, 29, 48, 480, 1080, 2160, 4320};
+    const size_t rows[] = {4, 160, 164, 2560, 7680, 15360, 30720};
+    // piece sizes: 4 MiB from 4 MiB frames up, quarters (>= 4 KiB, 64-B
+    // multiples) below
+    for (size_t fb : {(size_t)1, (size_t)4096, (size_t)12288, (size_t)1228800, (size_t)((4u << 20) - 1),
+                      (size_t)(4u << 20), (size_t)33177600}) {
+        const size_t pb = dips_host::piece_bytes(fb);
+        ++cases;
+        if (pb % 64 != 0 || pb < 4096 || pb > (4u << 20) || (fb >= (4u << 20) && pb != (4u << 20))) ++bad;
+        if (fb >= 16384 && fb < (4u << 20) && (fb + pb - 1) / pb < 4) ++bad;
+    }
+    for (uint32_t hgt : heights) for (size_t row : rows) {
         dips_host::DirectGeom g;
         g.init(hgt, row);
         ++cases;
+        if (g.k != dips_host::kDirectSplit) ++bad;
+        // a frame of at least 16 KiB is cut into several stripes
+        if ((size_t)hgt * row >= 16384 && hgt >= 8 && g.n_s < 2) ++bad;
         // stripes cover [0, height) in order, each non-empty
         uint32_t y = 0;
         for (uint32_t si = 0; si < g.n_s; ++si) {
@@ -153,11 +157,12 @@ int main() {
 
 
 def test_zero_copy_stripe_geometry(tmp_path):
-    """host_stream.h DirectGeom (the zero-copy per-frame pipeline): for every
-    stripe size, frame height, row size, copy-pool split and first-stripe
-    setting, the stripes cover the frame's rows in order with none empty, and
-    each stripe's pieces cover its bytes exactly with cuts 64-B aligned
-    inside the stripe."""
+    """host_stream.h piece_bytes and DirectGeom (the zero-copy per-frame
+    pipeline): 4 MiB pieces from 4 MiB frames up, at least four pieces of a
+    smaller frame; for every frame height and row size the stripes cover the
+    frame's rows in order with none empty (several for any frame of 16 KiB or
+    more), and each stripe's pieces cover its bytes exactly with cuts 64-B
+    aligned inside the stripe."""
     import os
     import shutil
     import subprocess
@@ -276,17 +281,13 @@ def test_pack_frame_for_the_zero_copy_input(tmp_path):
     assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout + r.stderr
 
 
-def test_bench_kernel_name_matches_library_choice(monkeypatch):
+def test_bench_kernel_name_matches_library_choice():
     """bench.py names the series_v2 instantiation the library runs, spelled
     as rocprofv3 prints it (ISI an int): run_series_device's choice of the
-    intensity-sum form."""
+    intensity-sum form (series_abi.hip series_isi_form)."""
     import bench
-    monkeypatch.delenv("DIPS_SERIES_ISI", raising=False)
     assert bench._v2_kernel_name(True, 8 / 255) == "series_v2_kernel<3, 0, 4, true, false, false, 1>"
     assert bench._v2_kernel_name(False, 8 / 255, with_map=True) == "series_v2_kernel<3, 0, 4, false, true, false, 1>"
+    assert bench._v2_kernel_name(True, 0.0) == "series_v2_kernel<3, 0, 4, true, false, false, 0>"
     assert bench._series_isi(0.0) == 0 and bench._series_isi(0.03) == 0 and bench._series_isi(1 / 32) == 1
     assert bench._series_isi(1.0) == 1
-    monkeypatch.setenv("DIPS_SERIES_ISI", "2")
-    assert bench._series_isi(8 / 255) == 2 and bench._series_isi(1.0) == 1
-    monkeypatch.setenv("DIPS_SERIES_ISI", "0")
-    assert bench._series_isi(8 / 255) == 0

@@ -197,3 +197,36 @@ def test_crate_files_and_integration_doc():
                 "pub fn dispatch(&mut self) -> Option<Vec<u8>>",
                 "pub fn frame_callback(width: u32, height: u32, frame_data: &[u8], compute: &mut ComputeState) -> Vec<u8>"):
         assert sig in lib, sig
+
+
+def _fn_body(src, sig):
+    """The body of the Rust fn whose signature starts with `sig` (brace matched)."""
+    i = src.index(sig)
+    j = src.index("{", i)
+    depth = 0
+    for k in range(j, len(src)):
+        depth += {"{": 1, "}": -1}.get(src[k], 0)
+        if depth == 0:
+            return src[j:k + 1]
+    raise AssertionError("unbalanced braces after " + sig)
+
+
+def test_failures_are_visible_at_the_rust_boundary():
+    """a device error must not look like the warm-up.
+    `try_dispatch` returns every failure; `dispatch` (the reference's
+    signature, gpu/mod.rs:306-397) gives None only for the warm-up and panics
+    on a negative status like the reference's wgpu path; `frame_callback`
+    (lib.rs:233-246) panics instead of passing the input through."""
+    lib = open(os.path.join(CRATE, "src", "lib.rs")).read()
+    assert "pub fn try_dispatch(&mut self) -> Result<Option<Vec<u8>>, DipsError>" in lib
+    assert "pub fn try_start_texture(&mut self) -> Result<Option<Vec<u8>>, DipsError>" in lib
+    body = _fn_body(lib, "pub fn try_dispatch(")
+    assert "check(r, self.h.as_ptr())?" in body  # negative status -> Err before the 1/0 match
+    body = _fn_body(lib, "pub fn dispatch(&mut self)")
+    assert "self.try_dispatch()" in body and "panic!" in body
+    body = _fn_body(lib, "pub fn frame_callback(width: u32")
+    assert "panic!" in body and "frame_data.to_vec()" not in body
+    ffi = open(FFI).read()
+    assert "pub const DIPS_ERR_INTERNAL: DipsStatus = -7;" in ffi
+    assert "pub const DIPS_ABI_VERSION: c_int = 2;" in ffi
+    assert "pub const DIPS_FLAG_CROSSCHECK: u32 = 0x8;" in ffi
