@@ -563,7 +563,7 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
     lib, hd = cs._hd._lib, cs._hd
     # every call writes its own output buffer (a caller's ring of frames),
     # faulted in before the timed calls; all outputs are compared after the
-    # loop (a compare between calls measured 0.85-0.9x, tools/pfc_variants.py)
+    # loop (a compare between calls measured 0.85-0.9x in round 4)
     outs = np.empty_like(host)
     outs.fill(0)
     times, phases = [], []

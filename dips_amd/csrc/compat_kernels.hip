@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void compat_main_kernel(CompatArgs a) {
 // One thread per pixel over the rows' pixel range, so that a wave moves 256
 // contiguous bytes each way.  (Four pixels per thread through 16-B
 // system-coherent buffer loads / stores measured slower: 557-575 against
-// 695-701 frames/s of 4K per-frame calls, tools/callback_direct_ab.py.)
+// 695-701 frames/s of 4K per-frame calls, profiles/r02_callback_direct_ab_vec.jsonl.)
 //
 // The output goes back as the RGBA8 texel (out_key 0) or as its key
 // (out_key 1 / 2): every texel of visual_epilogue has A = 255, gray has

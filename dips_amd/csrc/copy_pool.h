@@ -144,7 +144,7 @@ class CopyPool {
         // After a per-frame run, watch for the next one for 200 us before
         // parking on the condition variable: back-to-back per-frame calls then
         // find the workers awake on warm cores.  Measured over four alternated
-        // rounds of 200 4K frame_callback calls (tools/pfc_threads_ab.py,
+        // rounds of 200 4K frame_callback calls (round 4,
         // profiles/r04/k/): 1,689-1,837 frames/s (p90 0.56-0.63 ms) against
         // 1,363-1,687 (p90 0.61-0.88 ms) parking at once; the pool's own
         // pack / expand thread time drops too (1.6-1.8 vs 1.9-2.5 ms per

@@ -125,7 +125,7 @@ struct CompatBatchArgs {
 };
 constexpr int kUnrollCompatBatch = 2;
 // U vecs per lane and D frames of loads in flight per wave of the table
-// kernel.  In one process over one batch (tools/compat_variant_ab.py,
+// kernel.  In one process over one batch (round 2,
 // profiles/r02_compat_variant_ab.jsonl) U = 4, D = 3 ran 76.2 % of 8 TB/s
 // read + write, against 72.4 % for U = 2, D = 2 (an earlier cross-process
 // A/B had called U = 4 equal).  126 VGPRs: the 1024-thread workgroup's
@@ -145,7 +145,7 @@ hipError_t launch_compat_batch(const CompatBatchArgs& a, int chroma, int filter,
 constexpr int kAltMaxTextures = 16;  // MAX_TEMPORAL_ARRAY_SIZE (dips_alt pre_compute_shader.wgsl:12)
 constexpr int kUnrollAlt = 2;        // vecs (4 px) per lane of alt_batch_kernel
 // vecs per lane / frames of loads in flight of its epilogue-table form.  In one process
-// over one batch (tools/alt_variant_ab.py, profiles/r02_alt_variant_ab.jsonl):
+// over one batch (round 2, profiles/r02_alt_variant_ab.jsonl):
 // U = 4, D = 2 72.8 % of 8 TB/s read + write, U = 2, D = 2 72.1 %, the others
 // 71.2-72.3 % (8 groups of 256 threads per CU already keep enough in flight).
 constexpr int kUnrollAltLut = 4;

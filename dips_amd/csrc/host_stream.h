@@ -33,7 +33,7 @@ namespace dips_host {
 // Chunk copies of the host-fed pipelines between a pinned buffer and HBM: a
 // copy kernel (system-scope accesses to the pinned side) or hipMemcpyAsync
 // (a DMA engine), per call site.  Measured in one process
-// (tools/nt_copy_ab.py): the streamed series' uploads by kernel ran
+// (profiles/r02_pipe_kernel_copy_ab_box*.jsonl): the streamed series' uploads by kernel ran
 // 1.00-1.15x the DMA rate (`kernel` there), the visual operators' two-way
 // pipe 0.81-0.82x with a kernel upload (DMA kept).
 inline hipError_t pipe_h2d(void* dev, const void* pin, size_t bytes, hipStream_t s, bool kernel = false) {

@@ -89,7 +89,7 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
     const int ppv = dips::pixels_per_vec(C);
     // any alignment and pixel count: the vectorised kernel takes the whole
     // vecs of every frame (unaligned frames through unaligned buffer loads,
-    // exact on gfx950: tools/unaligned_probe.hip), the generic kernel the
+    // exact on gfx950: tests/test_gpu_series.py::test_unaligned_device_batches), the generic kernel the
     // < ppv trailing pixels
     const uint64_t nvec = npx / (uint64_t)ppv;
     if (nvec == 0 || fb >= (1ull << 31) || n_frames == 0) return g;
@@ -117,7 +117,7 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
 // the sampled pixels and either kGrayAutoHi of them or the sampled waves'
 // frame bytes span kGrayAutoSpread levels on average, else layout 2.  From
 // the layouts measured in one process over five 4K contents
-// (tools/gray_layout_ab.py, profiles/r04/d/gray_layout_ab.jsonl; band
+// (profiles/r04/d/gray_layout_ab.jsonl; band
 // fraction / mean spread of a wave's 1024 pixels; % of 8 TB/s):
 //   synthetic (0.64 / 247): layout 5 71.8-72.3, 3 64-70, 2 63-66;
 //   random (0.03 / 248): 2 61-63, 5 62-63, 3 60;
@@ -388,7 +388,7 @@ dips_status dips_diff_series_streamed(dips_handle* h, uint32_t width, uint32_t h
             // ring[b] was read by kernel k-3 (frames) and kernel k-2 (per-frame ref)
             if (k >= 2) DIPS_HIP(h, hipStreamWaitEvent(h->copy_stream, h->kernel_done[(k - 2) % 3u], 0));
             // the upload by a copy kernel (1.00-1.15x the DMA engine's rate here,
-            // tools/nt_copy_ab.py)
+            // profiles/r02_pipe_kernel_copy_ab_boxA.jsonl)
             DIPS_HIP(h, dips_host::pipe_h2d(h->ring[b].p, h->pinned[hb].p, (size_t)nk * fb, h->copy_stream, true));
             DIPS_HIP(h, hipEventRecord(h->copy_done[b], h->copy_stream));
             DIPS_HIP(h, hipStreamWaitEvent(h->stream, h->copy_done[b], 0));

@@ -15,7 +15,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // gfx950 buffer-resource flags word (raw buffer, 32-bit format).
 constexpr int kRsrcFlags = 0x00020000;
 // cache policy of the streamed frame loads: nt (stream once).  Probe builds
-// (tools/policy_probe.hip) override it to compare policies.
+// (round 2, profiles/r02_policy_energy.jsonl) overrode it to compare policies.
 #ifndef DIPS_LOAD_AUX
 #define DIPS_LOAD_AUX 2
 #endif

@@ -42,7 +42,7 @@ constexpr uint32_t kGrayV = 8421504u;          // V = kGrayV * d + corr
 // reference is smooth (b within a few levels across the 32 lanes of a half)
 // the lanes pile onto 2-4 banks: 4K gray8 with flat +-3 noise ran at 39 %
 // of 8 TB/s against 65 % on the bench's random-base frames
-// (tools/content_rate.py, profiles/r02_content_rate.jsonl).  XOR-ing the low
+// (profiles/r02_content_rate.jsonl).  XOR-ing the low
 // four bits of a into bank bits 2-5 spreads such boxes of (a, b) over the
 // banks (bank-conflict simulation: flat +-3 12.2 -> 3.9 LDS cycles per
 // read, random unchanged at 7.1) and costs two VALU per four pixels (the
@@ -325,7 +325,7 @@ __device__ __forceinline__ void gray_walk(const SeriesArgs& a, const uint8_t* ld
 // but few conflicts on such narrow content.  So: layout 5 when the band holds
 // >= probe_min / 1024 of the sampled pixels and either nearly all of them
 // (probe_hi / 1024) or the waves' bytes spread over >= probe_spread levels on
-// average, else layout 2 (tools/gray_layout_ab.py over five contents,
+// average, else layout 2 (measured over five contents,
 // profiles/r04/d/).  Until round 4's last pass a separate probe kernel took
 // one sample per launch; sampling inside the kernel drops that launch and its
 // fill (11-12 us of a 640x480 x 300-frame batch, profiles/r04/small/) and

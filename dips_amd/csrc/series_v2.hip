@@ -3,7 +3,7 @@
 // Same contract as series_fast_kernel (series_kernels.hip): per (tile, frame)
 // one 16-byte record of wave sums {SAD, SJ + count << 20, H, L}, summed per
 // frame by series_reduce_kernel.  What differs is how the work is shaped for
-// the CDNA4 VALU (measured issue costs: tools/vbench.hip, profiles/):
+// the CDNA4 VALU (measured issue costs: tools/gen_vbench.py, profiles/):
 //
 //  * intensity without conversions: with J = max+min (integer, needed for SJ
 //    anyway) and E = P(max) + P(min), P(c) = the largest power of two <= c,
@@ -180,7 +180,7 @@ __device__ __forceinline__ void funnel(uint32_t (&v)[L], uint32_t sh) {
 
 // The kernel body; AUX / SAUX are the cache-policy bits of the frame loads /
 // map stores (the library kernel below uses nt; probe builds instantiate
-// other policies to compare them in one process, tools/aux_ab.hip).
+// other policies to compare them in one process; profiles/r02_aux_ab_load.txt).
 // Schedule: a.part_frames == 0 (and SCHED 0) -- one contiguous (tile, frame)
 // range per wave; a.part_frames = L > 0 (or SCHED 1, probe builds) -- the
 // frames cut into parts of L, items (part, tile) taken part-major with

@@ -32,7 +32,7 @@ static double now() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-__global__ __launch_bounds__(256, (v2_min_waves<3, kUnrollV2, true, false, false, 1>())) void parts_isi(SeriesArgs a) {
+__global__ __launch_bounds__(256, (v2_min_waves<3, kUnrollV2, true, false, false>())) void parts_isi(SeriesArgs a) {
     series_v2_body<3, 0, kUnrollV2, true, false, kAuxNT, kAuxNT, 1, false, 1>(a);
 }
 

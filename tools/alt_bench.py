@@ -41,7 +41,6 @@ def main():
     ap.add_argument("--kernel", choices=["lut", "arith"], default="lut",
                     help="lut: alt_batch_kernel with the epilogue table (default); arith: per-pixel epilogue")
     args = ap.parse_args()
-    os.environ["DIPS_ALT_LUT"] = "1" if args.kernel == "lut" else "0"
 
     import torch
     from dips_amd import DiffSeriesOperator, PixelFormat
@@ -55,7 +54,7 @@ def main():
     op.close()
     out = torch.empty_like(frames)
     flags = [t == 2 for t in range(F)]
-    c = DiPsCompute(2, H, W, time_kernel=True)
+    c = DiPsCompute(2, H, W, time_kernel=True, crosscheck=args.kernel == "arith")
     for _ in range(args.warmup):
         c.send_frames_device(frames, out, flags)
     torch.cuda.synchronize()

@@ -1,7 +1,8 @@
 // altcheck.hip -- exhaustive device check of dips_amd/csrc/epilogue_fast.h
 // against the specification functions of dips_math.h (which the CPU oracle
-// states identically).  Build: make -C tools altcheck  (or the hipcc line in
-// tools/gpu_alt.sh); run on the GPU box: build/altcheck
+// states identically).  Build: hipcc --offload-arch=gfx950 -O3
+// -ffp-contract=off -std=c++17 -o build/altcheck tools/altcheck.hip; run on the
+// GPU box: build/altcheck
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>

@@ -30,22 +30,20 @@ CONFIGS = [
     ("extra: 3840x2160 gray8, 15000 frames, per-frame", 3840, 2160, 1, 15000, 1, 8 / 255),
 ]
 
-_GRAY_NAMES = {"0": "f32", "1": "lut8", "2": "lut16", "3": "band", "4": "auto", "5": "band5"}
+# GRAY8 kernel forms: the table kernel with its per-workgroup layout choice
+# (the default), either table pinned (DIPS_FLAG_GRAY_*_TABLE), or the f32
+# series_fast_kernel (DIPS_FLAG_CROSSCHECK)
+_GRAY_FORMS = {"auto": {}, "band": {"gray_table": "band"}, "pair": {"gray_table": "pair"}, "f32": {"crosscheck": True}}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--only", default="", help="run the configs whose name contains this string")
-    ap.add_argument("--gray-kernel", choices=["auto", "band5", "band", "lut16", "lut8", "f32"], default=None,
-                    help="GRAY8: series_gray_lut_kernel with the table chosen per launch (layout 4, the "
-                         "library default), the band-keyed table (5), the swizzled band-clamped table (3), "
-                         "the (a, b) u16 table (2) or the two byte tables (1), or the f32 "
-                         "series_fast_kernel (0); unset: the library's choice (DIPS_GRAY_LUT as set)")
+    ap.add_argument("--gray-kernel", choices=sorted(_GRAY_FORMS), default="auto",
+                    help="GRAY8: the table kernel with its per-workgroup layout choice (auto, the library "
+                         "default), the band-keyed or the pair-keyed table pinned, or the f32 kernel")
     args = ap.parse_args()
-    if args.gray_kernel:
-        os.environ["DIPS_GRAY_LUT"] = {"auto": "4", "band5": "5", "band": "3", "lut16": "2", "lut8": "1",
-                                       "f32": "0"}[args.gray_kernel]
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     from oracle import oracle
@@ -56,7 +54,8 @@ def main():
             continue
         shape = (F, H, W) if C == 1 else (F, H, W, C)
         frames = torch.empty(shape, dtype=torch.uint8, device=dev)
-        op = DiffSeriesOperator(PixelFormat(C), Mode(mode), tau, time_kernel=True)
+        op = DiffSeriesOperator(PixelFormat(C), Mode(mode), tau, time_kernel=True,
+                                **(_GRAY_FORMS[args.gray_kernel] if C == 1 else {}))
         op.synth_device(frames, W, H, 0xD1B5, 0)
         series = torch.zeros((F, 4), dtype=torch.int64, device=dev)
         op.run_device(frames, series)
@@ -73,7 +72,7 @@ def main():
         want, _, _ = oracle.series(host, mode=mode, tau=tau, nthreads=8)
         ok = bool(np.array_equal(series[:3].cpu().numpy().view(np.uint64), want))
         fb = W * H * C
-        print(json.dumps({"config": name, "steps": args.steps, "wall_ms": round(wall * 1e3, 4), **({"gray_kernel": args.gray_kernel or _GRAY_NAMES.get(os.environ.get("DIPS_GRAY_LUT", "4")[:1], "auto")} if C == 1 else {}),
+        print(json.dumps({"config": name, "steps": args.steps, "wall_ms": round(wall * 1e3, 4), **({"gray_kernel": args.gray_kernel} if C == 1 else {}),
                           "frames_per_s": round(F / wall, 1),
                           "kernel_ms": round(kms, 4), "kernel_GBps": round(F * fb / (kms / 1e3) / 1e9, 1),
                           "frac_of_8TBps": round(F * fb / (kms / 1e3) / 8e12, 4),

@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
-"""isi_ab.py -- the RGB8 series kernel's intensity-sum forms, named in argv[5]
-(default "isi,f64"; "sadi" = DIPS_SERIES_ISI=2; "contig" / "parts" =
-DIPS_SERIES_PARTS=0 / 1, the schedule): the integer intensity sum
-(series_v2.hip ISI, the default for tau >= 2^-5) against the f64 sum
-(DIPS_SERIES_ISI=0), alternated in ONE process over ONE resident buffer of
-the headline workload (5000 4K RGB8 frames, 'per-frame', tau 8/255): kernel
-time by the library's hipEvents, socket energy and PPT residency from the SMU
-read right before and after each variant's steps (tools/power_probe.py, no
-polling thread), series of both variants compared.  One JSON line per
-(round, variant), then a summary."""
+"""isi_ab.py -- variants of the RGB8 series kernel, named in argv[5]
+(default "isi,f64"): the integer intensity sum (series_v2.hip ISI = 1, the
+default for tau >= 2^-5), the f64 sum (ISI = 0, DIPS_FLAG_CROSSCHECK), and
+"wN" = the default form with DIPS_SERIES_WAVES_PER_SIMD=N -- alternated in ONE
+process over ONE resident buffer of the headline workload (5000 4K RGB8
+frames, 'per-frame', tau 8/255): kernel time by the library's hipEvents,
+socket energy and PPT residency from the SMU read right before and after
+each variant's steps (tools/power_probe.py, no polling thread), series of
+all variants compared.  One JSON line per (round, variant), then a summary.
+
+Usage: python tools/isi_ab.py [frames] [steps] [rounds] [per-frame|overall] [variants] [WxH]"""
 from __future__ import annotations
 
 import json
@@ -32,15 +33,10 @@ def main():
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     mode = Mode.PerFrame if (len(sys.argv) <= 4 or sys.argv[4] == "per-frame") else Mode.Overall
     names = (sys.argv[5] if len(sys.argv) > 5 else "isi,f64").split(",")
-    env_of = {"f64": ("DIPS_SERIES_ISI", "0"), "isi": ("DIPS_SERIES_ISI", "1"), "sadi": ("DIPS_SERIES_ISI", "2"),
-              "contig": ("DIPS_SERIES_PARTS", "0"), "parts": ("DIPS_SERIES_PARTS", "1"),
-              "partsall": ("DIPS_SERIES_PARTS", "2"), "kzero": ("DIPS_SERIES_KZERO", "1"),
-              "fill": ("DIPS_SERIES_KZERO", "0"),
-              "w5": ("DIPS_SERIES_WAVES_PER_SIMD", "5"), "w4": ("DIPS_SERIES_WAVES_PER_SIMD", "4"),
-              "w3": ("DIPS_SERIES_WAVES_PER_SIMD", "3"), "w2": ("DIPS_SERIES_WAVES_PER_SIMD", "2")}
+    ops = {k: DiffSeriesOperator(PixelFormat.RGB8, mode, 8 / 255, time_kernel=True, crosscheck=(k == "f64"))
+           for k in names}
     frames = torch.empty((F, H, W, 3), dtype=torch.uint8, device="cuda")
-    op = DiffSeriesOperator(PixelFormat.RGB8, mode, 8 / 255, time_kernel=True)
-    op.synth_device(frames, W, H, 0xD1B5, 0)
+    ops[names[0]].synth_device(frames, W, H, 0xD1B5, 0)
     ref = frames[0].clone()
     series = {k: torch.zeros((F, 4), dtype=torch.int64, device="cuda") for k in names}
     torch.cuda.synchronize()
@@ -54,13 +50,11 @@ def main():
         smp = None
     res = {}
     for rnd in range(rounds):
-        order = [(k, env_of[k]) for k in names]
-        for name, (var, env) in (order if rnd % 2 == 0 else order[::-1]):
-            os.environ.pop("DIPS_SERIES_ISI", None)
-            os.environ.pop("DIPS_SERIES_PARTS", None)
-            os.environ.pop("DIPS_SERIES_KZERO", None)
+        for name in (names if rnd % 2 == 0 else names[::-1]):
             os.environ.pop("DIPS_SERIES_WAVES_PER_SIMD", None)
-            os.environ[var] = env
+            if name.startswith("w"):
+                os.environ["DIPS_SERIES_WAVES_PER_SIMD"] = name[1:]
+            op = ops[name]
             r = None if mode == Mode.PerFrame else ref
             op.run_device(frames, series[name], ref=r)  # warm
             torch.cuda.synchronize()
@@ -74,11 +68,10 @@ def main():
             t1 = time.monotonic()
             if smp:
                 smp.sample()
-            each = op.kernel_times()
-            kms = float(np.median(each))
-            fps = F / (kms / 1e3)
+            kms = float(np.median(op.kernel_times()))
             rec = {"variant": name, "round": rnd, "steps": steps, "kernel_ms_median": round(kms, 4),
-                   "frames_per_s": round(fps, 1), "frac_of_8TBps": round(F * W * H * 3 / (kms / 1e3) / 8e12, 4),
+                   "frames_per_s": round(F / (kms / 1e3), 1),
+                   "frac_of_8TBps": round(F * W * H * 3 / (kms / 1e3) / 8e12, 4),
                    "wall_frames_per_s": round(F * steps / (t1 - t0), 1)}
             if smp:
                 g = smp.window(t0 - 0.5, t1 + 0.5)[0]
@@ -88,18 +81,17 @@ def main():
                                 "gfxclk_end_MHz": smp.rows[-1][4]})
             res.setdefault(name, []).append(rec)
             print(json.dumps(rec), flush=True)
-    os.environ.pop("DIPS_SERIES_ISI", None)
-    os.environ.pop("DIPS_SERIES_PARTS", None)
-    os.environ.pop("DIPS_SERIES_KZERO", None)
     os.environ.pop("DIPS_SERIES_WAVES_PER_SIMD", None)
     same = all(bool(torch.equal(series[names[0]], series[k])) for k in names[1:])
-    summ = {"summary": True, "size": f"{W}x{H}", "frames": F, "mode": "per-frame" if mode == Mode.PerFrame else "overall", "series_equal": same}
+    summ = {"summary": True, "size": f"{W}x{H}", "frames": F,
+            "mode": "per-frame" if mode == Mode.PerFrame else "overall", "series_equal": same}
     for k, v in res.items():
         summ[k] = {"frac_median": float(np.median([r["frac_of_8TBps"] for r in v])),
                    "mJ_per_frame_median": float(np.median([r.get("mJ_per_frame", np.nan) for r in v])),
                    "wall_frames_per_s_median": float(np.median([r["wall_frames_per_s"] for r in v]))}
     print(json.dumps(summ), flush=True)
-    op.close()
+    for op in ops.values():
+        op.close()
 
 
 if __name__ == "__main__":
