@@ -16,6 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdips_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dips_hip.h")
 
+ABI_VERSION = 2  # DIPS_ABI_VERSION of include/dips_hip.h
+
 DIPS_OK = 0
 DIPS_ERR_INVALID = -1
 DIPS_ERR_HIP = -2
@@ -181,6 +183,9 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res
+        if lib.dips_abi_version() != ABI_VERSION:
+            raise DipsLibraryError(f"{LIB_PATH} has ABI {lib.dips_abi_version()}, the bindings expect {ABI_VERSION}: "
+                                   "rebuild it (`make -C dips_amd/csrc`)")
         _lib = lib
         return lib
 

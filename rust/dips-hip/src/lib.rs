@@ -116,7 +116,21 @@ fn check_alt(st: c_int, h: *const ffi::DipsAltHandle) -> Result<c_int, DipsError
     }
 }
 
+/// The library this crate was written against (a stale or newer
+/// `libdips_hip.so` is refused, not half-used).
+fn check_abi() -> Result<(), DipsError> {
+    // SAFETY: no arguments.
+    let v = unsafe { ffi::dips_abi_version() };
+    if v == ffi::DIPS_ABI_VERSION {
+        Ok(())
+    } else {
+        Err(DipsError { status: ffi::DIPS_ERR_STATE,
+                        message: format!("libdips_hip.so has ABI {v}, this crate expects {}", ffi::DIPS_ABI_VERSION) })
+    }
+}
+
 fn create(p: &ffi::DipsParams, device: i32) -> Result<NonNull<ffi::DipsHandle>, DipsError> {
+    check_abi()?;
     let mut h = ptr::null_mut();
     // SAFETY: p is a valid dips_params, h an out pointer.
     check(unsafe { ffi::dips_create(p, device, &mut h) }, ptr::null())?;
@@ -480,6 +494,7 @@ impl DiPsCompute {
         p.chroma_filter = props.chroma_filter.code();
         p.num_textures = num_textures as u32;
         let (rows, cols) = (textures_width, textures_height);
+        check_abi()?;
         let mut h = ptr::null_mut();
         // SAFETY: p valid, h an out pointer.
         check_alt(unsafe { ffi::dips_alt_create(&p, cols, rows, 0, &mut h) }, ptr::null())?;

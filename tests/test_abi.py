@@ -28,7 +28,9 @@ def test_header_functions_exported():
     assert len(names) >= 18
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.dips_abi_version() == 2
+    hdr = open(os.path.join(ROOT, "include", "dips_hip.h")).read()
+    want = int(re.search(r"#define DIPS_ABI_VERSION (\d+)", hdr).group(1))
+    assert lib.dips_abi_version() == want == _lib.ABI_VERSION  # the binding refuses any other library
 
 
 def test_rust_crate_binds_every_entry_point():
