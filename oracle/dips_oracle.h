@@ -9,10 +9,13 @@
  * Parity status: the reference (RubenMovsesyan/DiPs, Rust + WGSL through
  * wgpu 24 / naga 24.0.0) cannot be built in this image (no cargo/rustc, crates
  * not vendored) and ships no tests, fixtures or golden vectors (SURVEY.md
- * s4, s8c).  This oracle is therefore pinned only by analytic known-answer
- * tests and by an independent numpy restatement (oracle/np_restatement.py);
- * against the reference itself it is "parity unpinned".  The pinned choices
- * for backend-defined behaviour are:
+ * s4, s8c).  Its shader files are executed instead: oracle/wgsl_exec.py
+ * interprets the reference's WGSL text, oracle/wgsl_ref.py restates the Rust
+ * host side around it, and this oracle reproduces those outputs bit for bit
+ * (tests/test_wgsl_pin.py, the wgsl_* fixtures; get_intensity over all 2^24
+ * RGB triples).  The restatement is thereby pinned to the shader text; what
+ * WGSL leaves to the backend is pinned as follows (the reference's bytes on
+ * a given GPU depend on its driver for these, which nothing here can run):
  *   - naga bounds-check policy `Restrict` (Vulkan/DX12) for the
  *     out-of-bounds bubble-sort index (dips_shader.wgsl:198-203),
  *   - rgba8unorm load u(c) = c / 255.0f (IEEE division),

@@ -3,7 +3,8 @@
 Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg
 import this module.  It loads ``oracle/libdips_oracle.so`` (built by
 ``oracle/Makefile``), a plain-C restatement of the DiPs reference semantics
-(see dips_oracle.h for the citations and the "parity unpinned" status).
+(see dips_oracle.h for the citations and the parity status: pinned to the
+reference's shader text by executing it, oracle/wgsl_exec.py).
 """
 from __future__ import annotations
 

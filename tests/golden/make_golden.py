@@ -4,8 +4,8 @@ The reference (Rust + WGSL through wgpu) cannot run in this image and ships
 no fixtures, so the fixtures are produced by the
 independent numpy restatement (oracle/np_restatement.py) and accepted only
 where the C oracle (oracle/dips_oracle.c) agrees bit for bit.  They pin the
-oracle against regressions; against the reference they are "parity
-unpinned" (DESIGN.md "Oracle").
+oracle against regressions; the pin against the reference's shader text is
+make_wgsl_golden.py's (DESIGN.md "Oracle").
 
 Run: python tests/golden/make_golden.py   (writes *.npz + manifest.json here)
 """
