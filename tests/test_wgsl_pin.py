@@ -324,3 +324,12 @@ def test_correctly_rounded_exp_log_moves_bytes_by_at_most_one(filt):
         b = _run_cs(wgsl_ref.ComputeState(True, 1, k, filt, 0, pins=Pins(exp_log="nearest")), frames, ops, w, h)[0]
         d = np.abs(a.astype(int) - b.astype(int))
         assert d.max() <= 1, k
+
+
+@needs_ref
+def test_dips_opencv_runs_the_same_shaders():
+    """dips_opencv's ComputeState (same signatures) compiles
+    byte-identical shader files, so the fixtures pin it too."""
+    for name in ("dips_shader.wgsl", "pre_compute_shader.wgsl"):
+        assert wgsl_ref.shader_sha256("dips_opencv/src/gpu/shaders/" + name) == \
+            WMAN["shaders"]["dips/src/gpu/shaders/" + name]
