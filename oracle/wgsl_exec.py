@@ -48,7 +48,7 @@ from __future__ import annotations
 
 import dataclasses
 import re
-from typing import Any, Callable, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -561,10 +561,8 @@ def _abstract_binop(op, a, b, ta, tb):
         r = a - b
     elif op == "*":
         r = a * b
-    elif op == "/":
-        r = a / b if isf else int(a / b) if b else a
-        if not isf:
-            r = abs(a) // abs(b) * (1 if (a >= 0) == (b > 0) else -1)
+    elif op == "/":  # abstract ints: truncating (a zero divisor is a shader-creation error)
+        r = a / b if isf else abs(a) // abs(b) * (1 if (a >= 0) == (b > 0) else -1)
     elif op == "%":
         r = a - b * int(a / b) if isf else a - b * (abs(a) // abs(b) * (1 if (a >= 0) == (b > 0) else -1))
     elif op in ("&", "|", "^") and not isf:
@@ -697,19 +695,11 @@ _SWIZ = {c: i for i, c in enumerate("xyzw")}
 _SWIZ.update({c: i for i, c in enumerate("rgba")})
 
 
-def _lane(d, P):
-    """Broadcast data with an optional lane axis to [P, ...]."""
-    d = np.asarray(d)
-    return d
-
-
 def _where(m, new, old):
     """Masked select with the mask over the leading (lane) axis."""
     new, old = np.asarray(new), np.asarray(old)
     nd = max(new.ndim, old.ndim)
     mm = m.reshape(m.shape + (1,) * (nd - 1)) if nd >= 1 else m
-    if new.ndim < nd and new.ndim == nd - 1 and old.ndim == nd and old.shape[0] == m.shape[0]:
-        pass
     return np.where(mm, new, old)
 
 
@@ -1009,10 +999,7 @@ class Pipeline:
                 v = convert_to(self.eval(s[1], m), fctx.ret_ty)
                 d = np.asarray(v.d)
                 if fctx.ret is None:
-                    shape = (self.P,) + d.shape[(1 if d.ndim and d.shape[0] == self.P and self.P > 1 else 0):] \
-                        if not isinstance(v.ty, str) else (self.P,)
-                    if isinstance(v.ty, tuple) and v.ty[0] == "vec":
-                        shape = (self.P, v.ty[1])
+                    shape = (self.P, v.ty[1]) if isinstance(v.ty, tuple) else (self.P,)
                     fctx.ret = V(v.ty, np.zeros(shape, dtype=_NP[scalar_of(v.ty)]))
                 fctx.ret = V(fctx.ret.ty, _where(m, np.broadcast_to(d, fctx.ret.d.shape), fctx.ret.d))
             fctx.done = fctx.done | m
@@ -1220,7 +1207,7 @@ class Pipeline:
                 d = np.asarray(a.d)
                 if isinstance(a.ty, tuple):
                     if a.ty[2] != s:
-                        d = self.construct(("vec", a.ty[1], s), [a]).d if False else _convert_data(d, a.ty[2], s)
+                        d = _convert_data(d, a.ty[2], s)
                     for i in range(a.ty[1]):
                         comps.append(d[..., i])
                 else:
