@@ -616,6 +616,32 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
                 "started (the pool runs every staging task first), last_kernel_wait_end = last output task past "
                 "its wait for its stripe's kernel, wall_in_library = return; cpu sums over the copy pool's tasks",
     } if ph else {"phases": "not recorded (call did not take the zero-copy path)"}
+    # the same calls on the all-GPU form (DIPS_FLAG_CROSSCHECK): the whole
+    # RGBA8 frame copied into pinned staging and DMA'd to HBM, every step of
+    # get_intensity / median / epilogue on the GPU, the RGBA8 output DMA'd
+    # back -- no arithmetic on the host
+    n_x = min(n_timed, 60)
+    cx = ComputeState(*props, crosscheck=True)
+    outs_x = np.empty_like(host[:warm + n_x])
+    outs_x.fill(0)
+    times_x = []
+    try:
+        lx, hx = cx._hd._lib, cx._hd
+        for t in range(warm + n_x):
+            t0 = time.perf_counter()
+            hx.check(lx.dips_frame_callback(hx.ptr, W, H, host[t].ctypes.data, host[t].nbytes,
+                                            outs_x[t].ctypes.data, outs_x[t].nbytes))
+            if t >= warm:
+                times_x.append(time.perf_counter() - t0)
+    finally:
+        cx.close()
+    all_gpu = {"frames_per_s": round(n_x / float(np.sum(times_x)), 1), "calls": n_x,
+               "ms_per_call_median": round(float(np.median(times_x)) * 1e3, 4),
+               "outputs_equal_batch_path": bool(np.array_equal(outs_x, want[:warm + n_x])),
+               "path": "DIPS_FLAG_CROSSCHECK: add_texture + dispatch with whole-frame RGBA8 DMA both ways "
+                       "through pinned staging; get_intensity, the median and the epilogue all on the GPU "
+                       "(no host arithmetic); same calls, same frames, same outputs"}
+    del outs_x
     rec = {"frames_per_s": round(n_timed / tot, 1), "calls": n_timed,
            "ms_per_call_median": round(float(np.median(times)) * 1e3, 4),
            "ms_per_call_p90": round(float(np.percentile(times, 90)) * 1e3, 4),
@@ -632,6 +658,7 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
                    "written back over PCIe); the pool expands the keys into the RGBA8 output as each stripe's "
                    "event fires (dips_abi.hip frame_callback_striped, copy_pool.h pack_frame / expand_keys)",
            "pcie_bytes_each_way_per_frame": {"host_to_device": W * H * 2, "device_to_host": W * H},
+           "all_gpu_form": all_gpu,
            "breakdown": breakdown}
     return rec, (host[:warm].copy(), want[:warm].copy())
 
