@@ -12,8 +12,9 @@ dips_alt splice and run loop) restated from its Rust.  These tests:
   reference shaders, tests/golden/make_wgsl_golden.py) -- no reference
   checkout needed;
 * where the reference checkout is present (this container): the fixtures'
-  shader hashes still match it and the cheap fixtures regenerate byte for
-  byte; get_intensity from dips_shader.wgsl equals the restatement over all
+  shader hashes still match it and every fixture but the W = 11 one (25 s
+  in the interpreter; generated under the same C-oracle assert) regenerates
+  byte for byte; get_intensity from dips_shader.wgsl equals the restatement over all
   2^24 RGB triples and every channel value; fresh randomized ComputeState /
   dips_alt draws equal the C oracle; the Metal bounds policy reproduces
   SURVEY.md s8 A3's all-zero start texture; correctly rounded exp / log move
@@ -209,7 +210,7 @@ def test_fixture_shader_hashes_match_the_reference():
 
 
 @needs_ref
-@pytest.mark.parametrize("case", [c for c in WMAN["compute_state"] if c["params"][1] <= 3], ids=lambda c: c["file"])
+@pytest.mark.parametrize("case", [c for c in WMAN["compute_state"] if c["params"][1] <= 7], ids=lambda c: c["file"])
 def test_wgsl_compute_state_fixture_regenerates(case):
     z = _load(case["file"])
     fr = z["frames"]
@@ -218,7 +219,7 @@ def test_wgsl_compute_state_fixture_regenerates(case):
 
 
 @needs_ref
-@pytest.mark.parametrize("case", [c for c in WMAN["alt"] if c["window"] <= 3], ids=lambda c: c["file"])
+@pytest.mark.parametrize("case", WMAN["alt"], ids=lambda c: c["file"])
 def test_wgsl_alt_fixture_regenerates(case):
     z = _load(case["file"])
     fr = z["frames"]
