@@ -274,7 +274,10 @@ dips_status dips_synth_frames(dips_handle *h, uint32_t width, uint32_t height,
 dips_status dips_kernel_time(dips_handle *h, double *total_ms, uint64_t *launches);
 dips_status dips_kernel_time_reset(dips_handle *h);
 /* The same launches one by one: up to `cap` per-launch milliseconds (oldest
- * first) into ms_each, the count since the last reset into *launches. */
+ * first) into ms_each, the number of launches held into *launches.  The
+ * handle holds the launches since the last reset, at most the most recent
+ * 65,536 (beyond that the older half is dropped; dips_kernel_time still
+ * counts every launch). */
 dips_status dips_kernel_time_each(dips_handle *h, double *ms_each, uint64_t cap, uint64_t *launches);
 
 /* Geometry of the series kernel for a frame shape (for roofline accounting):
