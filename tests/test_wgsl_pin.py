@@ -265,9 +265,16 @@ def test_random_compute_state_draws_equal_c_oracle(seed):
     frames = rng.integers(0, 256, (7, h, w, 4), dtype=np.uint8)
     if seed % 2:
         frames[..., :3] = (frames[..., :3] // 64) * 85  # few levels: ties and repeats
-    ops = []
-    for k in range(7):
-        ops += [k, DISPATCH] + ([DISPATCH] if rng.integers(0, 4) == 0 else [])
+    # a random interleaving: add_texture without a dispatch, repeated
+    # dispatches, dispatches before the ring is full
+    ops, k = [], 0
+    while k < 7:
+        if rng.random() < 0.6:
+            ops.append(k)
+            k += 1
+        else:
+            ops.append(DISPATCH)
+    ops.append(DISPATCH)
     a = _run_cs(wgsl_ref.ComputeState(*params), frames, ops, w, h)
     b = _run_cs(oracle.ComputeState(*params), frames, ops, w, h)
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0]), params
