@@ -230,3 +230,54 @@ def test_failures_are_visible_at_the_rust_boundary():
     assert "pub const DIPS_ERR_INTERNAL: DipsStatus = -7;" in ffi
     assert "pub const DIPS_ABI_VERSION: c_int = 2;" in ffi
     assert "pub const DIPS_FLAG_CROSSCHECK: u32 = 0x8;" in ffi
+
+
+def _rust_files():
+    base = os.path.join(ROOT, "rust", "dips-hip")
+    out = []
+    for d, _, fs in os.walk(base):
+        out += [os.path.join(d, f) for f in sorted(fs) if f.endswith(".rs")]
+    return out
+
+
+def test_rust_sources_lex_cleanly_and_balance():
+    """No cargo / rustc in the image, so the crate is checked lexically:
+    pygments' Rust lexer finds no error token in any .rs file, and every
+    (), [] and {} outside strings, chars and comments closes in order."""
+    from pygments.lexers import RustLexer
+    from pygments.token import Comment, Error, String
+    files = _rust_files()
+    assert len(files) >= 3, files
+    pairs = {")": "(", "]": "[", "}": "{"}
+    for path in files:
+        with open(path) as f:
+            src = f.read()
+        stack = []
+        for ttype, value in RustLexer().get_tokens(src):
+            assert ttype is not Error and ttype not in Error, (path, value)
+            if ttype in String or ttype in Comment:
+                continue
+            for ch in value:
+                if ch in "([{":
+                    stack.append(ch)
+                elif ch in ")]}":
+                    assert stack and stack[-1] == pairs[ch], (path, ch)
+                    stack.pop()
+        assert not stack, (path, stack)
+
+
+def test_rust_calls_only_declared_ffi():
+    """Every ffi::dips_* the safe wrapper and the examples call is declared
+    in ffi.rs (itself checked against the header above)."""
+    ffi = _read(os.path.join(ROOT, "rust", "dips-hip", "src", "ffi.rs"))
+    declared = set(re.findall(r"pub fn (dips_\w+)\(", ffi))
+    for path in _rust_files():
+        if path.endswith("ffi.rs"):
+            continue
+        for name in re.findall(r"ffi::(dips_\w+)\s*\(", _read(path)):
+            assert name in declared, (path, name)
+
+
+def _read(path):
+    with open(path) as f:
+        return f.read()
