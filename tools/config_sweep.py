@@ -48,6 +48,8 @@ def main():
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     from oracle import oracle
 
+    import bench  # the power legs: energy counter / PPT residency / gfx clock around a leg
+    smp = bench._power_sampler(torch, 0)
     dev = torch.device("cuda", 0)
     for name, W, H, C, F, mode, tau in CONFIGS:
         if args.only and args.only not in name:
@@ -61,13 +63,21 @@ def main():
         op.run_device(frames, series)
         torch.cuda.synchronize()
         op.kernel_time(reset=True)
-        t = time.perf_counter()
-        for _ in range(args.steps):
-            op.run_device(frames, series)
-        torch.cuda.synchronize()
-        wall = (time.perf_counter() - t) / args.steps
+
+        def timed():
+            t = time.perf_counter()
+            for _ in range(args.steps):
+                op.run_device(frames, series)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t) / args.steps
+
+        wall, power = bench._power_leg(smp, timed, F * args.steps, f"{args.steps} series launches")
         kms, n = op.kernel_time()
         kms /= max(n, 1)
+        # the compute-free read of the same bytes, its own power reading
+        reads, read_power = bench._power_leg(smp, lambda: [op.read_ceiling_ms(frames) for _ in range(args.steps)],
+                                             F * args.steps, f"{args.steps} read_ceiling_kernel launches")
+        read_ms = float(np.median(reads))
         host = frames[:3].cpu().numpy()
         want, _, _ = oracle.series(host, mode=mode, tau=tau, nthreads=8)
         ok = bool(np.array_equal(series[:3].cpu().numpy().view(np.uint64), want))
@@ -76,6 +86,10 @@ def main():
                           "frames_per_s": round(F / wall, 1),
                           "kernel_ms": round(kms, 4), "kernel_GBps": round(F * fb / (kms / 1e3) / 1e9, 1),
                           "frac_of_8TBps": round(F * fb / (kms / 1e3) / 8e12, 4),
+                          "power": power,
+                          "read_ceiling": {"ms": round(read_ms, 4),
+                                           "frac_of_8TBps": round(F * fb / (read_ms / 1e3) / 8e12, 4),
+                                           "power": read_power},
                           "first_frames_match_oracle": ok}), flush=True)
         op.close()
         del frames, series
