@@ -71,10 +71,10 @@ class ComputeState:
 
     def __init__(self, colorize: bool, spatial_window_size: int, sensitivity: float, filter_type: int,
                  chroma_filter: int, pins: Pins = PINS):
-        # the pipeline constants (gpu/mod.rs:104-111), f64 values
+        # the pipeline constants (gpu/mod.rs:101-109), f64 values
         consts = {"0": 1.0 if colorize else 0.0, "1": float(spatial_window_size),
                   "2": float(np.float32(sensitivity)), "3": float(filter_type), "4": float(chroma_filter)}
-        # both modules get the same map (gpu/mod.rs:123-126, 144-147)
+        # both modules get the same map (gpu/mod.rs:124, 145)
         self.pre = module(DIPS_PRE_SHADER).pipeline("pre_compute_main", consts, pins)
         self.main = module(DIPS_SHADER).pipeline("compute_main", consts, pins)
         self.textures: List[np.ndarray] = []   # the VecDeque (mod.rs:53, 170-176)
@@ -97,7 +97,7 @@ class ComputeState:
             out = Texture(np.zeros((height, width, 4), np.uint8))
             self.pre.dispatch({"start_texture_array": [Texture(t.copy()) for t in self.textures],
                                "output_texture": out}, _groups(width, height))
-            self.starting_texture = out.data.copy()   # read back, de-padded (mod.rs:268-300)
+            self.starting_texture = out.data.copy()   # read back, de-padded (mod.rs:218-303)
         if self.slots is None:  # MainComputeBindGroups::initialize Ok (starting index 0)
             self.slots = [Texture(t.copy()) for t in self.textures]
             self.start = Texture(self.starting_texture.copy())  # set_start_texture (bind_groups.rs:376-387)
@@ -158,7 +158,7 @@ class AltCompute:
                  scalar: float = 5.0, filter_type: int = 0, chroma: int = 0, pins: Pins = PINS):
         self.n = int(num_textures)
         self.width, self.height = int(width), int(height)
-        # get_properties_hash_map (mod.rs:189-207) + NUM_TEXTURES (mod.rs:451-455)
+        # get_properties_hash_map (mod.rs:189-207) + NUM_TEXTURES (mod.rs:453)
         consts = {"COLORIZE": 1.0 if colorize else 0.0, "WINDOW_SIZE": float(window),
                   "SIGMOID_HORIZONTAL_SCALAR": float(np.float32(scalar)), "FILTER_TYPE": float(filter_type),
                   "CHROMA_FILTER": float(chroma), "NUM_TEXTURES": float(self.n)}
