@@ -450,7 +450,7 @@ class DiffSeriesOperator:
         rp = None
         if ref is not None:
             ref = _as_u8(ref)
-            if ref.size != frames[0].size:
+            if ref.size != h * w * int(self.fmt):
                 raise ValueError("ref must have the shape of one frame")
             rp = ref.ctypes.data
         self._host.check(self._host._lib.dips_diff_series(
@@ -467,7 +467,7 @@ class DiffSeriesOperator:
         rp = None
         if ref is not None:
             ref = _as_u8(ref)
-            if ref.size != frames[0].size:
+            if ref.size != h * w * int(self.fmt):
                 raise ValueError("ref must have the shape of one frame")
             rp = ref.ctypes.data
         self._host.check(self._host._lib.dips_diff_series_streamed(
