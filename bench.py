@@ -100,10 +100,10 @@ def _series_isi(tau: float) -> int:
 
 def _v2_kernel_name(per_frame: bool, tau: float, with_map: bool = False) -> str:
     """The series_v2_kernel instantiation the library runs for an aligned RGB8
-    batch (series_v2.hip: <C, CH, U, PF, MAP, ALIGN, ISI>), spelled as
+    batch (series_v2.hip: <C, CH, U, PF, MAP, ALIGN, ISI>; U = 5 for RGB8), spelled as
     rocprofv3 prints it (ISI is an int template argument)."""
     b = lambda v: "true" if v else "false"  # noqa: E731
-    return f"series_v2_kernel<3, 0, 4, {b(per_frame)}, {b(with_map)}, false, {_series_isi(tau)}>"
+    return f"series_v2_kernel<3, 0, 5, {b(per_frame)}, {b(with_map)}, false, {_series_isi(tau)}>"
 
 
 def log(msg):

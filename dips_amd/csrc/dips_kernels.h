@@ -11,7 +11,10 @@ namespace dips {
 // Unroll (vecs per lane) of the fast series kernel; a tile = 64 * U vecs.
 constexpr int kUnrollRGB = 4;   // 1024 px / wave / frame for RGB8 and RGBA8
 constexpr int kUnrollGray = 2;  // 2048 px / wave / frame for GRAY8
-constexpr int kUnrollV2 = 4;    // series_v2_kernel (RGB8/RGBA8): 1024 px / wave / frame
+constexpr int kUnrollV2 = 4;    // series_v2_kernel RGBA8: 1024 px / wave / frame
+constexpr int kUnrollV2Rgb = 5; // series_v2_kernel RGB8: 1280 px / wave / frame (12-B vecs: 5 x 64 x 12 < 4096)
+template <int C>
+constexpr int v2_unroll() { return C == 3 ? kUnrollV2Rgb : kUnrollV2; }
 // series_gray_lut_kernel: 64 * 16 * U px / wave / frame (U = 4: 4K gray8
 // 61.9-62.1 % of 8 TB/s vs 60.4-60.6 % at U = 2, profiles/r02_gray_lut_unroll.jsonl;
 // confirmed in one process with the final kernel: U = 4 65.5-65.9 %, U = 3

@@ -456,7 +456,7 @@ __global__ __launch_bounds__(256) void read_walk_kernel(SeriesArgs a, uint32_t* 
 
 hipError_t launch_read_walk(const SeriesArgs& a, int vec_bytes, uint32_t blocks, uint32_t* out, hipStream_t s) {
     switch (vec_bytes) {
-        case 12: hipLaunchKernelGGL((read_walk_kernel<12, kUnrollV2>), dim3(blocks), dim3(256), 0, s, a, out); break;
+        case 12: hipLaunchKernelGGL((read_walk_kernel<12, kUnrollV2Rgb>), dim3(blocks), dim3(256), 0, s, a, out); break;
         case 16: hipLaunchKernelGGL((read_walk_kernel<16, kUnrollV2>), dim3(blocks), dim3(256), 0, s, a, out); break;
         default: return hipErrorInvalidValue;
     }
@@ -624,7 +624,7 @@ static const void* pick_fast_u(int chroma, bool pf, bool map) {
 }
 
 // RGB8 / RGBA8 run series_v2_kernel (series_v2.hip); GRAY8 the kernel above.
-int fast_unroll(int channels) { return channels == 1 ? kUnrollGray : kUnrollV2; }
+int fast_unroll(int channels) { return channels == 1 ? kUnrollGray : (channels == 3 ? kUnrollV2Rgb : kUnrollV2); }
 
 const void* series_fast_kernel_ptr(int channels, int chroma, bool per_frame, bool map, bool align, int isi) {
     switch (channels) {

@@ -18,10 +18,13 @@
 //  * a 4-slot register ring of frame vecs, rotated by unrolling four frames,
 //    so the bytes of frame t double as the SAD reference of frame t+1 with no
 //    register copies (the previous kernel spent ~10% of its VALU on v_mov);
-//  * U = 4 vecs per lane (1024 px per wave and frame), 96 VGPRs, 5 waves
-//    per SIMD: measured against U = 2 at 8 waves and U = 3 at 6 waves, the
-//    per-frame reduction amortised over more pixels wins by 1.5 % and halves
-//    the partial records;
+//  * U = 5 vecs per lane for RGB8 (1280 px per wave and frame; RGBA8's
+//    16-B vecs keep U = 4, the 12-bit offset limit): the per-frame wave
+//    reduction and record packing (~22 VALU per lane and frame) spread over
+//    20 pixels instead of 16, and a fifth fewer partial records; 116 VGPRs,
+//    4 waves per SIMD.  Measured against U = 4 (96 VGPRs, 5 waves) in
+//    alternated runs on one box: +0.3-0.7 points (profiles/r05/ab_u5/);
+//    U = 2 at 8 waves and U = 3 at 6 had lost to U = 4 the same way;
 //  * the two frames of a pair are reduced together and their 8 wave sums are
 //    stored straight from the lanes that hold them (no v_readlane).
 #include "intensity_v2.h"
@@ -43,8 +46,8 @@ constexpr float kSjMul = 255.0f / 4194304.0f;
 // v_cvt_u32_f32 and an integer add per pixel replace v_cvt_f64_f32 +
 // v_add_f64 (the f64 add is the most power-hungry VALU class this kernel
 // issues, profiles/r02_energy_per_instruction.jsonl), for one packed f16
-// multiply per pixel pair.  Two accumulators of 8 pixels each stay below
-// 2^31.  The record carries n = sum dI * 2^32 = 16 sum a as H = n >> 15,
+// multiply per pixel pair.  Two u32 accumulators of <= 12 pixels each stay
+// below 2^32 (U = 5: 8 and 12).  The record carries n = sum dI * 2^32 = 16 sum a as H = n >> 15,
 // L = n mod 2^15, exactly as the f64 form.
 constexpr float kIsiMinTau = 0.03125f;  // 2^-5
 
@@ -64,7 +67,7 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
     constexpr float sj_mul = ISI ? kSjMul / 32.0f : kSjMul;
     // exact per-lane intensity sum, offset by 2^43 so that the f64's low 52
     // mantissa bits ARE the fixed-point value n = sum(a_s) * 2^9 (ulp(2^43)
-    // = 2^-9, the a_s granularity; n < 2^35 keeps every add exact)
+    // = 2^-9, the a_s granularity; n < 2^37 keeps every add exact)
     double si = 0x1p43;
     uint32_t si0 = 0, si1 = 0;  // ISI: sum of a over vecs 0 .. U/2-1 and U/2 .. U-1
     uint32_t map[U][F::NDW];
@@ -116,15 +119,15 @@ __device__ __forceinline__ void frame_v2(const SeriesArgs& a, St2 (&st)[U], cons
     vals[0] = sad;
     vals[1] = (uint32_t)sj;
     if constexpr (ISI == 1) {
-        // n = 16 (si0 + si1): H = n >> 15, L = n mod 2^15 without forming
-        // the 33-bit sum
-        const uint32_t low = (si0 & 0x7FFu) + (si1 & 0x7FFu);
-        vals[2] = (si0 >> 11) + (si1 >> 11) + (low >> 11);
-        vals[3] = (low & 0x7FFu) << 4;
+        // n = 16 (si0 + si1): H = n >> 15, L = n mod 2^15 (the 33-bit sum
+        // through the carry: add, add-with-carry, alignbit)
+        const uint64_t s64 = (uint64_t)si0 + (uint64_t)si1;
+        vals[2] = (uint32_t)(s64 >> 11);
+        vals[3] = ((uint32_t)s64 & 0x7FFu) << 4;
     } else {
         const uint64_t yb = __builtin_bit_cast(uint64_t, si);
         const uint32_t lo = (uint32_t)yb, hi = (uint32_t)(yb >> 32);
-        vals[2] = __builtin_amdgcn_alignbit(hi, lo, 15);  // H = n >> 15 (n < 2^35: no exponent bits)
+        vals[2] = __builtin_amdgcn_alignbit(hi, lo, 15);  // H = n >> 15 (n < 2^37: no exponent bits)
         vals[3] = lo & 0x7FFFu;                           // L = n mod 2^15
     }
     cnt = c;
@@ -150,7 +153,7 @@ __device__ __forceinline__ void store_one(__amdgpu_buffer_rsrc_t rpart, uint32_t
 // keep their natural allocation (5-7 waves).
 template <int C, int U, bool PF, bool MAP, bool ALIGN = false>
 constexpr int v2_min_waves() {
-    return ALIGN ? (MAP ? 1 : 4) : ((C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : 5)) : 1);
+    return ALIGN ? (MAP ? 1 : (U >= 5 ? 3 : 4)) : ((C == 3 && PF && !MAP) ? (U <= 2 ? 8 : (U == 3 ? 6 : (U == 4 ? 5 : 4))) : 1);
 }
 
 // The aligned-load form of an RGB8 vec (ALIGN): a frame whose base address
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(256, (v2_min_waves<C, U, PF, MAP, ALIGN>())) void s
 // ---------------------------------------------------------------------------
 template <int C, int CH, bool PF, bool MAP, bool ALIGN, int ISI>
 static const void* v2_ptr() {
-    return reinterpret_cast<const void*>(&series_v2_kernel<C, CH, kUnrollV2, PF, MAP, ALIGN && (C == 3 || C == 4), ISI>);
+    return reinterpret_cast<const void*>(&series_v2_kernel<C, CH, v2_unroll<C>(), PF, MAP, ALIGN && (C == 3 || C == 4), ISI>);
 }
 
 template <int C, bool ALIGN, int ISI>

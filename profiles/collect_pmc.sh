@@ -18,7 +18,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 PF=$([ "$MODE" = per-frame ] && echo true || echo false)
 python3 tools/pmc_to_json.py $OUT $F $MODE gpurun_out/pmc_traffic.json \
-  "series_v2_kernel<3, 0, 4, $PF, false, false, 1>" && \
+  "series_v2_kernel<3, 0, 5, $PF, false, false, 1>" && \
 python3 tools/pmc_to_json.py $OUT 2500 $MODE gpurun_out/pmc_traffic_map.json \
-  "series_v2_kernel<3, 0, 4, $PF, true, false, 1>" $((3840 * 2160 * 3 * 2))
+  "series_v2_kernel<3, 0, 5, $PF, true, false, 1>" $((3840 * 2160 * 3 * 2))
 # copy gpurun_out/pmc_traffic*.json into profiles/ after merge-back

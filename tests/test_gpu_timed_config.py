@@ -1,6 +1,6 @@
 """The exact configuration bench.py times, pinned to the oracle frame by
 frame (BASELINE.json configs[2]: 3840x2160 RGB8, 'per-frame', tau = 8/255,
-the default intensity-sum form ISI = 1 -- series_v2_kernel<3, 0, 4, true,
+the default intensity-sum form ISI = 1 -- series_v2_kernel<3, 0, 5, true,
 false, false, 1>).
 
 The bench's 5000-frame batch runs the part-major schedule (series_abi.hip

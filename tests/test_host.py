@@ -286,8 +286,8 @@ def test_bench_kernel_name_matches_library_choice():
     as rocprofv3 prints it (ISI an int): run_series_device's choice of the
     intensity-sum form (series_abi.hip series_isi_form)."""
     import bench
-    assert bench._v2_kernel_name(True, 8 / 255) == "series_v2_kernel<3, 0, 4, true, false, false, 1>"
-    assert bench._v2_kernel_name(False, 8 / 255, with_map=True) == "series_v2_kernel<3, 0, 4, false, true, false, 1>"
-    assert bench._v2_kernel_name(True, 0.0) == "series_v2_kernel<3, 0, 4, true, false, false, 0>"
+    assert bench._v2_kernel_name(True, 8 / 255) == "series_v2_kernel<3, 0, 5, true, false, false, 1>"
+    assert bench._v2_kernel_name(False, 8 / 255, with_map=True) == "series_v2_kernel<3, 0, 5, false, true, false, 1>"
+    assert bench._v2_kernel_name(True, 0.0) == "series_v2_kernel<3, 0, 5, true, false, false, 0>"
     assert bench._series_isi(0.0) == 0 and bench._series_isi(0.03) == 0 and bench._series_isi(1 / 32) == 1
     assert bench._series_isi(1.0) == 1

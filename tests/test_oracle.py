@@ -270,7 +270,8 @@ def test_v2_sj_from_intensity_difference():
 
 def test_v2_sj_lane_sum_rounds_exactly():
     """The kernel's per-lane SJ accumulation: sj = 0.5, then 16 fused
-    sj = fma(|dI2s|, 255 * 2^-22, sj) (U = 4 vecs x 4 px per lane and frame);
+    sj = fma(|dI2s|, 255 * 2^-22, sj) (U = 5 vecs x 4 px per lane and frame,
+    the RGB8 kernel; RGBA8's 4 vecs make 16);
     trunc(sj) must equal the lane's sum of |dJ|.  Lanes of worst-case pixels
     (largest per-pixel error, largest |dJ|) and random ones."""
     rng = np.random.default_rng(11)
@@ -280,7 +281,7 @@ def test_v2_sj_lane_sum_rounds_exactly():
     i2s = ((nr.U_LUT[mx] + nr.U_LUT[mn]).astype(np.float32) * np.float32(2.0 ** 22)).astype(np.float32)
     j = (mx + mn).astype(np.int64)
     k_sj = np.float64(np.float32(255.0 / 4194304.0))
-    n_lanes, px = 200_000, 16
+    n_lanes, px = 200_000, 20
     p = rng.integers(0, i2s.size, (n_lanes, px))
     q = rng.integers(0, i2s.size, (n_lanes, px))
     # append lanes of the extreme pixel pairs

@@ -32,8 +32,8 @@ static double now() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-__global__ __launch_bounds__(256, (v2_min_waves<3, kUnrollV2, true, false, false>())) void parts_isi(SeriesArgs a) {
-    series_v2_body<3, 0, kUnrollV2, true, false, kAuxNT, kAuxNT, 1, false, 1>(a);
+__global__ __launch_bounds__(256, (v2_min_waves<3, kUnrollV2Rgb, true, false, false>())) void parts_isi(SeriesArgs a) {
+    series_v2_body<3, 0, kUnrollV2Rgb, true, false, kAuxNT, kAuxNT, 1, false, 1>(a);
 }
 
 struct Kind {
@@ -104,7 +104,7 @@ int main(int argc, char** argv) {
 
     int occ = 0;
     if (!k0 || hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k0, 256, 0) != hipSuccess || occ < 1) return 1;
-    const uint64_t nvec = fb / 12, tiles = (nvec + 64ull * kUnrollV2 - 1) / (64ull * kUnrollV2);
+    const uint64_t nvec = fb / 12, tiles = (nvec + 64ull * kUnrollV2Rgb - 1) / (64ull * kUnrollV2Rgb);
     uint64_t* partials = nullptr;
     dips_series_entry* series = nullptr;
     SeriesArgs a{};
