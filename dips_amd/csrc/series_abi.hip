@@ -52,7 +52,7 @@ uint64_t waves_per_simd(uint64_t occupancy) {
 // traffic), P from the one that gives every resident wave slot an item up to
 // 4x that: the smallest whose items fill >= 95 % of the slots (k items per
 // slot), else the best-filling one; the waves then get ceil(items / n_waves)
-// or one fewer items each (4K RGB8, 5000 frames: L = 1000, 5,063 waves).
+// or one fewer items each (4K RGB8, 5000 frames, U = 5: L = 1000, 4,050 waves).
 // Batches of fewer than 256 frames keep the contiguous ranges.
 void part_geometry(FastGeom& g, uint64_t n_frames, uint64_t resident) {
     if (n_frames < 256 || g.n_tiles == 0 || resident == 0) return;

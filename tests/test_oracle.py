@@ -269,7 +269,7 @@ def test_v2_sj_from_intensity_difference():
 
 
 def test_v2_sj_lane_sum_rounds_exactly():
-    """The kernel's per-lane SJ accumulation: sj = 0.5, then 16 fused
+    """The kernel's per-lane SJ accumulation: sj = 0.5, then 20 fused
     sj = fma(|dI2s|, 255 * 2^-22, sj) (U = 5 vecs x 4 px per lane and frame,
     the RGB8 kernel; RGBA8's 4 vecs make 16);
     trunc(sj) must equal the lane's sum of |dJ|.  Lanes of worst-case pixels

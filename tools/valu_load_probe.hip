@@ -7,7 +7,7 @@
 // folded into one result per thread.  K = 0 is the plain read.  For RGB8
 // frames a dword is 4/3 pixel, so K fma per dword = 0.75 K VALU ops per
 // pixel (+ the 2 ops per dword that make the value); the series kernel
-// issues ~12.75 per pixel.  Driven by tools/valu_load_probe.py, which reads
+// issues ~12.75 per pixel in its pixel loop (13.65 in all at U = 5).  Driven by tools/valu_load_probe.py, which reads
 // power, PPT residency and clocks around each K.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC -cuid=valu_load_probe \

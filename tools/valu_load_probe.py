@@ -10,7 +10,7 @@ bracketed by readings of the energy counter, PPT residency and gfx clock
 K: GB/s, fraction of 8 TB/s, ops per pixel, average W, PPT residency, clock.
 
 The question it answers: at how many VALU ops per byte does the stream start
-to lose bandwidth to the power limit, and is the series kernel's ~12.75 ops
+to lose bandwidth to the power limit, and is the series kernel's ~12.75-13.65 ops
 per pixel past that point?
 
 Build (here):  hipcc --offload-arch=gfx950 -O3 -shared -fPIC -cuid=valu_load_probe \\
