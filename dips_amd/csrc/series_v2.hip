@@ -34,8 +34,8 @@ namespace dips {
 // SJ from the intensity difference: 255 * |dI2| = |dJ| + err, |err| < 1.1e-4
 // (u() rounds up by < 2^-24, the sum and difference round by <= 2^-24 each;
 // exhaustive in tests/test_oracle.py), so the per-lane f32 sum of
-// |dI2s| * 255 * 2^-22 (exact multiplier, 16 px x 510 < 8192: rounding
-// <= 2^-11 per add) is within 0.01 of the integer SJ.
+// |dI2s| * 255 * 2^-22 (exact multiplier, <= 20 px x 510 < 16384: rounding
+// <= 2^-11 per add) is within 0.015 of the integer SJ.
 constexpr float kSjMul = 255.0f / 4194304.0f;
 
 // The integer intensity sum (ISI): for tau >= 2^-5 every selected dI is an
@@ -193,7 +193,7 @@ __device__ __forceinline__ void funnel(uint32_t (&v)[L], uint32_t sh) {
 // the contiguous ranges on each of four buffers, with 0.7-1.2 % less energy
 // per frame).
 template <int C, int CH, int U, bool PF, bool MAP, int AUX, int SAUX, int SCHED = 0, bool ALIGN = false,
-          int ISI = 0>
+          int ISI = 0, int WPB = 4>
 __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
     using F = Fmt<C>;
     static_assert(!ALIGN || C == 3 || C == 4, "the aligned-load form is the RGB8 / RGBA8 one");
@@ -202,7 +202,7 @@ __device__ __forceinline__ void series_v2_body(const SeriesArgs& a) {
     static_assert(U * 64 * F::VB <= 4096, "vec offsets must fit the 12-bit immediate");
     zero_series(a);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)WPB + (threadIdx.x >> 6));
     if (wave >= a.n_waves) return;
     const uint32_t fb = a.frame_bytes, vb = a.vec_bytes;
     // record dword offsets of the lanes that store reduced values; other

@@ -14,6 +14,8 @@
 // not measured, before the next buffer)] [L,L,...: also the part-major
 // schedule (series_v2_body SCHED = 1) with parts of L frames, per buffer]
 // [waves of the part-major runs: e.g. 4050 = 32,400 items of L = 1250 / 8]
+// (an L written with a trailing x, e.g. 1000x, runs the part-major schedule
+// in 1024-thread workgroups)
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o build/alloc_policy_ab tools/alloc_policy_ab.hip
 #include "../dips_amd/csrc/series_kernels.hip"
 #include "../dips_amd/csrc/series_v2.hip"
@@ -34,6 +36,11 @@ static double now() {
 
 __global__ __launch_bounds__(256, (v2_min_waves<3, kUnrollV2Rgb, true, false, false>())) void parts_isi(SeriesArgs a) {
     series_v2_body<3, 0, kUnrollV2Rgb, true, false, kAuxNT, kAuxNT, 1, false, 1>(a);
+}
+// the same in 1024-thread workgroups: the 16 waves of a CU (at 4 per SIMD)
+// take 16 adjacent tiles, 61 KB of each frame, instead of 4 groups of 4
+__global__ __launch_bounds__(1024, (v2_min_waves<3, kUnrollV2Rgb, true, false, false>())) void parts_isi_wg16(SeriesArgs a) {
+    series_v2_body<3, 0, kUnrollV2Rgb, true, false, kAuxNT, kAuxNT, 1, false, 1, 16>(a);
 }
 
 struct Kind {
@@ -95,9 +102,12 @@ int main(int argc, char** argv) {
     for (size_t j = 1; j < ok.size(); ++j)
         if (hipMemcpy(bufs[ok[j]], bufs[ok[0]], total, hipMemcpyDeviceToDevice) != hipSuccess) return 1;
     std::vector<uint32_t> Ls = {0};  // 0: the shipped schedule
+    std::vector<bool> xcd = {false};
     if (argc > 5)
         for (char* q = argv[5]; *q;) {
             Ls.push_back((uint32_t)strtoul(q, &q, 10));
+            xcd.push_back(*q == 'x');
+            if (*q == 'x') ++q;
             if (*q == ',') ++q;
         }
     const void* k0 = series_v2_kernel_ptr(3, 0, true, false, false, 1);
@@ -126,20 +136,22 @@ int main(int argc, char** argv) {
             const size_t i = ok[vv / Ls.size()];
             const uint32_t L = Ls[vv % Ls.size()];
             (void)0;
-            const void* k = L == 0 ? k0 : (const void*)&parts_isi;
+            const bool X = xcd[vv % Ls.size()];
+            const void* k = L == 0 ? k0 : (X ? (const void*)&parts_isi_wg16 : (const void*)&parts_isi);
             SeriesArgs args = a;
             args.frames = bufs[i];
             args.ref0 = bufs[i];
             args.part_frames = L;
             if (L != 0 && argc > 6) args.n_waves = (uint32_t)atoi(argv[6]);
-            const uint32_t blocks = (args.n_waves + 3) / 4;
+            const uint32_t wpb = X ? 16u : 4u;  // waves per workgroup
+            const uint32_t blocks = (args.n_waves + wpb - 1) / wpb;
             std::vector<float> ms;
             const double t0 = now();
             while (now() - t0 < secs) {
                 (void)hipMemsetAsync(series, 0, sizeof(dips_series_entry) * F, 0);
                 if (hipEventRecord(e0, 0) != hipSuccess) return 1;
                 void* params[] = {&args};
-                if (hipLaunchKernel(k, dim3(blocks), dim3(256), params, 0, 0) != hipSuccess) return 1;
+                if (hipLaunchKernel(k, dim3(blocks), dim3(wpb * 64u), params, 0, 0) != hipSuccess) return 1;
                 if (hipEventRecord(e1, 0) != hipSuccess) return 1;
                 if (launch_series_reduce(partials, F, a.n_tiles, 0, series, 0) != hipSuccess) return 1;
                 if (hipDeviceSynchronize() != hipSuccess) return 1;
@@ -159,8 +171,8 @@ int main(int argc, char** argv) {
             });
             std::sort(ms.begin(), ms.end());
             const double med = ms[ms.size() / 2];
-            printf("run\t%d\t%s#%zu/%s%u%s\t%.6f\t%.6f\t%.4f\t%.4f\t%u\n", r, kinds[i].name, i, L ? "P" : "S", L,
-                   same ? "" : " DIFF", t0, t1, med,
+            printf("run\t%d\t%s#%zu/%s%u%s%s\t%.6f\t%.6f\t%.4f\t%.4f\t%u\n", r, kinds[i].name, i, L ? "P" : "S", L,
+                   X ? "x" : "", same ? "" : " DIFF", t0, t1, med,
                    (double)total / (med / 1e3) / 8e12, F);
             fflush(stdout);
         }

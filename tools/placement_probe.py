@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--launches", type=int, default=3)
     ap.add_argument("--slices", type=int, default=16)
     ap.add_argument("--vmm", action="store_true", help="buffers through the HIP virtual-memory API instead")
+    ap.add_argument("--pair", default="", help="e.g. 'vd' / 'dv': a 1 GiB-aligned virtual-memory buffer (v) and a "
+                    "torch one (d), allocated in this order, then measured alternately, twice each")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -68,7 +70,7 @@ def main():
                "slice_GB": round(step / 1e9, 2)}
         print(json.dumps(rec), flush=True)
 
-    if not args.vmm:
+    if not args.vmm and not args.pair:
         a = torch.empty(F * fb, dtype=torch.uint8, device=dev)
         b = torch.empty(F * fb, dtype=torch.uint8, device=dev)
         measure("A", a)
@@ -98,6 +100,25 @@ def main():
         def __init__(self, ptr, n):
             self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False), "version": 3}
 
+    if args.pair:
+        bufs = []
+        for kind in args.pair:
+            if kind == "d":
+                bufs.append(("torch default", torch.empty(F * fb, dtype=torch.uint8, device=dev)))
+                continue
+            ptr = ctypes.c_void_p()
+            bid = vmm.vmm_alloc(0, size, GiB, size, ctypes.byref(ptr))
+            if bid < 0:
+                raise SystemExit(f"vmm_alloc failed: {bid}")
+            bufs.append(("vmm: 1 GiB-aligned, one physical allocation",
+                         torch.as_tensor(_Dev(ptr.value, size), device=dev)[: F * fb]))
+        for rep in range(2):
+            for name, buf in bufs:
+                measure(f"{name} (allocated #{[b[0] for b in bufs].index(name)}, pass {rep})", buf)
+        del bufs
+        torch.cuda.synchronize()
+        op.close()
+        return
     for name, align, chunk in (("vmm: 1 GiB-aligned, one physical allocation", GiB, size),
                                ("vmm: 2 MiB-aligned, one physical allocation", 2 * MiB, size),
                                ("vmm: 1 GiB-aligned, 1 GiB physical chunks", GiB, GiB),
