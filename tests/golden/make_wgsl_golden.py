@@ -93,6 +93,19 @@ CS_CASES = [
      [0, 1, 2, 3, DISPATCH, DISPATCH, 4, DISPATCH, 5, 6, DISPATCH, 7, DISPATCH, DISPATCH]),
 ]
 
+# added after the first set (generated after ALT_CASES, so that the earlier
+# fixtures keep their random frames): the windows 8-10, a window wider than
+# the frame, and a long op sequence that turns the ring over several times
+CS_CASES_2 = [
+    ((True, 8, 5.0, 0, 0), (16, 12), 6, ["random", "ties"], None),
+    ((False, 9, 5.0, 1, 1), (15, 11), 6, ["smooth"], None),
+    ((True, 10, 2.0, 255, 2), (14, 13), 6, ["random"], None),
+    ((True, 9, 5.0, 0, 3), (5, 4), 6, ["extreme", "random"], None),
+    ((True, 1, 5.0, 1, 0), (13, 7), 16, ["random", "smooth", "ties"],
+     [0, 1, DISPATCH, 2, 3, 4, DISPATCH, DISPATCH, 5, DISPATCH, 6, 7, 8, 9, DISPATCH, 10, DISPATCH, 11,
+      DISPATCH, 12, 13, 14, 15, DISPATCH, DISPATCH]),
+]
+
 # (num_textures, colorize, window, scalar, filter, chroma), (w, h), frames, kinds, refresh markers
 ALT_CASES = [
     ((2, True, 1, 5.0, 0, 0), (24, 14), 10, ["random"], [5]),
@@ -151,7 +164,8 @@ def main():
         "alt": [],
     }
     rng = np.random.default_rng(20261018)
-    for idx, (params, (w, h), n, kinds, ops) in enumerate(CS_CASES):
+
+    def cs_fixture(idx, params, w, h, n, kinds, ops):
         t0 = time.time()
         frames = mixed_frames(n, h, w, rng, kinds)
         ops = ops or default_ops(n)
@@ -163,6 +177,9 @@ def main():
         manifest["compute_state"].append({"file": name, "params": list(params), "width": w, "height": h,
                                           "content": kinds})
         print(f"{name} {params} {w}x{h} {time.time() - t0:.1f}s", flush=True)
+
+    for idx, (params, (w, h), n, kinds, ops) in enumerate(CS_CASES):
+        cs_fixture(idx, params, w, h, n, kinds, ops)
     for idx, (params, (w, h), n, kinds, markers) in enumerate(ALT_CASES):
         t0 = time.time()
         frames = mixed_frames(n, h, w, rng, kinds)
@@ -176,6 +193,8 @@ def main():
                                 "scalar": k, "filter": filt, "chroma": chroma, "markers": markers,
                                 "content": kinds})
         print(f"{name} {params} {w}x{h} {time.time() - t0:.1f}s", flush=True)
+    for idx, (params, (w, h), n, kinds, ops) in enumerate(CS_CASES_2):
+        cs_fixture(len(CS_CASES) + idx, params, w, h, n, kinds, ops)
     with open(os.path.join(HERE, "wgsl_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(f"wrote {len(manifest['compute_state'])} ComputeState + {len(manifest['alt'])} dips_alt fixtures")
