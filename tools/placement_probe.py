@@ -13,7 +13,7 @@ compute-free read of each of 16 equal slices -- so a slow region of the
 address space, if there is one, shows as slow slices.  Then B is freed, a
 third buffer C takes its place, and C is measured too.
 
-Run on the GPU box: python tools/placement_probe.py [--launches 3]
+Run on the GPU box: python tools/placement_probe.py [--launches 3] [--vmm | --pair vd]
 """
 from __future__ import annotations
 
@@ -113,8 +113,8 @@ def main():
             bufs.append(("vmm: 1 GiB-aligned, one physical allocation",
                          torch.as_tensor(_Dev(ptr.value, size), device=dev)[: F * fb]))
         for rep in range(2):
-            for name, buf in bufs:
-                measure(f"{name} (allocated #{[b[0] for b in bufs].index(name)}, pass {rep})", buf)
+            for idx, (name, buf) in enumerate(bufs):
+                measure(f"{name} (allocated #{idx}, pass {rep})", buf)
         del bufs
         torch.cuda.synchronize()
         op.close()
