@@ -19,7 +19,7 @@ from typing import Callable, Iterable, Iterator, List, Optional, Tuple
 import numpy as np
 
 from . import _lib
-from ._lib import DipsError, DipsParams, SeriesEntry, check
+from ._lib import DipsError, DipsParams, check
 
 
 class DiPsFilter(enum.IntEnum):

@@ -15,7 +15,6 @@ import os
 import re
 import subprocess
 
-import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "dips_hip.h")
