@@ -3,7 +3,7 @@
 that costs the headline kernel.
 
 Round 3 found two 124 GB buffers of one process 2.5-3 points apart whatever
-their memory type ("Open items after round 3"); round 5 saw
+their memory type (HISTORY.md, "Open items after round 3"); round 5 saw
 consecutive bench processes alternate between ~72.5 % and ~74.7 %
 (`profiles/r05/ab_u5/`).  This allocates two such buffers in one process
 (A, then B; 249 GB of the 288 GB), fills both with the bench's frames, and
