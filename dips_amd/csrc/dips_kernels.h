@@ -253,7 +253,7 @@ hipError_t launch_series_gray_lut(const SeriesArgs& a, bool per_frame, bool map,
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
 hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, hipStream_t s);
-// read-only walk in the RGB8 / RGBA8 series kernel's shape (vec_bytes 12 / 16, U = kUnrollV2)
+// read-only walk in the RGB8 / RGBA8 series kernel's shape (vec_bytes 12 / 16, U = kUnrollV2Rgb / kUnrollV2)
 hipError_t launch_read_walk(const SeriesArgs& a, int vec_bytes, uint32_t blocks, uint32_t* out, hipStream_t s);
 hipError_t launch_compat_precompute(const CompatArgs& a, hipStream_t s);
 hipError_t launch_compat_main(const CompatArgs& a, hipStream_t s);
