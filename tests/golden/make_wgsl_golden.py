@@ -121,6 +121,18 @@ ALT_CASES = [
 ]
 
 
+# added after the first sets, generated last: the dips_alt windows 4, 6, 9
+# and 11, a frame narrower than the window, and a long loop with several
+# refresh markers
+ALT_CASES_2 = [
+    ((2, True, 4, 5.0, 0, 0), (15, 11), 8, ["random", "ties"], [5]),
+    ((3, False, 6, 2.0, 1, 1), (14, 10), 8, ["smooth"], []),
+    ((2, True, 9, 5.0, 0, 2), (13, 9), 7, ["random"], [4]),
+    ((2, True, 11, 5.0, 1, 0), (6, 5), 7, ["extreme", "random"], []),
+    ((4, True, 1, 5.0, 0, 3), (17, 8), 24, ["random", "smooth", "gray"], [6, 11, 12, 19]),
+]
+
+
 def _save(name, **arrays):
     path = os.path.join(HERE, name)
     if os.path.exists(path):
@@ -180,7 +192,8 @@ def main():
 
     for idx, (params, (w, h), n, kinds, ops) in enumerate(CS_CASES):
         cs_fixture(idx, params, w, h, n, kinds, ops)
-    for idx, (params, (w, h), n, kinds, markers) in enumerate(ALT_CASES):
+
+    def alt_fixture(idx, params, w, h, n, kinds, markers):
         t0 = time.time()
         frames = mixed_frames(n, h, w, rng, kinds)
         n_tex, col, win, k, filt, chroma = params
@@ -193,8 +206,13 @@ def main():
                                 "scalar": k, "filter": filt, "chroma": chroma, "markers": markers,
                                 "content": kinds})
         print(f"{name} {params} {w}x{h} {time.time() - t0:.1f}s", flush=True)
+
+    for idx, (params, (w, h), n, kinds, markers) in enumerate(ALT_CASES):
+        alt_fixture(idx, params, w, h, n, kinds, markers)
     for idx, (params, (w, h), n, kinds, ops) in enumerate(CS_CASES_2):
         cs_fixture(len(CS_CASES) + idx, params, w, h, n, kinds, ops)
+    for idx, (params, (w, h), n, kinds, markers) in enumerate(ALT_CASES_2):
+        alt_fixture(len(ALT_CASES) + idx, params, w, h, n, kinds, markers)
     with open(os.path.join(HERE, "wgsl_manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(f"wrote {len(manifest['compute_state'])} ComputeState + {len(manifest['alt'])} dips_alt fixtures")
