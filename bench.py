@@ -80,6 +80,9 @@ def parse():
                     help="skip the configs[3] / configs[4] legs (profiling runs)")
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of each configs[3] / configs[4] leg")
     ap.add_argument("--no-per-frame-call", action="store_true", help="skip the per_frame_call leg")
+    ap.add_argument("--no-placement-probe", action="store_true",
+                    help="one plain allocation of the frame batch instead of the faster of two candidate "
+                         "placements (dips_amd.placement.resident_frames)")
     ap.add_argument("--per-frame-calls", type=int, default=200,
                     help="timed dips_frame_callback calls of the per_frame_call leg (4K RGBA8)")
     ap.add_argument("--dump-series", default=None,
@@ -434,6 +437,15 @@ def _devices(torch, dist, world, local):
     return out
 
 
+def _gather_objects(dist, world, obj):
+    """Every rank's obj, in rank order (all_gather_object)."""
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def _max_over_ranks(torch, dist, world, dev, values):
     t = torch.tensor(values, dtype=torch.float64, device=dev)
     if world > 1:
@@ -739,8 +751,13 @@ def _main(args):
     op = DiffSeriesOperator(PixelFormat.RGB8, mode, args.tau, time_kernel=True, device=local)
 
     t0 = rank * F  # global frame index of this rank's first frame
-    frames = torch.empty((F, H, W, C), dtype=torch.uint8, device=dev)
-    op.synth_device(frames, W, H, SEED, t0)
+    # the batch in the faster of two candidate placements (where the driver
+    # puts a 124 GB buffer moves this power-bound kernel by 2-3 points;
+    # dips_amd/placement.py), both candidates' times reported in the line
+    from dips_amd.placement import resident_frames
+    frames, placement = resident_frames(
+        op, (F, H, W, C), dev, lambda t: op.synth_device(t, W, H, SEED, t0),
+        probe=not args.no_placement_probe, ref_of=(lambda t: t[0]) if mode == Mode.Overall else None)
     series = torch.zeros((F, 4), dtype=torch.int64, device=dev)
     ref = torch.empty((H, W, C), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
@@ -815,6 +832,7 @@ def _main(args):
     elapsed_max, kernel_ms = float(tt[0]), float(tt[1])
 
     devices = _devices(torch, dist, world, local)
+    placements = _gather_objects(dist, world, placement)
     # Self-check of the timed step at every world size (collective): each
     # rank re-derives its first entries against the halo / reference it
     # received, rank 0 re-derives the gathered rows at every shard boundary
@@ -972,6 +990,7 @@ def _main(args):
             },
             "ranks": world,
             "devices": devices,
+            "placement": placements,
             "check": check,
             "roofline": {
                 "bound": "hbm",

@@ -13,7 +13,7 @@ mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d $OUT/$c -o run -- \
     python3 bench.py --frames-per-gpu $F --steps 2 --warmup 1 --mode $MODE --no-cpu-baseline --no-pcie \
-    --no-tau0 --no-legs --no-per-frame-call --map-frames 2500 > $OUT/$c.log 2>&1
+    --no-tau0 --no-legs --no-per-frame-call --no-placement-probe --map-frames 2500 > $OUT/$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 PF=$([ "$MODE" = per-frame ] && echo true || echo false)

@@ -23,7 +23,7 @@ cp gpurun_out/pmc_traffic_map.json $O/pmc_traffic_map.json
 timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.log; rc=$?
 cat $O/bench.json; [ $rc -ne 0 ] && { tail -5 $O/bench.log; exit $rc; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- \
-  python3 bench.py --no-cpu-baseline --no-pcie --no-map --no-check --no-legs --no-per-frame-call \
+  python3 bench.py --no-cpu-baseline --no-pcie --no-map --no-check --no-legs --no-per-frame-call --no-placement-probe \
   > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.log
 rc=$?; echo "rocprof bench rc=$rc"; exit $rc
 fi
