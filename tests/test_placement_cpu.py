@@ -1,0 +1,68 @@
+"""The selection logic of dips_amd.placement.resident_frames on the CPU
+(torch.cuda calls stubbed; a fake operator whose launches on the second
+candidate take longer, or shorter): the faster candidate is kept and holds
+the fill, both timings are reported, the timer is left reset, and the plain
+paths (probe=False, no room for two, an empty batch) allocate once."""
+import pytest
+import torch
+
+from dips_amd import placement
+
+
+class _FakeOp:
+    def __init__(self, slow_second):
+        self.slow_second = slow_second
+        self.seen = []
+        self.ms = 0.0
+        self.n = 0
+
+    def run_device(self, frames, series, ref=None):
+        if frames.data_ptr() not in self.seen:
+            self.seen.append(frames.data_ptr())
+        second = self.seen.index(frames.data_ptr()) == 1
+        self.ms += (21.2 if second == self.slow_second else 20.7)
+        self.n += 1
+
+    def kernel_time(self, reset=False):
+        out = (self.ms, self.n)
+        if reset:
+            self.ms, self.n = 0.0, 0
+        return out
+
+
+@pytest.fixture
+def no_cuda(monkeypatch):
+    state = {"free": 1 << 40}
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (state["free"], 1 << 40))
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda dev=None: None)
+    monkeypatch.setattr(torch.cuda, "empty_cache", lambda: None)
+    return state
+
+
+@pytest.mark.parametrize("slow_second", [True, False])
+def test_keeps_the_faster_candidate(no_cuda, slow_second):
+    op = _FakeOp(slow_second)
+    fills = []
+
+    def fill(t):
+        t.fill_(7)
+        fills.append(t.data_ptr())
+
+    t, rep = placement.resident_frames(op, (4, 3, 5, 3), "cpu", fill, launches=2)
+    assert rep["probe"] and rep["launches_each"] == 2
+    assert rep["kept"] == (0 if slow_second else 1)
+    assert rep["candidate_kernel_ms"] == ([20.7, 21.2] if slow_second else [21.2, 20.7])
+    assert t.data_ptr() == fills[rep["kept"]] and int(t.sum()) == 7 * t.numel()
+    assert op.kernel_time() == (0.0, 0)  # left reset
+
+
+def test_plain_paths(no_cuda):
+    op = _FakeOp(True)
+    t, rep = placement.resident_frames(op, (4, 3, 5, 3), "cpu", lambda x: x.fill_(1), probe=False)
+    assert rep == {"probe": False, "reason": "disabled"} and op.n == 0 and int(t.sum()) == t.numel()
+    no_cuda["free"] = 100  # no room for two candidates
+    t, rep = placement.resident_frames(op, (4, 3, 5, 3), "cpu", lambda x: x.fill_(1))
+    assert rep == {"probe": False, "reason": "no room for two candidates"} and op.n == 0
+    no_cuda["free"] = 1 << 40
+    t, rep = placement.resident_frames(op, (0, 3, 5, 3), "cpu", lambda x: None)
+    assert rep == {"probe": False, "reason": "empty batch"} and tuple(t.shape) == (0, 3, 5, 3)
