@@ -50,9 +50,12 @@ uint64_t waves_per_simd(uint64_t occupancy) {
 // 74.1 against 72.05 % (profiles/r03/parts/, profiles/r04/l/).  Parts of at
 // least 128 frames (each item re-reads its reference tile: +1/L of the
 // traffic), P from the one that gives every resident wave slot an item up to
-// 4x that: the smallest whose items fill >= 95 % of the slots (k items per
-// slot), else the best-filling one; the waves then get ceil(items / n_waves)
-// or one fewer items each (4K RGB8, 5000 frames, U = 5: L = 1000, 4,050 waves).
+// 4x that: the smallest whose items fill >= 98 % of the slots (k items per
+// slot), else the best-filling one (98 rather than 95 %: 8K's 3 parts fill
+// 99.9 % against 2 parts' 97.4 %, +0.5 points in alternated runs,
+// profiles/r05/ab_fill/; every other config keeps its part count); the
+// waves then get ceil(items / n_waves) or one fewer items each (4K RGB8, 5000
+// frames, U = 5: L = 1000, 4,050 waves).
 // Batches of fewer than 256 frames keep the contiguous ranges.
 void part_geometry(FastGeom& g, uint64_t n_frames, uint64_t resident) {
     if (n_frames < 256 || g.n_tiles == 0 || resident == 0) return;
@@ -71,7 +74,7 @@ void part_geometry(FastGeom& g, uint64_t n_frames, uint64_t resident) {
             best_fill = fill;
             best_p = p;
         }
-        if (fill >= 0.95) break;
+        if (fill >= 0.98) break;
     }
     const uint64_t L = (n_frames + best_p - 1) / best_p;
     const uint64_t items = ((n_frames + L - 1) / L) * g.n_tiles;

@@ -32,7 +32,7 @@ def part_schedule(n_tiles: int, n_frames: int, resident: int):
         fill = items / (k * resident)
         if fill > best_fill + 1e-9:
             best_fill, best_p = fill, p
-        if fill >= 0.95:
+        if fill >= 0.98:
             break
     L = (n_frames + best_p - 1) // best_p
     parts = (n_frames + L - 1) // L
