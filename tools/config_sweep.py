@@ -43,9 +43,12 @@ def main():
     ap.add_argument("--gray-kernel", choices=sorted(_GRAY_FORMS), default="auto",
                     help="GRAY8: the table kernel with its per-workgroup layout choice (auto, the library "
                          "default), the band-keyed or the pair-keyed table pinned, or the f32 kernel")
+    ap.add_argument("--no-placement-probe", action="store_true",
+                    help="one plain allocation per config (dips_amd.placement.resident_frames probe=False)")
     args = ap.parse_args()
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    from dips_amd.placement import resident_frames
     from oracle import oracle
 
     import bench  # the power legs: energy counter / PPT residency / gfx clock around a leg
@@ -55,10 +58,11 @@ def main():
         if args.only and args.only not in name:
             continue
         shape = (F, H, W) if C == 1 else (F, H, W, C)
-        frames = torch.empty(shape, dtype=torch.uint8, device=dev)
         op = DiffSeriesOperator(PixelFormat(C), Mode(mode), tau, time_kernel=True,
                                 **(_GRAY_FORMS[args.gray_kernel] if C == 1 else {}))
-        op.synth_device(frames, W, H, 0xD1B5, 0)
+        # the batch in the faster of two candidate placements, as bench.py
+        frames, placement = resident_frames(op, shape, dev, lambda t: op.synth_device(t, W, H, 0xD1B5, 0),
+                                            probe=not args.no_placement_probe)
         series = torch.zeros((F, 4), dtype=torch.int64, device=dev)
         op.run_device(frames, series)
         torch.cuda.synchronize()
@@ -90,6 +94,7 @@ def main():
                           "read_ceiling": {"ms": round(read_ms, 4),
                                            "frac_of_8TBps": round(F * fb / (read_ms / 1e3) / 8e12, 4),
                                            "power": read_power},
+                          "placement": placement,
                           "first_frames_match_oracle": ok}), flush=True)
         op.close()
         del frames, series
