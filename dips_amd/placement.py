@@ -40,7 +40,14 @@ def resident_frames(op, shape: Tuple[int, ...], device, fill: Callable, probe: b
         report["reason"] = "disabled" if not probe else ("empty batch" if shape[0] == 0 else
                                                           "no room for two candidates")
         return t, report
-    cands = [torch.empty(shape, dtype=torch.uint8, device=device) for _ in range(2)]
+    cands = [torch.empty(shape, dtype=torch.uint8, device=device)]
+    try:
+        cands.append(torch.empty(shape, dtype=torch.uint8, device=device))
+    except torch.cuda.OutOfMemoryError:  # reported free, not allocatable: one plain buffer
+        torch.cuda.empty_cache()
+        fill(cands[0])
+        report["reason"] = "second candidate not allocatable"
+        return cands[0], report
     series = torch.empty((shape[0], 4), dtype=torch.int64, device=device)
     ms = []
     for c in cands:

@@ -66,3 +66,20 @@ def test_plain_paths(no_cuda):
     no_cuda["free"] = 1 << 40
     t, rep = placement.resident_frames(op, (0, 3, 5, 3), "cpu", lambda x: None)
     assert rep == {"probe": False, "reason": "empty batch"} and tuple(t.shape) == (0, 3, 5, 3)
+
+
+def test_second_candidate_not_allocatable(no_cuda, monkeypatch):
+    op = _FakeOp(True)
+    real_empty = torch.empty
+    calls = []
+
+    def empty(*a, **k):
+        calls.append(1)
+        if len(calls) == 2:
+            raise torch.cuda.OutOfMemoryError("no room")
+        return real_empty(*a, **k)
+
+    monkeypatch.setattr(torch, "empty", empty)
+    t, rep = placement.resident_frames(op, (4, 3, 5, 3), "cpu", lambda x: x.fill_(2))
+    assert rep == {"probe": False, "reason": "second candidate not allocatable"}
+    assert op.n == 0 and int(t.sum()) == 2 * t.numel()
