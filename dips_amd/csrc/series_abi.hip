@@ -196,9 +196,9 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     const bool kzero = g.ok && (glut || C != 1) && n_frames < (1u << 30);
     if (!kzero) DIPS_HIP(h, hipMemsetAsync(series, 0, sizeof(dips_series_entry) * (size_t)n_frames, s));
     auto launch_generic = [&](uint64_t px0) -> dips_status {
-        const uint64_t bpf = (npx - px0 + 255u) / 256u;
-        if (bpf * (uint64_t)n_frames >= (1ull << 31))
-            return fail(h, DIPS_ERR_INVALID, "frame batch too large for the generic kernel; split the batch");
+        const uint64_t bpf = (npx - px0 + 255u) / 256u;  // 256-pixel segments per frame
+        if (bpf >= (1ull << 32))
+            return fail(h, DIPS_ERR_INVALID, "frame too large for the generic kernel (2^40 pixels)");
         dips::GenericArgs a{};
         a.frames = frames;
         a.ref0 = ref0;

@@ -471,15 +471,10 @@ hipError_t launch_read_ceiling(const uint8_t* p, uint64_t bytes, uint32_t* out, 
     return hipGetLastError();
 }
 
-// Generic path: any frame shape and alignment.  One thread per pixel, the
-// intensity computed in the reference's own form ((cmax+cmin)/2.0,
-// dips_shader.wgsl:73-81) rather than the fast kernel's I2 pairs, so the two
-// kernels cross-check each other.
 template <int C>
-__global__ __launch_bounds__(256) void series_generic_kernel(GenericArgs a) {
-    __shared__ uint64_t red[4][4];
-    const uint32_t t = blockIdx.x / a.blocks_per_frame;
-    const uint64_t p = a.px0 + (uint64_t)(blockIdx.x - t * a.blocks_per_frame) * 256u + threadIdx.x;
+__device__ __forceinline__ void generic_segment(const GenericArgs& a, uint64_t seg, uint64_t (&red)[4][4]) {
+    const uint32_t t = (uint32_t)(seg / a.blocks_per_frame);
+    const uint64_t p = a.px0 + (seg - (uint64_t)t * a.blocks_per_frame) * 256u + threadIdx.x;
     const uint64_t fb = a.frame_bytes;
     const uint8_t* F = a.frames + (uint64_t)t * fb;
     const uint8_t* R = a.mode == 1u ? (t == 0 ? a.ref0 : a.frames + (uint64_t)(t - 1) * fb) : a.ref0;
@@ -533,6 +528,24 @@ __global__ __launch_bounds__(256) void series_generic_kernel(GenericArgs a) {
     if (threadIdx.x < 4) {
         const uint64_t v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
         atomicAdd(reinterpret_cast<unsigned long long*>(&a.series[t]) + threadIdx.x, (unsigned long long)v);
+    }
+    __syncthreads();  // red is reused by the next segment
+}
+
+// Generic path: any frame shape and alignment.  One thread per pixel, the
+// intensity computed in the reference's own form ((cmax+cmin)/2.0,
+// dips_shader.wgsl:73-81) rather than the fast kernel's I2 pairs, so the two
+// kernels cross-check each other.  Each workgroup walks 256-pixel segments
+// with a stride of the grid: a dispatch's grid is at most 2^32 work-items,
+// which two GRAY8 frames of 2^31 pixels already exceed
+// (tests/test_gpu_max_frames.py; the launch then ran only the grid size
+// modulo 2^32).
+template <int C>
+__global__ __launch_bounds__(256) void series_generic_kernel(GenericArgs a) {
+    __shared__ uint64_t red[4][4];
+    const uint64_t n_seg = (uint64_t)a.blocks_per_frame * a.n_frames;
+    for (uint64_t seg = blockIdx.x; seg < n_seg; seg += gridDim.x) {
+        generic_segment<C>(a, seg, red);
     }
 }
 
@@ -668,7 +681,11 @@ hipError_t launch_series_reduce(const uint64_t* partials, uint32_t n_frames, uin
 }
 
 hipError_t launch_series_generic(const GenericArgs& a, int channels, hipStream_t s) {
-    const uint64_t blocks = (uint64_t)a.blocks_per_frame * a.n_frames;
+    // one workgroup per 256-pixel segment up to 4 M of them (every batch below
+    // that launches as before); past it the workgroups loop over segments
+    const uint64_t n_seg = (uint64_t)a.blocks_per_frame * a.n_frames;
+    const uint64_t blocks = n_seg < (1ull << 22) ? n_seg : (1ull << 22);
+    if (blocks == 0) return hipSuccess;
     switch (channels) {
         case 1: hipLaunchKernelGGL(series_generic_kernel<1>, dim3((uint32_t)blocks), dim3(256), 0, s, a); break;
         case 3: hipLaunchKernelGGL(series_generic_kernel<3>, dim3((uint32_t)blocks), dim3(256), 0, s, a); break;
