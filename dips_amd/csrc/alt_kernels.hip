@@ -524,6 +524,7 @@ hipError_t launch_frame_host_n(const AltArgs& a, const uint8_t* in, uint8_t* new
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (a.y0 >= yend || yend > a.height || a.window > 1 || newest >= (uint32_t)N) return hipErrorInvalidValue;
     const uint64_t n_px = (uint64_t)(yend - a.y0) * a.width;
+    if (!fits_grid256(n_px)) return hipErrorInvalidValue;
     hipLaunchKernelGGL((alt_frame_host_kernel<N>), dim3((uint32_t)((n_px + 255) / 256)), dim3(256), 0, s, a, in,
                        newest_slot, newest);
     return hipGetLastError();

@@ -307,6 +307,7 @@ __global__ __launch_bounds__(256) void compat_quantise_slot_kernel(uint8_t* slot
 
 hipError_t launch_compat_quantise_slot(uint8_t* slot, uint64_t n_px, uint32_t chroma, hipStream_t s) {
     if (n_px == 0) return hipSuccess;
+    if (!fits_grid256(n_px)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(compat_quantise_slot_kernel, dim3((uint32_t)((n_px + 255) / 256)), dim3(256), 0, s, slot, n_px,
                        chroma);
     return hipGetLastError();
@@ -314,6 +315,7 @@ hipError_t launch_compat_quantise_slot(uint8_t* slot, uint64_t n_px, uint32_t ch
 
 hipError_t launch_compat_gray(const uint8_t* src, uint8_t* dst, uint64_t n_px, uint32_t chroma, hipStream_t s) {
     if (n_px == 0) return hipSuccess;
+    if (!fits_grid256(n_px)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(compat_gray_kernel, dim3((uint32_t)((n_px + 255) / 256)), dim3(256), 0, s, src, dst, n_px, chroma);
     return hipGetLastError();
 }
@@ -427,7 +429,7 @@ static hipError_t launch_host_copy(const uint8_t* src, uint8_t* dst, uint64_t by
     if (!w8 && (bytes % 4u != 0 || ((uintptr_t)src & 3u) != 0 || ((uintptr_t)dst & 3u) != 0))
         return hipErrorInvalidValue;
     const uint64_t n = w8 ? bytes / 8u : bytes / 4u;
-    if ((n + 255) / 256 >= (1ull << 31)) return hipErrorInvalidValue;
+    if (!fits_grid256(n)) return hipErrorInvalidValue;
     const dim3 grid((uint32_t)((n + 255) / 256));
     if (w8) {
         auto* a = reinterpret_cast<const uint64_t*>(src);
@@ -474,6 +476,7 @@ hipError_t launch_compat_main_host(const CompatArgs& a, hipStream_t s, int slot_
     const uint32_t yend = a.y1 ? a.y1 : a.height;
     if (a.y0 >= yend || yend > a.height) return hipErrorInvalidValue;
     const uint64_t n_px = (uint64_t)(yend - a.y0) * a.width;
+    if (!fits_grid256(n_px)) return hipErrorInvalidValue;
     if (a.out_key != 0u && a.in_key != 0u) {
         const uint32_t G = 4u / a.in_key;
         const uint64_t p0 = (uint64_t)a.y0 * a.width, p1 = (uint64_t)yend * a.width;

@@ -9,6 +9,12 @@
 namespace dips {
 
 // Unroll (vecs per lane) of the fast series kernel; a tile = 64 * U vecs.
+// A dispatch holds fewer than 2^32 work-items (the grid size is a 32-bit
+// count of work-items, not of workgroups): one-dimensional launches of
+// 256-thread workgroups over n items must check n against this, or the grid
+// wraps and the launch silently runs only the remainder.
+constexpr bool fits_grid256(uint64_t n) { return n <= (1ull << 32) - 256u; }
+
 constexpr int kUnrollRGB = 4;   // 1024 px / wave / frame for RGB8 and RGBA8
 constexpr int kUnrollGray = 2;  // 2048 px / wave / frame for GRAY8
 constexpr int kUnrollV2 = 4;    // series_v2_kernel RGBA8: 1024 px / wave / frame
