@@ -3,7 +3,7 @@ shape (the default shape is what the driver runs; this checks the line's
 form, not its number): every required key with its type, value = frames /
 step time, roofline.frac = achieved / peak with the guide's 8 TB/s HBM peak,
 a cpu_baseline of kind "port" with its core count and sample, the self-check
-passed, and one JSON line on stdout."""
+passed, the batch's placement report, and one JSON line on stdout."""
 import json
 import os
 import subprocess
@@ -46,3 +46,8 @@ def test_bench_line_keeps_the_contract():
     assert isinstance(c["cores"], int) and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
     assert c["series_matches_gpu"] is True
     assert d["check"]["equal"] is True
+    # the batch's placement: both candidates timed, the faster kept (dips_amd/placement.py)
+    pl = d["placement"]
+    assert isinstance(pl, list) and len(pl) == 1 and pl[0]["probe"] is True
+    ms = pl[0]["candidate_kernel_ms"]
+    assert len(ms) == 2 and ms[pl[0]["kept"]] == min(ms)
