@@ -11,6 +11,12 @@ reference frame is broadcast once at setup).
 
 A step = one pass of the hot path over the rank's resident frame batch:
 series kernel + reduction (+ halo exchange + series gather when N > 1).
+At N > 1 the step is ONE call of the library's native sharded entry point,
+dips_diff_series_sharded (shard_abi.hip), over an RCCL communicator the
+ranks build from a unique id passed over the torch process group: the halo
+ncclSend/ncclRecv beside the series launch and one ncclGather of the series,
+all inside libdips_hip.so.  (DIPS_BENCH_SHARD=torch runs the older
+Python-level protocol of dips_amd.shard over torch.distributed instead.)
 Frames are generated into HBM by the shared integer generator before timing.
 
 After the timed steps, at every N (the driver's 8-GPU run included):
@@ -81,8 +87,8 @@ def parse():
     ap.add_argument("--leg-steps", type=int, default=5, help="timed steps of each configs[3] / configs[4] leg")
     ap.add_argument("--no-per-frame-call", action="store_true", help="skip the per_frame_call leg")
     ap.add_argument("--no-placement-probe", action="store_true",
-                    help="one plain allocation of the frame batch instead of the faster of two candidate "
-                         "placements (dips_amd.placement.resident_frames)")
+                    help="one plain allocation of the frame batch instead of the probed choice between two "
+                         "candidate placements (tools/placement.py resident_frames)")
     ap.add_argument("--per-frame-calls", type=int, default=200,
                     help="timed dips_frame_callback calls of the per_frame_call leg (4K RGBA8)")
     ap.add_argument("--dump-series", default=None,
@@ -383,7 +389,7 @@ def _map_variant(torch, op_cls, frames, n, W, H, mode_pf, tau):
         op.close()
 
 
-def _tau0_leg(torch, smp, op_cls, frames, series_hl, mode_pf, tau_hl, steps):
+def _tau0_leg(torch, smp, op_cls, frames, series_hl, mode_pf, tau_hl, steps, device=0):
     """The headline shape at tau = 0 (BASELINE.json configs[2] does not state
     tau): every pixel with dI > 0 counted, the exact f64 intensity sum
     (series_v2.hip ISI = 0) instead of the integer sum the headline's tau >=
@@ -393,7 +399,9 @@ def _tau0_leg(torch, smp, op_cls, frames, series_hl, mode_pf, tau_hl, steps):
     from dips_amd import Mode, PixelFormat
     F = frames.shape[0]
     fb = frames[0].numel()
-    op = op_cls(PixelFormat.RGB8, Mode.PerFrame if mode_pf else Mode.Overall, 0.0, time_kernel=True)
+    # N = 1 only (bench.py runs it there): one launch over the whole batch,
+    # the headline's own path at one rank
+    op = op_cls(PixelFormat.RGB8, Mode.PerFrame if mode_pf else Mode.Overall, 0.0, time_kernel=True, device=device)
     try:
         ser = torch.zeros((F, 4), dtype=torch.int64, device=frames.device)
         op.run_device(frames, ser)  # warm
@@ -425,6 +433,21 @@ def _tau0_leg(torch, smp, op_cls, frames, series_hl, mode_pf, tau_hl, steps):
         op.close()
 
 
+def _plain_allocation(placement, algo_bytes, kernel_ms):
+    """roofline.plain_kernel_ms / plain_frac: the series kernel on the plain
+    (first) allocation of the batch, next to the headline's kept one."""
+    if placement.get("probe"):
+        ms = float(placement["candidate_kernel_ms"][0])
+        note = ("candidate 0 (the plain allocation): median of its probe launches; the headline ran on "
+                f"candidate {placement['kept']}")
+    else:
+        ms = kernel_ms
+        note = "no placement probe: the headline ran on the plain allocation"
+    return {"plain_kernel_ms": round(ms, 4),
+            "plain_frac": round(algo_bytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+            "plain_note": note}
+
+
 def _devices(torch, dist, world, local):
     """PCI bus id of every rank's GPU (all_gather), so the line proves which
     devices ran."""
@@ -435,6 +458,53 @@ def _devices(torch, dist, world, local):
     out = [None] * world
     dist.all_gather_object(out, mine)
     return out
+
+
+class _DamagingTransport:
+    """The rehearsal's host transport with the halo rank 1 receives damaged
+    on purpose (DIPS_BENCH_CORRUPT_HALO=1: the self-check must catch it)."""
+
+    def __init__(self, inner, rank):
+        self.inner, self.rank = inner, rank
+
+    def broadcast(self, buf, root):
+        self.inner.broadcast(buf, root)
+
+    def sendrecv(self, send, to, recv, src):
+        self.inner.sendrecv(send, to, recv, src)
+        if recv is not None and self.rank == 1:
+            recv[12345 % recv.size] ^= 0x5A
+
+    def gather(self, send, recv, root):
+        self.inner.gather(send, recv, root)
+
+
+def _make_comm(torch, dist, backend, world, rank, local, corrupt_halo):
+    """(communicator, note) of the native sharded path: RCCL over the ranks of
+    the process group (backend "nccl", the unique id broadcast over it), or
+    the host transport over gloo (the one-GPU rehearsal).  Every rank must get
+    one; otherwise all release theirs and return (None, why)."""
+    from dips_amd.comm import Comm, TorchHostTransport, rccl_from_process_group
+    comm, err = None, None
+    try:
+        if backend == "nccl":
+            comm = rccl_from_process_group(local)
+        else:
+            tr = TorchHostTransport()
+            comm = Comm.host(_DamagingTransport(tr, rank) if corrupt_halo else tr, world, rank, local)
+    except Exception as e:  # reported in the line, and the torch path runs instead
+        err = f"{type(e).__name__}: {e}"
+    flag = torch.tensor([0 if comm is not None else 1], dtype=torch.int64,
+                        device=torch.device("cuda", local) if backend == "nccl" else "cpu")
+    dist.all_reduce(flag)
+    if int(flag[0]) != 0:
+        if comm is not None:
+            comm.close()
+        log(f"rank {rank}: native communicator unavailable on {int(flag[0])} rank(s) ({err}); torch path")
+        return None, {"failed": err or "on another rank"}
+    kind = "rccl" if backend == "nccl" else f"host ({backend}, rehearsal)"
+    log(f"rank {rank}: native sharded path over {comm!r}")
+    return comm, {"transport": kind}
 
 
 def _gather_objects(dist, world, obj):
@@ -454,14 +524,16 @@ def _max_over_ranks(torch, dist, world, dev, values):
 
 
 def _config_leg(torch, dist, buf, *, name, W, H, F, mode, tau, steps, world, rank, local, dev, check=True,
-                dump=None):
+                dump=None, comm=None):
     """One more BASELINE.json config on the same ranks and the same resident
     buffer (regenerated in place, so HBM holds one batch at a time): 'overall'
     mode, the reference broadcast once (RCCL), each step the series kernel
-    over the rank's F frames + one gather of the series; then the same
-    self-check as the headline.  Returns its frames/s, roofline fraction,
-    RCCL times and check."""
+    over the rank's F frames + one gather of the series -- one
+    dips_diff_series_sharded call with `comm` (the native path); then the
+    same self-check as the headline.  Returns its frames/s, roofline
+    fraction, RCCL times and check."""
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat, shard
+
     fb = W * H * 3
     if F * fb > buf.numel():
         raise ValueError("leg does not fit the resident buffer")
@@ -471,25 +543,38 @@ def _config_leg(torch, dist, buf, *, name, W, H, F, mode, tau, steps, world, ran
         op.synth_device(frames, W, H, SEED, rank * F)
         series = torch.zeros((F, 4), dtype=torch.int64, device=dev)
         ref = torch.empty((H, W, 3), dtype=torch.uint8, device=dev)
-        gather = shard.SeriesGather(world * F, dev)
+        native = comm is not None and world > 1
+        if native:
+            gathered = torch.zeros((world * F, 4), dtype=torch.int64, device=dev) if rank == 0 else None
+        else:
+            gather_t = shard.SeriesGather(world * F, dev)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t = time.perf_counter()
         if mode == Mode.Overall:
-            if rank == 0:
-                ref.copy_(frames[0])
-            shard.broadcast_reference(ref)
+            if native:
+                op.shard_broadcast_device(comm, frames[0] if rank == 0 else None, ref)
+            else:
+                if rank == 0:
+                    ref.copy_(frames[0])
+                shard.broadcast_reference(ref)
         torch.cuda.synchronize()
         ref_ms = (time.perf_counter() - t) * 1e3
 
         def compute():
-            if mode == Mode.Overall:
+            if native:
+                op.run_sharded(comm, frames, world * F, series, gathered,
+                               ref=ref if mode == Mode.Overall else None, ref_resident=mode == Mode.Overall)
+            elif mode == Mode.Overall:
                 op.run_device(frames, series, ref=ref)
             elif world == 1:
                 op.run_device(frames, series)
             else:
                 shard.per_frame_overlapped(frames, ref, series, lambda fr, r, out: op.run_device(fr, out, ref=r))
+
+        def gather(ser):
+            return gathered if native else gather_t(ser)
 
         compute()
         gather(series)  # warm
@@ -508,14 +593,17 @@ def _config_leg(torch, dist, buf, *, name, W, H, F, mode, tau, steps, world, ran
             dist.barrier()
         elapsed = time.perf_counter() - t
         kms, _ = op.kernel_time()
-        # the gather alone, once more (its share of a step)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        final = gather(series)
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - t) * 1e3
+        # the gather alone, once more (its share of a step; inside the
+        # sharded call on the native path, so not separable there)
+        gather_ms = 0.0
+        if not native:
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            final = gather(series)
+            torch.cuda.synchronize()
+            gather_ms = (time.perf_counter() - t) * 1e3
         elapsed, kms, gather_ms, ref_ms = _max_over_ranks(torch, dist, world, dev,
                                                           [elapsed, kms / steps, gather_ms, ref_ms])
         chk = None
@@ -533,7 +621,9 @@ def _config_leg(torch, dist, buf, *, name, W, H, F, mode, tau, steps, world, ran
                 "steps": steps, "frames_per_s": round(world * F * steps / elapsed, 2),
                 "ms_per_step": round(elapsed / steps * 1e3, 4),
                 "kernel_ms": round(kms, 4), "achieved_GBps": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
-                "rccl_gather_ms": round(gather_ms, 4) if world > 1 else 0.0,
+                "rccl_gather_ms": (round(gather_ms, 4) if world > 1 and not native else
+                                   ("inside dips_diff_series_sharded" if native else 0.0)),
+                "step_minus_kernel_ms": round(elapsed / steps * 1e3 - kms, 4),
                 "rccl_reference_ms": round(ref_ms, 4) if world > 1 else 0.0,
                 "kernel": _v2_kernel_name(mode == Mode.PerFrame, tau),
                 "check": chk}
@@ -724,11 +814,13 @@ def _main(args):
         _WHO["bus"] = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
     except Exception:  # the report only
         pass
-    if world > 1:
-        # leave one wave slot per SIMD to RCCL's send/recv kernels (the halo
-        # exchange runs beside the persistent series kernel); 4 and 5 waves
-        # per SIMD run the kernel at the same speed
-        os.environ.setdefault("DIPS_SERIES_WAVES_PER_SIMD", "4")
+    shard_path = os.environ.get("DIPS_BENCH_SHARD", "native") if world > 1 else None
+    if shard_path == "torch":
+        # the Python-level protocol launches the series through run_device:
+        # leave one wave slot per SIMD (occupancy 4 - 1 for the RGB8 kernel)
+        # to the halo's send/recv kernels beside it; the native path reserves
+        # the slot itself (dips_shard_plan)
+        os.environ.setdefault("DIPS_SERIES_WAVES_PER_SIMD", "3")
     dev = torch.device("cuda", local)
     if world > 1:
         # a bounded wait: a rank stuck in a collective (a peer that died, a
@@ -744,6 +836,16 @@ def _main(args):
 
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat, shard
 
+    # the native sharded path's communicator: RCCL (driver runs) or the host
+    # transport over gloo (the one-GPU rehearsal); every rank must get one,
+    # else all fall back to the torch protocol and the line says why
+    comm, comm_note = None, None
+    if shard_path == "native":
+        comm, comm_note = _make_comm(torch, dist, backend, world, rank, local, corrupt_halo)
+        if comm is None:
+            shard_path = "torch"
+            os.environ.setdefault("DIPS_SERIES_WAVES_PER_SIMD", "3")
+
     W, H, F = args.width, args.height, args.frames_per_gpu
     C = 3
     fb = W * H * C
@@ -751,10 +853,11 @@ def _main(args):
     op = DiffSeriesOperator(PixelFormat.RGB8, mode, args.tau, time_kernel=True, device=local)
 
     t0 = rank * F  # global frame index of this rank's first frame
-    # the batch in the faster of two candidate placements (where the driver
-    # puts a 124 GB buffer moves this power-bound kernel by 2-3 points;
-    # dips_amd/placement.py), both candidates' times reported in the line
-    from dips_amd.placement import resident_frames
+    # the batch in the plain allocation, or in a second candidate placement
+    # when that runs faster by > 1 % (where the driver puts a 124 GB buffer
+    # moves this power-bound kernel by 2-3 points; tools/placement.py), both
+    # candidates' times reported in the line
+    from tools.placement import resident_frames
     frames, placement = resident_frames(
         op, (F, H, W, C), dev, lambda t: op.synth_device(t, W, H, SEED, t0),
         probe=not args.no_placement_probe, ref_of=(lambda t: t[0]) if mode == Mode.Overall else None)
@@ -765,27 +868,41 @@ def _main(args):
 
     # Reference frame of the rank's first frame ('overall': broadcast once per
     # job, the reference is fixed; 'per-frame': the halo frame, exchanged
-    # every step by dips_amd.shard.per_frame_overlapped).
+    # every step -- inside dips_diff_series_sharded on the native path, by
+    # dips_amd.shard.per_frame_overlapped on the torch path).
     if mode == Mode.Overall:
-        if rank == 0:
-            ref.copy_(frames[0])
-        shard.broadcast_reference(ref, src=0)
-    gather = shard.SeriesGather(world * F, dev)
-
-    def compute(fr, r, out):
-        if corrupt_halo and rank == 1 and r is ref:
-            r.view(-1)[12345] ^= 0x5A  # the received halo frame, damaged on purpose
-        op.run_device(fr, out, ref=r)
-
-    def step():
-        if mode == Mode.Overall:
-            compute(frames, ref, series)
-        elif world == 1:
-            compute(frames, None, series)
+        if comm is not None:
+            op.shard_broadcast_device(comm, frames[0] if rank == 0 else None, ref)
+            torch.cuda.synchronize()
         else:
-            # the halo transfer overlaps the compute of frames 1..F-1
-            shard.per_frame_overlapped(frames, ref, series, compute)
-        return gather(series)
+            if rank == 0:
+                ref.copy_(frames[0])
+            shard.broadcast_reference(ref, src=0)
+    if comm is not None:
+        gathered = torch.zeros((world * F, 4), dtype=torch.int64, device=dev) if rank == 0 else None
+
+        def step():
+            # halo send/recv beside the series launch, one ncclGather
+            op.run_sharded(comm, frames, world * F, series, gathered,
+                           ref=ref if mode == Mode.Overall else None, ref_resident=mode == Mode.Overall)
+            return gathered
+    else:
+        gather = shard.SeriesGather(world * F, dev)
+
+        def compute(fr, r, out):
+            if corrupt_halo and rank == 1 and r is ref:
+                r.view(-1)[12345] ^= 0x5A  # the received halo frame, damaged on purpose
+            op.run_device(fr, out, ref=r)
+
+        def step():
+            if mode == Mode.Overall:
+                compute(frames, ref, series)
+            elif world == 1:
+                compute(frames, None, series)
+            else:
+                # the halo transfer overlaps the compute of frames 1..F-1
+                shard.per_frame_overlapped(frames, ref, series, compute)
+            return gather(series)
 
     smp = _power_sampler(torch, local) if rank == 0 else None
     final = None
@@ -838,6 +955,11 @@ def _main(args):
     # received, rank 0 re-derives the gathered rows at every shard boundary
     # and 8 random frames (dips_amd.shard.verify_sharded_series)
     check = None
+    if comm is not None and mode == Mode.PerFrame and world > 1:
+        # what the library compared this rank's first frame with: the halo it
+        # received (rank > 0), for the self-check below
+        op.shard_reference_device(ref)
+        torch.cuda.synchronize()
     if not args.no_check:
         check = shard.verify_sharded_series(op, width=W, height=H, seed=SEED, n_total=world * F,
                                             per_frame=(mode == Mode.PerFrame), local_series=series, ref=ref,
@@ -891,7 +1013,7 @@ def _main(args):
         if not args.no_tau0:
             try:
                 tau0 = _tau0_leg(torch, smp, DiffSeriesOperator, frames, series, mode == Mode.PerFrame, args.tau,
-                                 max(3, args.steps))
+                                 max(3, args.steps), device=local)
                 log(f"tau0: frac {tau0['frac']}, power {tau0['power']}")
             except Exception as e:  # report, never hide
                 tau0 = {"skipped": str(e)}
@@ -938,7 +1060,7 @@ def _main(args):
                     raise ValueError("fewer than 2 frames per GPU at this size")
                 legs[key] = _config_leg(torch, dist, buf, name=name, W=lw, H=lh, F=lf, mode=Mode.Overall,
                                         tau=args.tau, steps=args.leg_steps, world=world, rank=rank, local=local,
-                                        dev=dev, check=not args.no_check,
+                                        dev=dev, check=not args.no_check, comm=comm,
                                         dump=(os.path.splitext(args.dump_series)[0] + f"_{key}.npy"
                                               if args.dump_series else None))
                 log(f"{key}: {legs[key]['frames_per_s']} frames/s, frac {legs[key]['frac']}, "
@@ -983,11 +1105,16 @@ def _main(args):
                 "workload": f"{W}x{H} RGB8, {F} frames per GPU, '{args.mode}' mode, tau={args.tau:.6g} "
                             f"(BASELINE.json configs[{2 if mode == Mode.PerFrame else 3}] per-GPU slice)",
                 "frames_per_gpu": F, "width": W, "height": H, "mode": args.mode,
-                "parallelism": f"frame-range x{world}" + ((" + RCCL halo send/recv + gather" if backend == "nccl"
-                                                             else f" + {backend} halo send/recv + gather "
-                                                                  "(rehearsal, ranks share one GPU)")
-                                                            if world > 1 else ""),
+                "parallelism": f"frame-range x{world}" + (
+                    ((" native dips_diff_series_sharded: RCCL halo ncclSend/ncclRecv beside the series launch "
+                      "+ one ncclGather" if backend == "nccl" else
+                      f" native dips_diff_series_sharded over the {backend} host transport (rehearsal, ranks "
+                      "share one GPU)") if shard_path == "native" else
+                     (" + RCCL halo send/recv + gather (torch protocol, dips_amd.shard)" if backend == "nccl"
+                      else f" + {backend} halo send/recv + gather (torch protocol; rehearsal, ranks share one "
+                           "GPU)")) if world > 1 else ""),
             },
+            "shard_path": ({"path": shard_path, **(comm_note or {})} if world > 1 else None),
             "ranks": world,
             "devices": devices,
             "placement": placements,
@@ -1003,6 +1130,10 @@ def _main(args):
                 "kernel_ms": round(kernel_ms, 4),
                 "kernel_ms_median": round(float(np.median(each)), 4) if world == 1 and each else None,
                 "kernel_launches_timed": len(each),
+                # what a plain caller gets: the batch's first allocation
+                # (tools/placement.py candidate 0, the median of its probe
+                # launches), beside the headline's kept placement
+                **_plain_allocation(placement, algo_bytes, kernel_ms),
                 "read_ceiling": {
                     "achieved": round(F * fb / (read_ms / 1e3) / 1e9, 1),
                     "unit": "GB/s",
@@ -1037,6 +1168,8 @@ def _main(args):
         print(json.dumps(out), flush=True)
     if op is not None:
         op.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
     if not ok:

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdips_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "dips_hip.h")
 
-ABI_VERSION = 2  # DIPS_ABI_VERSION of include/dips_hip.h
+ABI_VERSION = 3  # DIPS_ABI_VERSION of include/dips_hip.h
 
 DIPS_OK = 0
 DIPS_ERR_INVALID = -1
@@ -26,6 +26,7 @@ DIPS_ERR_NOMEM = -4
 DIPS_ERR_CAPACITY = -5
 DIPS_ERR_NODEVICE = -6
 DIPS_ERR_INTERNAL = -7
+DIPS_ERR_COMM = -8
 
 FLAG_DEVICE_PTRS = 0x1
 FLAG_TIME_KERNEL = 0x2
@@ -39,6 +40,12 @@ FMT_RGB8 = 3
 FMT_RGBA8 = 4
 MODE_OVERALL = 0
 MODE_PER_FRAME = 1
+
+COMM_ID_BYTES = 128
+COMM_RCCL = 1
+COMM_LOOPBACK = 2
+COMM_HOST = 3
+SHARD_REF_RESIDENT = 0x1
 
 
 class DipsLibraryError(RuntimeError):
@@ -83,6 +90,22 @@ class SeriesEntry(ctypes.Structure):
         ("sj", ctypes.c_uint64),
         ("count", ctypes.c_uint64),
         ("si_fixed", ctypes.c_uint64),
+    ]
+
+
+# dips_comm_ops: the caller's transport of DIPS_COMM_HOST (host buffers)
+COMM_BROADCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
+COMM_SENDRECV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_int, ctypes.c_size_t)
+COMM_GATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                  ctypes.c_int)
+
+
+class DipsCommOps(ctypes.Structure):
+    _fields_ = [
+        ("broadcast", COMM_BROADCAST_FN),
+        ("sendrecv", COMM_SENDRECV_FN),
+        ("gather", COMM_GATHER_FN),
     ]
 
 
@@ -163,6 +186,18 @@ def load() -> ctypes.CDLL:
             "dips_read_ceiling": ([_vp, _u8p, u64, P(ctypes.c_double)], st),
             "dips_read_ceiling_walk": ([_vp, _u8p, u32, u32, u32, P(ctypes.c_double)], st),
             "dips_series_geometry": ([_vp, u32, u32, u32, P(u64), P(u64), P(u64)], st),
+            "dips_comm_unique_id": ([_vp], st),
+            "dips_comm_create": ([_vp, st, st, st, P(_vp)], st),
+            "dips_comm_create_loopback": ([st, st, _vp], st),
+            "dips_comm_create_host": ([P(DipsCommOps), _vp, st, st, st, P(_vp)], st),
+            "dips_comm_destroy": ([_vp], None),
+            "dips_comm_last_error": ([_vp], ctypes.c_char_p),
+            "dips_comm_info": ([_vp, P(st), P(st), P(st)], st),
+            "dips_shard_range": ([u64, st, st, P(u64), P(u32)], st),
+            "dips_shard_broadcast": ([_vp, _vp, u32, u32, _u8p, _u8p], st),
+            "dips_diff_series_sharded": ([_vp, _vp, u32, u32, _u8p, u32, u64, _u8p, u32, _vp, _vp], st),
+            "dips_shard_plan": ([_vp, _vp, u32, u32, u64, P(u64), P(u32), P(u64), P(u64)], st),
+            "dips_shard_reference": ([_vp, _u8p, ctypes.c_size_t], st),
             "dips_alt_params_default": ([P(DipsAltParams)], st),
             "dips_alt_create": ([P(DipsAltParams), u32, u32, st, P(_vp)], st),
             "dips_alt_destroy": ([_vp], None),
@@ -194,6 +229,15 @@ def check(status: int, handle=None) -> int:
     if status < 0:
         lib = load()
         msg = lib.dips_last_error(handle)
+        raise DipsError(status, msg.decode() if msg else "")
+    return status
+
+
+def check_comm(status: int, comm=None) -> int:
+    """A communicator call's status (message from dips_comm_last_error)."""
+    if status < 0:
+        lib = load()
+        msg = lib.dips_comm_last_error(comm)
         raise DipsError(status, msg.decode() if msg else "")
     return status
 

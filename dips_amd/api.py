@@ -499,6 +499,81 @@ class DiffSeriesOperator:
                 ref.data_ptr() if ref is not None else None, series_out.data_ptr(),
                 map_out.data_ptr() if map_out is not None else None))
 
+    # -- frame-range sharding (native: shard_abi.hip) -------------------------
+    def run_sharded(self, comm, frames, n_total: int, series_local, series_all=None, ref=None,
+                    ref_resident: bool = False, stream=None) -> None:
+        """dips_diff_series_sharded on device tensors, asynchronous on the
+        tensor's current stream: this rank's frames [n_local, H, W(, C)]
+        (its dips_shard_range of n_total), series_local int64 [n_local, 4],
+        series_all int64 [n_total, 4] on rank 0 (ignored elsewhere); `ref`:
+        'overall' rank 0's reference (None = its first frame) or, with
+        ref_resident, every rank's copy; 'per-frame' rank 0's predecessor of
+        global frame 0 (None = frame 0)."""
+        n, h, w = _frame_geometry(frames, self.fmt)
+        if tuple(series_local.shape) != (n, 4) or series_local.element_size() != 8:
+            raise ValueError("series_local must be an 8-byte tensor of shape [n_local, 4]")
+        if comm.rank == 0 and (series_all is None or tuple(series_all.shape) != (int(n_total), 4)
+                               or series_all.element_size() != 8):
+            raise ValueError("rank 0 needs series_all, an 8-byte tensor of shape [n_total, 4]")
+        for t in (frames, series_local, series_all, ref):
+            if t is not None and (not t.is_cuda or not t.is_contiguous()):
+                raise ValueError("device path needs contiguous HIP tensors")
+        if ref is not None and ref.numel() != h * w * int(self.fmt):
+            raise ValueError("ref must have the size of one frame")
+        lib = self._dev._lib
+        with _stream_of(self._dev, frames, stream):
+            self._dev.check(lib.dips_diff_series_sharded(
+                self._dev.ptr, comm.ptr, w, h, frames.data_ptr(), n, int(n_total),
+                ref.data_ptr() if ref is not None else None,
+                _lib.SHARD_REF_RESIDENT if ref_resident else 0, series_local.data_ptr(),
+                series_all.data_ptr() if (series_all is not None and comm.rank == 0) else None))
+
+    def sharded(self, comm, frames: np.ndarray, n_total: int, ref: Optional[np.ndarray] = None,
+                ref_resident: bool = False) -> Tuple[Series, Optional[Series]]:
+        """The same on host arrays (staged through HBM, synchronous):
+        returns (this rank's series, the gathered series on rank 0 / None)."""
+        frames = _as_u8(frames)
+        n, h, w = _frame_geometry(frames, self.fmt)
+        local = np.zeros((n, 4), dtype=np.uint64)
+        full = np.zeros((int(n_total), 4), dtype=np.uint64) if comm.rank == 0 else None
+        rp = None
+        if ref is not None:
+            ref = _as_u8(ref)
+            if ref.size != h * w * int(self.fmt):
+                raise ValueError("ref must have the shape of one frame")
+            rp = ref.ctypes.data
+        self._host.check(self._host._lib.dips_diff_series_sharded(
+            self._host.ptr, comm.ptr, w, h, frames.ctypes.data, n, int(n_total), rp,
+            _lib.SHARD_REF_RESIDENT if ref_resident else 0, local.ctypes.data,
+            full.ctypes.data if full is not None else None))
+        return Series.from_array(local), (Series.from_array(full) if full is not None else None)
+
+    def shard_broadcast_device(self, comm, frame, out, stream=None) -> None:
+        """Rank 0's `frame` into `out` on every rank (dips_shard_broadcast)."""
+        h, w = int(out.shape[0]), int(out.shape[1])
+        lib = self._dev._lib
+        with _stream_of(self._dev, out, stream):
+            self._dev.check(lib.dips_shard_broadcast(self._dev.ptr, comm.ptr, w, h,
+                                                     frame.data_ptr() if frame is not None else None,
+                                                     out.data_ptr()))
+
+    def shard_plan(self, comm, width: int, height: int, n_total: int) -> dict:
+        """dips_shard_plan: this rank's frame range and the waves of its
+        series launch beside the halo transfer (and uncapped)."""
+        first, count = ctypes.c_uint64(), ctypes.c_uint32()
+        waves, unc = ctypes.c_uint64(), ctypes.c_uint64()
+        self._dev.check(self._dev._lib.dips_shard_plan(self._dev.ptr, comm.ptr, width, height, int(n_total),
+                                                       ctypes.byref(first), ctypes.byref(count),
+                                                       ctypes.byref(waves), ctypes.byref(unc)))
+        return {"first": first.value, "count": count.value, "waves": waves.value, "waves_uncapped": unc.value}
+
+    def shard_reference_device(self, out, stream=None) -> bool:
+        """The reference the last run_sharded used for this rank's first
+        frame, into a uint8 device tensor; False before any sharded call."""
+        with _stream_of(self._dev, out, stream):
+            return self._dev.check(self._dev._lib.dips_shard_reference(self._dev.ptr, out.data_ptr(),
+                                                                       out.numel())) == 1
+
     def synth_device(self, dst, width: int, height: int, seed: int, t0: int, stream=None) -> None:
         """Fill a uint8 device tensor [N, H, W(, C)] with synthetic frames t0..t0+N-1."""
         n = dst.shape[0]

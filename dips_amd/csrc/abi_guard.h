@@ -26,6 +26,7 @@
 
 struct dips_handle;
 struct dips_alt_handle;
+struct dips_comm;
 
 namespace dips_abi {
 
@@ -35,13 +36,17 @@ namespace dips_abi {
 // throw (a failed string assignment leaves the old message).
 struct CreateTag {};
 struct AltCreateTag {};
+struct CommCreateTag {};
 void note_error(dips_handle* h, const char* msg) noexcept;
 void note_error(dips_alt_handle* h, const char* msg) noexcept;
+void note_error(dips_comm* c, const char* msg) noexcept;
 void note_error(CreateTag, const char* msg) noexcept;
 void note_error(AltCreateTag, const char* msg) noexcept;
+void note_error(CommCreateTag, const char* msg) noexcept;
 // read-only handles and handle-free functions have nowhere to write
 inline void note_error(const dips_handle*, const char*) noexcept {}
 inline void note_error(const dips_alt_handle*, const char*) noexcept {}
+inline void note_error(const dips_comm*, const char*) noexcept {}
 inline void note_error(std::nullptr_t, const char*) noexcept {}
 
 // The value a function of return type R gives for a caught exception.

@@ -636,8 +636,11 @@ void dips_alt_destroy(dips_alt_handle* h) {
 const char* dips_alt_last_error(const dips_alt_handle* h) {
     return guard(h, [&]() -> const char* {
         if (h) return h->err.c_str();
+        // this thread's copy (see dips_last_error)
+        thread_local std::string copy;
         std::lock_guard<std::mutex> lk(g_alt_err_mu);
-        return g_alt_create_err.c_str();
+        copy = g_alt_create_err;
+        return copy.c_str();
     });
 }
 

@@ -189,6 +189,7 @@ void dips_destroy(dips_handle* h) {
         (void)hipSetDevice(h->device);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
         if (h->copy_stream) (void)hipStreamSynchronize(h->copy_stream);
+        if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream);
         for (auto& pr : h->ev_pending) {
             (void)hipEventDestroy(pr.first);
             (void)hipEventDestroy(pr.second);
@@ -221,6 +222,13 @@ void dips_destroy(dips_handle* h) {
         h->start.release();
         h->out.release();
         h->io.release();
+        h->shard_ref.release();
+        h->shard_halo.release();
+        h->shard_send.release();
+        h->shard_recv.release();
+        if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
+        if (h->shard_ev_in) (void)hipEventDestroy(h->shard_ev_in);
+        if (h->shard_ev_halo) (void)hipEventDestroy(h->shard_ev_halo);
         if (h->switch_ev) (void)hipEventDestroy(h->switch_ev);
         if (h->join_ev) (void)hipEventDestroy(h->join_ev);
         if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -232,8 +240,12 @@ void dips_destroy(dips_handle* h) {
 const char* dips_last_error(const dips_handle* h) {
     return guard(h, [&]() -> const char* {
         if (h) return h->err.c_str();
+        // this thread's copy: a failed dips_create on another thread may
+        // replace the record while the caller still reads the message
+        thread_local std::string copy;
         std::lock_guard<std::mutex> lk(g_err_mu);
-        return g_create_err.c_str();
+        copy = g_create_err;
+        return copy.c_str();
     });
 }
 

@@ -103,6 +103,15 @@ struct dips_handle {
     uint32_t cb_lut_filter = 0, cb_lut_col = 0;
     float cb_lut_k = 0.0f;
 
+    // frame-range sharding (shard_abi.hip): the broadcast reference, the
+    // received halo frame, the padded send / gather buffers of the series,
+    // the stream the halo exchange runs on beside the series launch
+    dips_host::DevBuf shard_ref, shard_halo, shard_send, shard_recv;
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t shard_ev_in = nullptr, shard_ev_halo = nullptr;
+    const uint8_t* shard_last_ref = nullptr;  // the reference of the last sharded call's first frame
+    uint64_t shard_last_bytes = 0;
+
     bool crosscheck() const { return (p.flags & DIPS_FLAG_CROSSCHECK) != 0; }
 };
 
@@ -118,6 +127,13 @@ hipEvent_t take_event(dips_handle* h);
 int occupancy_blocks(dips_handle* h, const void* kernel);
 // a deferred frame's speculative kernels finished (compat_abi.hip)
 dips_status flush_pending(dips_handle* h);
+// the series of device frames, asynchronously on `s` (series_abi.hip);
+// `reserve` leaves one wave slot per SIMD free beside the launch
+dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
+                              uint32_t n_frames, const uint8_t* ref0, dips_series_entry* series, uint8_t* map,
+                              hipStream_t s, bool reserve = false);
+// waves of that launch for an aligned batch of this shape (0: not eligible)
+uint64_t series_waves(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool reserve);
 
 }  // namespace dips_internal
 

@@ -11,6 +11,13 @@
 //            [--chroma none|red|green|blue] [--batch N]
 //   dips_raw series IN.raw W H rgb8|rgba8|gray8 [--mode overall|per-frame]
 //            [--tau T] [--chunk N]        -> CSV frame,sad,sj,count,si
+//   dips_raw sharded IN.raw W H rgb8|rgba8|gray8 --ranks N [--mode ...]
+//            [--tau T]                    -> the same CSV, computed by N
+//            ranks (one thread and one handle each) over a loopback
+//            communicator with dips_diff_series_sharded: each rank hands its
+//            frame range of the file to the library, rank 0 prints the
+//            gathered series (the frame-range sharding a multi-GPU host
+//            drives the same way over dips_comm_create's RCCL)
 //
 // Input files are memory-mapped and handed over as host pointers: the
 // library stages them through pinned memory and overlaps the PCIe transfers
@@ -27,6 +34,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dips_hip.h"
@@ -61,7 +69,9 @@ int usage() {
                  "usage: dips_raw callback IN.rgba W H OUT.rgba [--colorize] [--window N] [--sensitivity K]\n"
                  "                [--filter sigmoid|inverse|none] [--chroma none|red|green|blue] [--batch N]\n"
                  "       dips_raw series IN.raw W H rgb8|rgba8|gray8 [--mode overall|per-frame] [--tau T]\n"
-                 "                [--chunk N]\n");
+                 "                [--chunk N]\n"
+                 "       dips_raw sharded IN.raw W H rgb8|rgba8|gray8 --ranks N [--mode overall|per-frame]\n"
+                 "                [--tau T]\n");
     return 1;
 }
 
@@ -156,6 +166,99 @@ int run_callback(int argc, char** argv) {
     return rc;
 }
 
+void print_series(const dips_series_entry* series, uint64_t n) {
+    std::printf("frame,sad,sj,count,si\n");
+    for (uint64_t t = 0; t < n; ++t)
+        std::printf("%llu,%llu,%llu,%llu,%.17g\n", (unsigned long long)t, (unsigned long long)series[t].sad,
+                    (unsigned long long)series[t].sj, (unsigned long long)series[t].count,
+                    dips_series_si(&series[t]));
+}
+
+int run_sharded(int argc, char** argv) {
+    if (argc < 6) return usage();
+    uint32_t w = 0, h = 0, ranks = 0;
+    if (!parse_u32(argv[3], &w) || !parse_u32(argv[4], &h)) return usage();
+    dips_params p;
+    dips_params_default(&p);
+    const std::string fmt = argv[5];
+    p.format = fmt == "rgb8" ? DIPS_FMT_RGB8 : fmt == "rgba8" ? DIPS_FMT_RGBA8 : fmt == "gray8" ? DIPS_FMT_GRAY8 : 0u;
+    if (!p.format) return usage();
+    for (int i = 6; i < argc; ++i) {
+        const std::string a = argv[i];
+        const bool has = i + 1 < argc;
+        if (a == "--mode" && has) {
+            const std::string m = argv[++i];
+            if (m != "overall" && m != "per-frame") return usage();
+            p.mode = m == "overall" ? DIPS_MODE_OVERALL : DIPS_MODE_PER_FRAME;
+        } else if (a == "--tau" && has) {
+            p.tau = std::strtof(argv[++i], nullptr);
+        } else if (a == "--ranks" && has) {
+            if (!parse_u32(argv[++i], &ranks) || ranks > 64) return usage();
+        } else {
+            return usage();
+        }
+    }
+    if (ranks == 0) return usage();
+    Mapped in;
+    if (!in.open(argv[2])) {
+        std::fprintf(stderr, "dips_raw: cannot map %s\n", argv[2]);
+        return 1;
+    }
+    const size_t fb = (size_t)w * h * p.format;
+    if (in.n % fb != 0) {
+        std::fprintf(stderr, "dips_raw: %s is not a whole number of %ux%u %s frames\n", argv[2], w, h, fmt.c_str());
+        return 1;
+    }
+    const uint64_t n_total = in.n / fb;
+    std::vector<dips_comm*> comms(ranks, nullptr);
+    int st = dips_comm_create_loopback((int)ranks, 0, comms.data());
+    if (st != DIPS_OK) {
+        std::fprintf(stderr, "dips_raw: dips_comm_create_loopback failed (%d): %s\n", st, dips_comm_last_error(nullptr));
+        return 2;
+    }
+    std::vector<dips_series_entry> all(n_total);
+    std::vector<int> rc(ranks, 0);
+    std::vector<std::string> why(ranks);
+    std::vector<std::thread> threads;
+    for (uint32_t r = 0; r < ranks; ++r) {
+        threads.emplace_back([&, r]() {
+            uint64_t first = 0;
+            uint32_t count = 0;
+            if (dips_shard_range(n_total, (int)ranks, (int)r, &first, &count) != DIPS_OK) {
+                rc[r] = 1;
+                why[r] = "bad shard range";
+                return;
+            }
+            dips_handle* hd = nullptr;
+            int s2 = dips_create(&p, 0, &hd);
+            if (s2 != DIPS_OK) {
+                rc[r] = s2;
+                why[r] = dips_last_error(nullptr);
+                return;
+            }
+            std::vector<dips_series_entry> local(count);
+            // host pointers: the rank's frames straight from the mapped file
+            s2 = dips_diff_series_sharded(hd, comms[r], w, h, in.p + first * fb, count, n_total, nullptr, 0,
+                                          local.data(), r == 0 ? all.data() : nullptr);
+            if (s2 != DIPS_OK) {
+                rc[r] = s2;
+                why[r] = dips_last_error(hd);
+            }
+            dips_destroy(hd);
+        });
+    }
+    for (auto& t : threads) t.join();
+    for (auto* c : comms) dips_comm_destroy(c);
+    for (uint32_t r = 0; r < ranks; ++r)
+        if (rc[r] != 0) {
+            std::fprintf(stderr, "dips_raw: rank %u: dips_diff_series_sharded failed (%d): %s\n", r, rc[r],
+                         why[r].c_str());
+            return 2;
+        }
+    print_series(all.data(), n_total);
+    return 0;
+}
+
 int run_series(int argc, char** argv) {
     if (argc < 6) return usage();
     uint32_t w = 0, h = 0, chunk = 0;
@@ -201,11 +304,7 @@ int run_series(int argc, char** argv) {
         dips_destroy(hd);
         return rc;
     }
-    std::printf("frame,sad,sj,count,si\n");
-    for (uint32_t t = 0; t < n; ++t)
-        std::printf("%u,%llu,%llu,%llu,%.17g\n", t, (unsigned long long)series[t].sad,
-                    (unsigned long long)series[t].sj, (unsigned long long)series[t].count,
-                    dips_series_si(&series[t]));
+    print_series(series.data(), n);
     dips_destroy(hd);
     return 0;
 }
@@ -217,5 +316,6 @@ int main(int argc, char** argv) {
     const std::string cmd = argv[1];
     if (cmd == "callback") return run_callback(argc, argv);
     if (cmd == "series") return run_series(argc, argv);
+    if (cmd == "sharded") return run_sharded(argc, argv);
     return usage();
 }

@@ -27,17 +27,20 @@ struct FastGeom {
     uint32_t part_frames = 0;  // part-major schedule: frames per part (0: contiguous ranges)
 };
 
-// Resident waves per SIMD for a kernel of `occupancy` waves per SIMD,
-// capped by DIPS_SERIES_WAVES_PER_SIMD (bench.py sets 4 at N > 1 so that
-// RCCL's halo kernels find a free slot beside the persistent grid instead of
-// delaying part of it; 3-5 waves per SIMD run at the same speed,
-// profiles/r01_wave_count_probe.txt).
-uint64_t waves_per_simd(uint64_t occupancy) {
+// Resident waves per SIMD for a kernel of `occupancy` waves per SIMD:
+// `reserve` leaves one slot per SIMD free (occupancy - 1) -- the sharded
+// 'per-frame' launch that runs while the transport's halo kernels are in
+// flight (shard_abi.hip), so that they start beside the persistent grid
+// instead of after it; DIPS_SERIES_WAVES_PER_SIMD caps every launch below
+// that (a deployment knob).
+uint64_t waves_per_simd(uint64_t occupancy, bool reserve) {
+    uint64_t w = occupancy;
+    if (reserve && w > 1) w -= 1;
     if (const char* cap = std::getenv("DIPS_SERIES_WAVES_PER_SIMD")) {
         const unsigned long c = std::strtoul(cap, nullptr, 10);
-        if (c >= 1 && c < occupancy) return c;
+        if (c >= 1 && c < w) w = c;
     }
-    return occupancy;
+    return w;
 }
 
 // The part-major schedule of the series kernels (series_v2.hip,
@@ -85,7 +88,7 @@ void part_geometry(FastGeom& g, uint64_t n_frames, uint64_t resident) {
 }
 
 FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, int C, bool pf,
-                       bool map, bool align = false, int isi = 0) {
+                       bool map, bool align = false, int isi = 0, bool reserve = false) {
     FastGeom g;
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t fb = npx * (uint64_t)C;
@@ -103,7 +106,7 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
     g.items = g.n_tiles * n_frames;
     const void* k = dips::series_fast_kernel_ptr(C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map, align, isi);
     if (!k) return g;
-    const uint64_t resident = waves_per_simd((uint64_t)occupancy_blocks(h, k)) * (uint64_t)h->cu_count * 4u;
+    const uint64_t resident = waves_per_simd((uint64_t)occupancy_blocks(h, k), reserve) * (uint64_t)h->cu_count * 4u;
     g.n_waves = g.items < resident ? g.items : resident;
     g.blocks = (g.n_waves + 3) / 4;
     if (C == 3 || C == 4) part_geometry(g, n_frames, resident);
@@ -132,7 +135,7 @@ constexpr int kGrayLayout = 4;
 
 bool gray_lut_enabled(const dips_handle* h) { return !h->crosscheck(); }
 
-FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames) {
+FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool reserve = false) {
     FastGeom g;
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t nvec = npx / 16u;
@@ -144,7 +147,7 @@ FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint
     g.n_tiles = (nvec + 64 * U - 1) / (64 * U);
     g.items = g.n_tiles * n_frames;
     // one group per CU (the tables fill its LDS): 4 waves per SIMD
-    const uint64_t resident = waves_per_simd(gw / 4u) * 4u * (uint64_t)h->cu_count;
+    const uint64_t resident = waves_per_simd(gw / 4u, reserve) * 4u * (uint64_t)h->cu_count;
     g.n_waves = g.items < resident ? g.items : resident;
     // 'per-frame' batches: the part-major schedule, as for RGB8 (part_geometry)
     if (h->p.mode == DIPS_MODE_PER_FRAME) part_geometry(g, n_frames, resident);
@@ -172,10 +175,15 @@ int series_isi_form(const dips_handle* h) {
     return 1;
 }
 
-// Run the series on device pointers, asynchronously on `s`.
+}  // namespace
+
+namespace dips_internal {
+
+// Run the series on device pointers, asynchronously on `s` (`reserve`: see
+// waves_per_simd).
 dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
                               uint32_t n_frames, const uint8_t* ref0, dips_series_entry* series, uint8_t* map,
-                              hipStream_t s) {
+                              hipStream_t s, bool reserve) {
     const int C = (int)h->p.format;
     const bool pf = h->p.mode == DIPS_MODE_PER_FRAME;
     const uint64_t npx = (uint64_t)width * height;
@@ -188,8 +196,8 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     const bool align = (C == 3 || C == 4) && ((((uintptr_t)frames | (uintptr_t)fb | (uintptr_t)ref0) & 3u) != 0u);
     const int isi = series_isi_form(h);
     if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC))
-        g = glut ? gray_lut_geometry(h, width, height, n_frames)
-                 : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr, align, isi);
+        g = glut ? gray_lut_geometry(h, width, height, n_frames, reserve)
+                 : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr, align, isi, reserve);
     // the series starts at zero: the table and RGB(A) kernels clear it
     // themselves (SeriesArgs::zero), saving a fill launch; the others after a
     // fill
@@ -219,6 +227,20 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     const bool timing = (h->p.flags & DIPS_FLAG_TIME_KERNEL) != 0;
     dips_status st = DIPS_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    // the timing events go back to the free list on every early return; they
+    // join ev_pending only once both are recorded
+    struct EventReturn {
+        dips_handle* h;
+        hipEvent_t* e0;
+        hipEvent_t* e1;
+        ~EventReturn() {
+            try {
+                if (*e0) h->ev_free.push_back(*e0);
+                if (*e1) h->ev_free.push_back(*e1);
+            } catch (...) {
+            }
+        }
+    } ev_return{h, &e0, &e1};
     if (timing) {
         e0 = take_event(h);
         e1 = take_event(h);
@@ -278,12 +300,28 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     if (timing) {
         DIPS_HIP(h, hipEventRecord(e1, s));
         h->ev_pending.emplace_back(e0, e1);
+        e0 = e1 = nullptr;
     }
     if (g.ok)
         DIPS_HIP(h, dips::launch_series_reduce(h->partials.as<uint64_t>(), n_frames, (uint32_t)g.n_tiles,
                                                C == 1 ? (glut ? 2 : 1) : 0, series, s));
     return DIPS_OK;
 }
+
+// Waves of the series launch an aligned batch of this shape runs (0 if the
+// shape is not eligible for the fast kernels).
+uint64_t series_waves(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool reserve) {
+    const int C = (int)h->p.format;
+    FastGeom g = C == 1 && gray_lut_enabled(h)
+                     ? gray_lut_geometry(h, width, height, n_frames, reserve)
+                     : fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false, false,
+                                     series_isi_form(h), reserve);
+    return g.ok ? g.n_waves : 0;
+}
+
+}  // namespace dips_internal
+
+namespace {
 
 // One timed launch of a read-only leg on the handle's stream: *ms = its
 // hipEvent duration (synchronous).

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define DIPS_ABI_VERSION 2
+#define DIPS_ABI_VERSION 3
 
 typedef enum dips_status {
     DIPS_OK = 0,
@@ -34,9 +34,12 @@ typedef enum dips_status {
     DIPS_ERR_NOMEM = -4,    /* device or host allocation failed */
     DIPS_ERR_CAPACITY = -5, /* caller's output buffer too small */
     DIPS_ERR_NODEVICE = -6, /* no HIP device / device index out of range */
-    DIPS_ERR_INTERNAL = -7  /* a C++ exception inside the library, caught at the
+    DIPS_ERR_INTERNAL = -7, /* a C++ exception inside the library, caught at the
                                boundary (see dips_last_error); the handle may
                                be left mid-call and should be destroyed */
+    DIPS_ERR_COMM = -8      /* a communicator's transport failed (RCCL error,
+                               a loopback rank that never arrived, a host
+                               transport callback's non-zero return) */
 } dips_status;
 
 /* DiPsFilter -> override id 3 (dips/src/lib.rs:25-41, dips_shader.wgsl:20). */
@@ -302,6 +305,134 @@ dips_status dips_read_ceiling_walk(dips_handle *h, const uint8_t *dev_frames, ui
 
 /* Library ABI version (DIPS_ABI_VERSION). */
 int dips_abi_version(void);
+
+/* ------------------------------------------------------------------------
+ * Frame-range sharding of the difference series over one rank per GPU
+ * (BASELINE.json north_star: "sharded by frame-range across
+ * the 8 GPUs of one node with a single RCCL gather").  The reference is
+ * single-device -- one wgpu adapter and queue (dips/src/gpu/mod.rs:66-98,
+ * chosen at :71-78) driving frames strictly in order -- so these entry
+ * points have no reference counterpart; they let a Rust (or C) host that
+ * replaces dips/src/gpu/mod.rs:39-398 with this library use every GPU of a
+ * node without any other runtime.
+ *
+ * Rank r of G owns the contiguous global frames [r*N/G, (r+1)*N/G)
+ * (dips_shard_range).  The exchanges are:
+ *   'overall':   the reference frame, broadcast from rank 0;
+ *   'per-frame': the halo frame r*N/G - 1, sent by rank r-1 to rank r,
+ *                overlapped with the series launch over the rank's own frames
+ *                1..n-1 (which need no halo);
+ *   both:        the per-frame series entries (32 B each), reassembled on
+ *                rank 0 by ONE gather (ncclGather, rccl.h:745).
+ * No collective touches the frame batch itself.
+ *
+ * A communicator is one of three transports behind one internal table:
+ *   DIPS_COMM_RCCL      RCCL over xGMI (librccl), one process per GPU;
+ *   DIPS_COMM_LOOPBACK  ranks as threads of one process on one device,
+ *                       stream-ordered hipMemcpyAsync + events (tests, and a
+ *                       host that shards one GPU between decoders);
+ *   DIPS_COMM_HOST      the caller's own transport (MPI, a torch process
+ *                       group, ...) through host-memory callbacks,
+ *                       synchronous.
+ * Collective contract (as RCCL's): every rank makes the same sequence of
+ * sharded calls with the same n_total, mode and shard_flags; an argument
+ * error one rank alone detects returns on that rank before any collective
+ * and leaves the others waiting in theirs.
+ * ------------------------------------------------------------------------ */
+typedef struct dips_comm dips_comm;
+
+#define DIPS_COMM_ID_BYTES 128u /* NCCL_UNIQUE_ID_BYTES (rccl.h:40) */
+#define DIPS_COMM_RCCL 1
+#define DIPS_COMM_LOOPBACK 2
+#define DIPS_COMM_HOST 3
+
+/* Caller-supplied transport of DIPS_COMM_HOST: every buffer is HOST memory
+ * owned by the library for the call; each function returns 0 on success and
+ * any other value on failure.  broadcast: `bytes` from rank `root` into
+ * `buf` on every rank (in place).  sendrecv: send `bytes` of `send` to rank
+ * `to` and receive `bytes` from rank `from` into `recv`, concurrently (either
+ * side < 0: none).  gather: `bytes` of `send` from every rank into `recv` at
+ * offset rank*bytes on rank `root` (`recv` NULL elsewhere). */
+typedef struct dips_comm_ops {
+    int (*broadcast)(void *ctx, void *buf, size_t bytes, int root);
+    int (*sendrecv)(void *ctx, const void *send, int to, void *recv, int from, size_t bytes);
+    int (*gather)(void *ctx, const void *send, void *recv, size_t bytes, int root);
+} dips_comm_ops;
+
+/* A new RCCL unique id (ncclGetUniqueId) into id[DIPS_COMM_ID_BYTES]; rank 0
+ * makes it and the caller hands it to every rank out of band. */
+dips_status dips_comm_unique_id(uint8_t *id);
+
+/* Join the RCCL communicator `id` as `rank` of `nranks` on HIP device
+ * `device` (ncclCommInitRank; blocks until every rank has joined). */
+dips_status dips_comm_create(const uint8_t *id, int nranks, int rank, int device, dips_comm **out);
+
+/* `nranks` loopback communicators on `device`, comms[r] = rank r; each must
+ * be driven by its own thread (the collectives meet on the host). */
+dips_status dips_comm_create_loopback(int nranks, int device, dips_comm **comms);
+
+/* A communicator over the caller's transport `ops` (context `ctx`). */
+dips_status dips_comm_create_host(const dips_comm_ops *ops, void *ctx, int nranks, int rank, int device,
+                                  dips_comm **out);
+
+/* Leave and free a communicator (ncclCommDestroy for RCCL). */
+void dips_comm_destroy(dips_comm *comm);
+
+/* Last error message of `comm` (or of the last failed creation if NULL). */
+const char *dips_comm_last_error(const dips_comm *comm);
+
+/* Transport (DIPS_COMM_*), size and rank of `comm`. */
+dips_status dips_comm_info(const dips_comm *comm, int *kind, int *nranks, int *rank);
+
+/* The frame range of `rank` of `nranks` over `n_total` frames: global
+ * frames [*first, *first + *count), balanced to within one frame. */
+dips_status dips_shard_range(uint64_t n_total, int nranks, int rank, uint64_t *first, uint32_t *count);
+
+/* DIPS_SHARD_REF_RESIDENT: 'overall' mode, every rank passes in `ref`
+ * its own copy of the reference (e.g. from dips_shard_broadcast), so the
+ * call skips the broadcast. */
+#define DIPS_SHARD_REF_RESIDENT 0x1u
+
+/* Broadcast one frame (width*height*C bytes) from rank 0's `frame` into
+ * `out` on every rank (on rank 0 `out` may equal `frame`).  Device pointers
+ * with DIPS_FLAG_DEVICE_PTRS (asynchronous on the handle's stream), host
+ * pointers otherwise. */
+dips_status dips_shard_broadcast(dips_handle *h, dips_comm *comm, uint32_t width, uint32_t height,
+                                 const uint8_t *frame, uint8_t *out);
+
+/* The sharded series: this rank's `n_local` frames (its dips_shard_range of
+ * n_total; every rank needs >= 1 frame, so n_total >= nranks), the same
+ * semantics as one dips_diff_series over all n_total frames.
+ *   ref:          'overall': on rank 0 the reference (NULL = its frames[0]),
+ *                 broadcast to every rank; with DIPS_SHARD_REF_RESIDENT every
+ *                 rank's own copy.  'per-frame': on rank 0 the frame before
+ *                 global frame 0 (NULL = frame 0 itself); ignored elsewhere
+ *                 (the halo comes from rank r-1).
+ *   series_local: n_local entries, this rank's slice (required).
+ *   series_all:   rank 0: n_total entries, the gathered series (required;
+ *                 may begin at series_local); other ranks: ignored.
+ * With DIPS_FLAG_DEVICE_PTRS every pointer is a device pointer and the call
+ * is asynchronous on the handle's stream (RCCL / loopback); otherwise host
+ * pointers, staged through HBM, and the call returns with the results in
+ * host memory.  h's device must be the communicator's. */
+dips_status dips_diff_series_sharded(dips_handle *h, dips_comm *comm, uint32_t width, uint32_t height,
+                                     const uint8_t *frames, uint32_t n_local, uint64_t n_total,
+                                     const uint8_t *ref, uint32_t shard_flags, dips_series_entry *series_local,
+                                     dips_series_entry *series_all);
+
+/* The plan of that call on this rank, without running it: its frame range,
+ * the waves of the series launch over its frames 1..n-1 and of the same
+ * launch uncapped ('per-frame' at nranks > 1 leaves one wave slot per SIMD
+ * free for the transport's halo kernels; equal otherwise). */
+dips_status dips_shard_plan(dips_handle *h, const dips_comm *comm, uint32_t width, uint32_t height,
+                            uint64_t n_total, uint64_t *first, uint32_t *count, uint64_t *waves,
+                            uint64_t *waves_uncapped);
+
+/* Copy the reference the last sharded call used for this rank's first frame
+ * (the received halo, the broadcast reference, or rank 0's own) into `out`
+ * (width*height*C bytes; device pointer with DIPS_FLAG_DEVICE_PTRS).
+ * Returns 1 if copied, 0 before any sharded call. */
+int dips_shard_reference(dips_handle *h, uint8_t *out, size_t cap);
 
 /* ------------------------------------------------------------------------
  * dips_alt operator.  The dips_alt crate's GPU

@@ -19,8 +19,9 @@ pub const DIPS_ERR_NOMEM: DipsStatus = -4;
 pub const DIPS_ERR_CAPACITY: DipsStatus = -5;
 pub const DIPS_ERR_NODEVICE: DipsStatus = -6;
 pub const DIPS_ERR_INTERNAL: DipsStatus = -7;
+pub const DIPS_ERR_COMM: DipsStatus = -8;
 
-pub const DIPS_ABI_VERSION: c_int = 2;
+pub const DIPS_ABI_VERSION: c_int = 3;
 
 pub const DIPS_FILTER_SIGMOID: u32 = 0;
 pub const DIPS_FILTER_INVERSE_SIGMOID: u32 = 1;
@@ -41,6 +42,11 @@ pub const DIPS_FLAG_CROSSCHECK: u32 = 0x8;
 pub const DIPS_FLAG_GRAY_BAND_TABLE: u32 = 0x10;
 pub const DIPS_FLAG_GRAY_PAIR_TABLE: u32 = 0x20;
 pub const DIPS_CALLBACK_PHASES: u32 = 11;
+pub const DIPS_COMM_ID_BYTES: u32 = 128;
+pub const DIPS_COMM_RCCL: c_int = 1;
+pub const DIPS_COMM_LOOPBACK: c_int = 2;
+pub const DIPS_COMM_HOST: c_int = 3;
+pub const DIPS_SHARD_REF_RESIDENT: u32 = 0x1;
 
 /// `dips_params`: ComputeState::new's arguments (dips/src/gpu/mod.rs:59-65,
 /// DiPsProperties dips/src/lib.rs:63-86) + the batch series configuration.
@@ -90,6 +96,28 @@ pub struct DipsHandle {
 #[repr(C)]
 pub struct DipsAltHandle {
     _p: [u8; 0],
+}
+
+/// Opaque `dips_comm`: one rank's communicator of the sharded series.
+#[repr(C)]
+pub struct DipsComm {
+    _p: [u8; 0],
+}
+
+/// `dips_comm_ops`: the caller's transport of DIPS_COMM_HOST (host buffers;
+/// each returns 0 on success).
+#[repr(C)]
+#[derive(Clone, Copy)]
+pub struct DipsCommOps {
+    pub broadcast: Option<unsafe extern "C" fn(ctx: *mut c_void, buf: *mut c_void, bytes: usize, root: c_int) -> c_int>,
+    pub sendrecv: Option<
+        unsafe extern "C" fn(ctx: *mut c_void, send: *const c_void, to: c_int, recv: *mut c_void, from: c_int,
+                             bytes: usize) -> c_int,
+    >,
+    pub gather: Option<
+        unsafe extern "C" fn(ctx: *mut c_void, send: *const c_void, recv: *mut c_void, bytes: usize, root: c_int)
+                             -> c_int,
+    >,
 }
 
 // The same layout the header pins with DIPS_LAYOUT_ASSERT.
@@ -158,6 +186,31 @@ extern "C" {
     pub fn dips_read_ceiling_walk(h: *mut DipsHandle, dev_frames: *const u8, width: u32, height: u32,
                                   n_frames: u32, ms: *mut f64) -> DipsStatus;
     pub fn dips_abi_version() -> c_int;
+
+    // -- frame-range sharding (no reference counterpart: dips/src/gpu/mod.rs:71-78
+    //    asks for one adapter) ------------------------------------------------
+    pub fn dips_comm_unique_id(id: *mut u8) -> DipsStatus;
+    pub fn dips_comm_create(id: *const u8, nranks: c_int, rank: c_int, device: c_int, out: *mut *mut DipsComm)
+                            -> DipsStatus;
+    pub fn dips_comm_create_loopback(nranks: c_int, device: c_int, comms: *mut *mut DipsComm) -> DipsStatus;
+    pub fn dips_comm_create_host(ops: *const DipsCommOps, ctx: *mut c_void, nranks: c_int, rank: c_int,
+                                 device: c_int, out: *mut *mut DipsComm) -> DipsStatus;
+    pub fn dips_comm_destroy(comm: *mut DipsComm);
+    pub fn dips_comm_last_error(comm: *const DipsComm) -> *const c_char;
+    pub fn dips_comm_info(comm: *const DipsComm, kind: *mut c_int, nranks: *mut c_int, rank: *mut c_int)
+                          -> DipsStatus;
+    pub fn dips_shard_range(n_total: u64, nranks: c_int, rank: c_int, first: *mut u64, count: *mut u32)
+                            -> DipsStatus;
+    pub fn dips_shard_broadcast(h: *mut DipsHandle, comm: *mut DipsComm, width: u32, height: u32, frame: *const u8,
+                                out: *mut u8) -> DipsStatus;
+    pub fn dips_diff_series_sharded(h: *mut DipsHandle, comm: *mut DipsComm, width: u32, height: u32,
+                                    frames: *const u8, n_local: u32, n_total: u64, reference: *const u8,
+                                    shard_flags: u32, series_local: *mut DipsSeriesEntry,
+                                    series_all: *mut DipsSeriesEntry) -> DipsStatus;
+    pub fn dips_shard_plan(h: *mut DipsHandle, comm: *const DipsComm, width: u32, height: u32, n_total: u64,
+                           first: *mut u64, count: *mut u32, waves: *mut u64, waves_uncapped: *mut u64)
+                           -> DipsStatus;
+    pub fn dips_shard_reference(h: *mut DipsHandle, out: *mut u8, cap: usize) -> c_int;
 
     // -- dips_alt DiPsCompute (dips_alt/src/dips_compute/mod.rs) ----------------
     pub fn dips_alt_params_default(p: *mut DipsAltParams) -> DipsStatus;

@@ -439,6 +439,120 @@ impl DiffSeries {
     }
 }
 
+impl DiffSeries {
+    /// Frame-range sharding over `comm` (dips_diff_series_sharded): this
+    /// rank's host frames -- its `shard_range(n_total, ..)` -- give this
+    /// rank's series entries and, on rank 0, the whole gathered series (the
+    /// same as one `run` over all n_total frames).  `reference`: 'overall'
+    /// rank 0's reference (None = its first frame), broadcast to every rank;
+    /// 'per-frame' rank 0's predecessor of frame 0 (None = frame 0), the
+    /// other ranks get theirs from rank r-1.  Every rank calls this with the
+    /// same n_total, like a collective.
+    pub fn run_sharded(&mut self, comm: &mut Comm, width: u32, height: u32, frames: &[u8], n_total: u64,
+                       reference: Option<&[u8]>)
+                       -> Result<(Vec<ffi::DipsSeriesEntry>, Option<Vec<ffi::DipsSeriesEntry>>), DipsError> {
+        let n = self.frames_of(width, height, frames)?;
+        let ref_ptr = self.reference_ptr(width, height, reference)?;
+        let mut local = vec![ffi::DipsSeriesEntry::default(); n as usize];
+        let mut all = if comm.rank == 0 {
+            let total = usize::try_from(n_total)
+                .map_err(|_| DipsError { status: ffi::DIPS_ERR_INVALID, message: "n_total too large".into() })?;
+            Some(vec![ffi::DipsSeriesEntry::default(); total])
+        } else {
+            None
+        };
+        let all_ptr = all.as_mut().map_or(ptr::null_mut(), |v| v.as_mut_ptr());
+        // SAFETY: sizes checked; every buffer is caller-owned for the call (host
+        // pointers: the call returns with the results in them).
+        let st = unsafe {
+            ffi::dips_diff_series_sharded(self.h.as_ptr(), comm.c.as_ptr(), width, height, frames.as_ptr(), n,
+                                          n_total, ref_ptr, 0, local.as_mut_ptr(), all_ptr)
+        };
+        check(st, self.h.as_ptr())?;
+        Ok((local, all))
+    }
+}
+
+/// One rank's communicator of the sharded series (dips_comm_*): RCCL over
+/// xGMI across processes, or loopback ranks as threads of one process.
+pub struct Comm {
+    c: NonNull<ffi::DipsComm>,
+    pub nranks: i32,
+    pub rank: i32,
+}
+
+// A communicator is driven by one thread at a time and may move between them.
+unsafe impl Send for Comm {}
+
+fn check_comm(st: c_int, c: *const ffi::DipsComm) -> Result<c_int, DipsError> {
+    if st >= 0 {
+        Ok(st)
+    } else {
+        // SAFETY: c is a live communicator or null (the last creation error).
+        Err(DipsError { status: st, message: message(unsafe { ffi::dips_comm_last_error(c) }) })
+    }
+}
+
+impl Comm {
+    fn wrap(c: *mut ffi::DipsComm) -> Result<Self, DipsError> {
+        let c = NonNull::new(c).ok_or(DipsError { status: ffi::DIPS_ERR_STATE, message: "null communicator".into() })?;
+        let (mut kind, mut nranks, mut rank) = (0, 0, 0);
+        // SAFETY: c is live; the outputs are locals.
+        check_comm(unsafe { ffi::dips_comm_info(c.as_ptr(), &mut kind, &mut nranks, &mut rank) }, c.as_ptr())?;
+        Ok(Self { c, nranks, rank })
+    }
+
+    /// A new RCCL unique id: rank 0 makes it and hands it to every rank.
+    pub fn unique_id() -> Result<[u8; ffi::DIPS_COMM_ID_BYTES as usize], DipsError> {
+        check_abi()?;
+        let mut id = [0u8; ffi::DIPS_COMM_ID_BYTES as usize];
+        // SAFETY: id has DIPS_COMM_ID_BYTES bytes.
+        check_comm(unsafe { ffi::dips_comm_unique_id(id.as_mut_ptr()) }, ptr::null())?;
+        Ok(id)
+    }
+
+    /// Join the RCCL communicator `id` as `rank` of `nranks` on `device`.
+    pub fn rccl(id: &[u8; ffi::DIPS_COMM_ID_BYTES as usize], nranks: i32, rank: i32, device: i32)
+                -> Result<Self, DipsError> {
+        check_abi()?;
+        let mut c = ptr::null_mut();
+        // SAFETY: id has DIPS_COMM_ID_BYTES bytes, c is an out pointer.
+        check_comm(unsafe { ffi::dips_comm_create(id.as_ptr(), nranks, rank, device, &mut c) }, ptr::null())?;
+        Self::wrap(c)
+    }
+
+    /// `nranks` loopback ranks on `device`; each must be driven by its own
+    /// thread (their collectives meet on the host).
+    pub fn loopback(nranks: i32, device: i32) -> Result<Vec<Self>, DipsError> {
+        check_abi()?;
+        let count = usize::try_from(nranks)
+            .map_err(|_| DipsError { status: ffi::DIPS_ERR_INVALID, message: "nranks < 0".into() })?;
+        let mut cs = vec![ptr::null_mut(); count];
+        // SAFETY: cs has nranks slots.
+        check_comm(unsafe { ffi::dips_comm_create_loopback(nranks, device, cs.as_mut_ptr()) }, ptr::null())?;
+        cs.into_iter().map(Self::wrap).collect()
+    }
+}
+
+impl Drop for Comm {
+    fn drop(&mut self) {
+        // SAFETY: the communicator is live and dropped once.
+        unsafe { ffi::dips_comm_destroy(self.c.as_ptr()) }
+    }
+}
+
+/// Global frames [first, first + count) of `rank` of `nranks` over n_total.
+pub fn shard_range(n_total: u64, nranks: i32, rank: i32) -> Result<(u64, u32), DipsError> {
+    let (mut first, mut count) = (0u64, 0u32);
+    // SAFETY: the outputs are locals.
+    let st = unsafe { ffi::dips_shard_range(n_total, nranks, rank, &mut first, &mut count) };
+    if st == ffi::DIPS_OK {
+        Ok((first, count))
+    } else {
+        Err(DipsError { status: st, message: "rank outside [0, nranks)".into() })
+    }
+}
+
 impl Drop for DiffSeries {
     fn drop(&mut self) {
         // SAFETY: the handle is live and dropped once.

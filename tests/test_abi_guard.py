@@ -97,11 +97,14 @@ def test_every_exported_function_body_is_inside_the_guard():
         where = m.group(1)
         # the error goes to the handle argument, or (creation / handle-free
         # functions) to the process-wide record or nowhere
-        assert where in ("h", "nullptr", "dips_abi::CreateTag{}", "dips_abi::AltCreateTag{}"), (name, where)
+        assert where in ("h", "comm", "nullptr", "dips_abi::CreateTag{}", "dips_abi::AltCreateTag{}",
+                         "dips_abi::CommCreateTag{}"), (name, where)
         if where in ("dips_abi::CreateTag{}", "dips_abi::AltCreateTag{}"):
             assert name in ("dips_create", "dips_alt_create"), name
+        if where == "dips_abi::CommCreateTag{}":
+            assert name.startswith(("dips_comm_create", "dips_comm_unique_id")), name
     # the guard's translation units use the guard from abi_guard.h
-    for fn in ("dips_abi.hip", "compat_abi.hip", "series_abi.hip", "alt_abi.hip"):
+    for fn in ("dips_abi.hip", "compat_abi.hip", "series_abi.hip", "alt_abi.hip", "shard_abi.hip"):
         assert "using dips_abi::guard;" in sources[fn], fn
 
 

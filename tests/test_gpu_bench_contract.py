@@ -46,8 +46,13 @@ def test_bench_line_keeps_the_contract():
     assert isinstance(c["cores"], int) and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
     assert c["series_matches_gpu"] is True
     assert d["check"]["equal"] is True
-    # the batch's placement: both candidates timed, the faster kept (dips_amd/placement.py)
+    # the batch's placement: both candidates timed alternately, the plain one
+    # kept unless the other is faster by more than the threshold
+    # (tools/placement.py), and the plain allocation's rate in the roofline
+    from tools.placement import choose
     pl = d["placement"]
     assert isinstance(pl, list) and len(pl) == 1 and pl[0]["probe"] is True
     ms = pl[0]["candidate_kernel_ms"]
-    assert len(ms) == 2 and ms[pl[0]["kept"]] == min(ms)
+    assert len(ms) == 2 and pl[0]["kept"] == choose(ms[0], ms[1], pl[0]["threshold"])[0]
+    assert r["plain_kernel_ms"] == pytest.approx(ms[0], abs=1e-4)
+    assert r["plain_frac"] == pytest.approx(F * W * H * 3 / (ms[0] / 1e3) / 1e9 / 8000.0, rel=2e-3)

@@ -1,21 +1,21 @@
 """bench.py's N > 1 path rehearsed on the one GPU of a test box: two ranks
-over gloo (which moves device tensors for every collective the step uses on
-this torch build, tools/gloo_cuda_probe.py) on device 0 -- the halo
-send/recv of device tensors beside the persistent series kernel under the
-4-wave cap, the gather, the configs[3] / configs[4] legs and the
-self-check, exactly as the driver's RCCL run executes them; RCCL itself
-refuses two ranks on one GPU.
+on device 0 over gloo, RCCL itself refusing two ranks on one GPU.
 
-The shape is chosen so that the schedule the driver's 4K run takes is the
-one rehearsed: 2560x1440 RGB8, 300 frames per rank -- the 1 + (F - 1)
-split of shard.per_frame_overlapped gives a 299-frame launch, which under
-DIPS_SERIES_WAVES_PER_SIMD=4 runs the part-major schedule (2 parts of 150
-frames on a 256-CU MI355X; asserted through the library's own geometry).
-The gathered series is dumped and compared with the CPU oracle on every
-shard-boundary frame and a seeded sample; `--check` makes rank 0 compare
-the gather with one single-device launch over all 600 frames too.  A
-damaged halo must make the run exit non-zero with "equal": false in its
-line."""
+The native path (the default): each step is one dips_diff_series_sharded
+call per rank, the library's own sharding -- halo exchange, the series
+launches, the gather of the series -- over the DIPS_COMM_HOST transport
+backed by the gloo group (dips_amd.comm.TorchHostTransport); the driver's
+run is the same call over an RCCL communicator.  The torch path
+(DIPS_BENCH_SHARD=torch) is the older Python-level protocol of
+dips_amd.shard with gloo moving device tensors.  Both run the configs[3] /
+configs[4] legs and the self-check, exactly as the driver's run does.
+
+2560x1440 RGB8, 300 frames per rank: rank 1's (F - 1)-frame launch beside
+the halo runs the part-major schedule.  The gathered series is dumped and
+compared with the CPU oracle on every shard-boundary frame and a seeded
+sample; `--check` makes rank 0 compare the gather with one single-device
+launch over all 600 frames too.  A damaged halo must make the run exit
+non-zero with "equal": false in its line, on either path."""
 import json
 import os
 import socket
@@ -45,8 +45,8 @@ def _port():
     return p
 
 
-def _run(mode, corrupt, dump=None, frames=F, width=W, height=H, extra=(), env_extra=None):
-    env = dict(os.environ, DIPS_BENCH_BACKEND="gloo", DIPS_BENCH_ONE_DEVICE="1",
+def _run(mode, corrupt, dump=None, frames=F, width=W, height=H, extra=(), env_extra=None, path="native"):
+    env = dict(os.environ, DIPS_BENCH_BACKEND="gloo", DIPS_BENCH_ONE_DEVICE="1", DIPS_BENCH_SHARD=path,
                DIPS_BENCH_CORRUPT_HALO="1" if corrupt else "0", **(env_extra or {}))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(WORLD),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
@@ -84,25 +84,26 @@ def _picks(n_total, world, n_random=6):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("mode", ["per-frame", "overall"])
-def test_bench_two_ranks_rehearsal(mode, tmp_path, monkeypatch):
+@pytest.mark.parametrize("mode,path", [("per-frame", "native"), ("overall", "native"), ("per-frame", "torch")])
+def test_bench_two_ranks_rehearsal(mode, path, tmp_path):
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     if mode == "per-frame":
-        # the schedule of the rank's (F - 1)-frame launch under the bench's
-        # N > 1 wave cap: part-major with >= 2 parts
-        monkeypatch.setenv("DIPS_SERIES_WAVES_PER_SIMD", "4")
+        # the schedule of rank 1's (F - 1)-frame launch: part-major, >= 2 parts
         op = DiffSeriesOperator(PixelFormat.RGB8, Mode.PerFrame, TAU)
         try:
             sch = library_schedule(op, W, H, F - 1)
         finally:
             op.close()
-        monkeypatch.delenv("DIPS_SERIES_WAVES_PER_SIMD")
         assert sch is not None and sch[1] >= 2, sch
     dump = str(tmp_path / "series.npy")
-    rc, line, err = _run(mode, corrupt=False, dump=dump, extra=("--check",))
+    rc, line, err = _run(mode, corrupt=False, dump=dump, extra=("--check",), path=path)
     assert rc == 0, err
     assert line["n_gpus"] == WORLD and line["ranks"] == WORLD and len(line["devices"]) == WORLD, line
     assert "rehearsal" in line["config"]["parallelism"]
+    assert line["shard_path"]["path"] == path, line["shard_path"]
+    if path == "native":
+        assert "dips_diff_series_sharded" in line["config"]["parallelism"]
+        assert line["shard_path"]["transport"].startswith("host (gloo")
     assert "--check: gathered series" in err
     assert line["check"]["equal"] is True and line["check"]["frames_checked"] >= 12
     for key in ("configs3", "configs4"):
@@ -124,10 +125,12 @@ def test_bench_two_ranks_rehearsal(mode, tmp_path, monkeypatch):
 
 
 @pytest.mark.timeout(600)
-def test_bench_two_ranks_damaged_halo_fails():
-    rc, line, err = _run("per-frame", corrupt=True, frames=24, width=640, height=360)
+@pytest.mark.parametrize("path", ["native", "torch"])
+def test_bench_two_ranks_damaged_halo_fails(path):
+    rc, line, err = _run("per-frame", corrupt=True, frames=24, width=640, height=360, path=path)
     assert rc != 0
     assert line is not None and line["check"]["equal"] is False, (line, err)
+    assert line["shard_path"]["path"] == path
 
 
 @pytest.mark.timeout(300)

@@ -3,8 +3,11 @@ the per-rank compute: two processes on the one GPU of the box, gloo as the
 process group (RCCL refuses two ranks on one device, "Duplicate GPU
 detected"), the halo frame and the series staged through host tensors since
 gloo has no device send/recv.  Each rank runs DiffSeriesOperator.run_device
-on its shard under the bench's N > 1 wave cap (DIPS_SERIES_WAVES_PER_SIMD=4);
-the gathered series must equal one single-process launch over all frames."""
+on its shard under the torch path's N > 1 wave cap (DIPS_SERIES_WAVES_PER_SIMD=3,
+one slot per SIMD below the RGB8 kernel's occupancy); the gathered series must
+equal one single-process launch over all frames.  The last test runs the
+native sharded call (dips_diff_series_sharded) in the same two processes over
+the DIPS_COMM_HOST transport backed by the gloo group."""
 import os
 import socket
 
@@ -45,7 +48,7 @@ def _hip_compute(op):
 def _worker(rank, world, port, n_total, mode, overlapped, result_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    os.environ["DIPS_SERIES_WAVES_PER_SIMD"] = "4"
+    os.environ["DIPS_SERIES_WAVES_PER_SIMD"] = "3"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     op = None
     try:
@@ -116,7 +119,7 @@ def _verify_worker(rank, world, port, n_total, mode, corrupt, result_q):
     on the device; `corrupt` = "halo" damages rank 1's received halo."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    os.environ["DIPS_SERIES_WAVES_PER_SIMD"] = "4"
+    os.environ["DIPS_SERIES_WAVES_PER_SIMD"] = "3"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     op = None
     try:
@@ -179,3 +182,66 @@ def test_bench_self_check(mode, corrupt):
     for _, chk in got:
         assert chk["equal"] is (corrupt is None), chk
         assert chk["frames_checked"] >= len(shard.check_frames(n_total, world))
+
+
+def _native_worker(rank, world, port, n_total, mode, host_ptrs, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    op = comm = None
+    try:
+        from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+        from dips_amd.comm import Comm, TorchHostTransport, shard_range
+        torch.cuda.set_device(0)
+        s, e = shard_range(n_total, world, rank)
+        op = DiffSeriesOperator(PixelFormat.RGB8, Mode(mode), TAU)
+        comm = Comm.host(TorchHostTransport(), world, rank, 0)
+        dev = torch.empty((e - s, H, W, 3), dtype=torch.uint8, device="cuda")
+        op.synth_device(dev, W, H, SEED, s)
+        torch.cuda.synchronize()
+        if host_ptrs:
+            _, full = op.sharded(comm, dev.cpu().numpy(), n_total)
+            full = full.as_array() if full is not None else None
+        else:
+            loc = torch.zeros((e - s, 4), dtype=torch.int64, device="cuda")
+            all_ = torch.zeros((n_total, 4), dtype=torch.int64, device="cuda") if rank == 0 else None
+            op.run_sharded(comm, dev, n_total, loc, all_)
+            torch.cuda.synchronize()
+            full = all_.cpu().numpy().view(np.uint64) if rank == 0 else None
+        if rank == 0:
+            result_q.put(full.copy())
+    finally:
+        if op is not None:
+            op.close()
+        if comm is not None:
+            comm.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,host_ptrs", [(0, False), (1, False), (1, True)])
+def test_native_sharded_over_host_transport(mode, host_ptrs):
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    world, n_total = 2, 33
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_worker, args=(r, world, port, n_total, mode, host_ptrs, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = q.get(timeout=300)
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    op = DiffSeriesOperator(PixelFormat.RGB8, Mode(mode), TAU)
+    try:
+        allf = torch.empty((n_total, H, W, 3), dtype=torch.uint8, device="cuda")
+        op.synth_device(allf, W, H, SEED, 0)
+        one = torch.zeros((n_total, 4), dtype=torch.int64, device="cuda")
+        op.run_device(allf, one)
+        torch.cuda.synchronize()
+    finally:
+        op.close()
+    assert np.array_equal(got, one.cpu().numpy().view(np.uint64))

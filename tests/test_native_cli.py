@@ -74,3 +74,29 @@ def test_series_csv_matches_oracle(tmp_path, fmt, c, mode):
     out4, si, _ = oracle.series(frames, mode=0 if mode == "overall" else 1, tau=8 / 255)
     assert np.array_equal(got, out4[:, :3])
     np.testing.assert_allclose([float(row[4]) for row in rows], si, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,n", [(2, 17), (5, 23)])
+@pytest.mark.parametrize("mode", ["overall", "per-frame"])
+def test_sharded_csv_equals_series_csv(tmp_path, ranks, n, mode):
+    """`dips_raw sharded`: N ranks (threads, one handle each) over a loopback
+    communicator through dips_diff_series_sharded give the single-handle
+    series of the whole file, and the oracle's."""
+    w, h = 96, 40
+    frames = oracle.synth(3, w, h, 5, 0, n)
+    src = tmp_path / "in.raw"
+    frames.tofile(src)
+    r1 = _run(["series", src, w, h, "rgb8", "--mode", mode, "--tau", 8 / 255])
+    rn = _run(["sharded", src, w, h, "rgb8", "--ranks", ranks, "--mode", mode, "--tau", 8 / 255])
+    assert r1.returncode == 0 and rn.returncode == 0, r1.stderr + rn.stderr
+    assert rn.stdout == r1.stdout
+    rows = [line.split(",") for line in rn.stdout.strip().splitlines()[1:]]
+    got = np.array([[int(x) for x in row[1:4]] for row in rows], dtype=np.uint64)
+    out4, _, _ = oracle.series(frames, mode=0 if mode == "overall" else 1, tau=8 / 255)
+    assert np.array_equal(got, out4[:, :3])
+
+
+def test_sharded_usage():
+    r = _run(["sharded", "x", "8", "4", "rgb8"])
+    assert r.returncode == 1 and "usage" in r.stderr  # --ranks is required

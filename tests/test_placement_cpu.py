@@ -1,26 +1,32 @@
-"""The selection logic of dips_amd.placement.resident_frames on the CPU
-(torch.cuda calls stubbed; a fake operator whose launches on the second
-candidate take longer, or shorter): the faster candidate is kept and holds
-the fill, both timings are reported, the timer is left reset, and the plain
-paths (probe=False, no room for two, an empty batch) allocate once."""
+"""The selection logic of tools/placement.py resident_frames (bench-only)
+on the CPU (torch.cuda calls stubbed; a fake operator whose launches on the
+second candidate take longer, or shorter): the candidates are timed
+alternately, candidate 0 (the plain allocation) is kept unless candidate 1 is
+faster by more than the threshold, the kept one holds the fill, both timings
+and the margin are reported, the timer is left reset, and the plain paths
+(probe=False, no room for two, an empty batch) allocate once."""
 import pytest
 import torch
 
-from dips_amd import placement
+from tools import placement
 
 
 class _FakeOp:
-    def __init__(self, slow_second):
+    def __init__(self, slow_second, slow=21.2, fast=20.7):
         self.slow_second = slow_second
+        self.slow, self.fast = slow, fast
         self.seen = []
+        self.order = []
         self.ms = 0.0
         self.n = 0
 
     def run_device(self, frames, series, ref=None):
         if frames.data_ptr() not in self.seen:
             self.seen.append(frames.data_ptr())
-        second = self.seen.index(frames.data_ptr()) == 1
-        self.ms += (21.2 if second == self.slow_second else 20.7)
+        idx = self.seen.index(frames.data_ptr())
+        self.order.append(idx)
+        second = idx == 1
+        self.ms += (self.slow if second == self.slow_second else self.fast)
         self.n += 1
 
     def kernel_time(self, reset=False):
@@ -48,12 +54,23 @@ def test_keeps_the_faster_candidate(no_cuda, slow_second):
         t.fill_(7)
         fills.append(t.data_ptr())
 
-    t, rep = placement.resident_frames(op, (4, 3, 5, 3), "cpu", fill, launches=2)
-    assert rep["probe"] and rep["launches_each"] == 2
+    t, rep = placement.resident_frames(op, (4, 3, 5, 3), "cpu", fill, rounds=3)
+    assert rep["probe"] and rep["launches_each"] == 3
     assert rep["kept"] == (0 if slow_second else 1)
     assert rep["candidate_kernel_ms"] == ([20.7, 21.2] if slow_second else [21.2, 20.7])
+    assert abs(rep["margin"] - ((20.7 / 21.2 - 1) if slow_second else (21.2 / 20.7 - 1))) < 1e-4
     assert t.data_ptr() == fills[rep["kept"]] and int(t.sum()) == 7 * t.numel()
     assert op.kernel_time() == (0.0, 0)  # left reset
+    assert op.order == [0, 1] + [0, 1] * 3  # warm launches, then alternated
+
+
+def test_keeps_the_plain_allocation_within_the_threshold(no_cuda):
+    """Candidate 1 faster by 0.5 % (noise for a power-bound kernel): the
+    plain allocation stays."""
+    op = _FakeOp(False, slow=20.8, fast=20.7)
+    t, rep = placement.resident_frames(op, (4, 3, 5, 3), "cpu", lambda x: x.fill_(3))
+    assert rep["kept"] == 0 and 0 < rep["margin"] < rep["threshold"] == 0.01
+    assert placement.choose(21.0, 20.7)[0] == 1 and placement.choose(20.7, 21.0)[0] == 0
 
 
 def test_plain_paths(no_cuda):

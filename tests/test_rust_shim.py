@@ -25,6 +25,7 @@ STRUCTS = {"dips_params": "DipsParams", "dips_series_entry": "DipsSeriesEntry", 
 BASE = {"uint8_t": "u8", "uint16_t": "u16", "int32_t": "i32", "uint32_t": "u32", "uint64_t": "u64",
         "float": "f32", "double": "f64", "size_t": "usize", "int": "c_int", "void": "c_void", "char": "c_char",
         "dips_status": "DipsStatus", "dips_handle": "DipsHandle", "dips_alt_handle": "DipsAltHandle",
+        "dips_comm": "DipsComm", "dips_comm_ops": "DipsCommOps",
         **STRUCTS}
 
 
@@ -227,7 +228,7 @@ def test_failures_are_visible_at_the_rust_boundary():
     assert "panic!" in body and "frame_data.to_vec()" not in body
     ffi = open(FFI).read()
     assert "pub const DIPS_ERR_INTERNAL: DipsStatus = -7;" in ffi
-    assert "pub const DIPS_ABI_VERSION: c_int = 2;" in ffi
+    assert "pub const DIPS_ABI_VERSION: c_int = 3;" in ffi
     assert "pub const DIPS_FLAG_CROSSCHECK: u32 = 0x8;" in ffi
 
 
