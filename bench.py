@@ -814,13 +814,11 @@ def _main(args):
         _WHO["bus"] = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
     except Exception:  # the report only
         pass
+    # N > 1: the native sharded call (default) or the torch protocol.  Neither
+    # caps the series grid for the halo's kernels: posted first, they run
+    # beside the full grid at +0.03-0.07 ms, where a grid one wave per SIMD
+    # short cost 2-5 ms (profiles/r06/halo_contention/)
     shard_path = os.environ.get("DIPS_BENCH_SHARD", "native") if world > 1 else None
-    if shard_path == "torch":
-        # the Python-level protocol launches the series through run_device:
-        # leave one wave slot per SIMD (occupancy 4 - 1 for the RGB8 kernel)
-        # to the halo's send/recv kernels beside it; the native path reserves
-        # the slot itself (dips_shard_plan)
-        os.environ.setdefault("DIPS_SERIES_WAVES_PER_SIMD", "3")
     dev = torch.device("cuda", local)
     if world > 1:
         # a bounded wait: a rank stuck in a collective (a peer that died, a
@@ -844,7 +842,6 @@ def _main(args):
         comm, comm_note = _make_comm(torch, dist, backend, world, rank, local, corrupt_halo)
         if comm is None:
             shard_path = "torch"
-            os.environ.setdefault("DIPS_SERIES_WAVES_PER_SIMD", "3")
 
     W, H, F = args.width, args.height, args.frames_per_gpu
     C = 3

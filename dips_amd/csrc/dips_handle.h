@@ -127,13 +127,13 @@ hipEvent_t take_event(dips_handle* h);
 int occupancy_blocks(dips_handle* h, const void* kernel);
 // a deferred frame's speculative kernels finished (compat_abi.hip)
 dips_status flush_pending(dips_handle* h);
-// the series of device frames, asynchronously on `s` (series_abi.hip);
-// `reserve` leaves one wave slot per SIMD free beside the launch
+// the series of device frames, asynchronously on `s` (series_abi.hip)
 dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
                               uint32_t n_frames, const uint8_t* ref0, dips_series_entry* series, uint8_t* map,
-                              hipStream_t s, bool reserve = false);
-// waves of that launch for an aligned batch of this shape (0: not eligible)
-uint64_t series_waves(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool reserve);
+                              hipStream_t s);
+// waves of that launch for an aligned batch of this shape (0: not eligible),
+// with or without the DIPS_SERIES_WAVES_PER_SIMD cap
+uint64_t series_waves(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool env_cap);
 
 }  // namespace dips_internal
 

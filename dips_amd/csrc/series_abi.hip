@@ -27,20 +27,21 @@ struct FastGeom {
     uint32_t part_frames = 0;  // part-major schedule: frames per part (0: contiguous ranges)
 };
 
-// Resident waves per SIMD for a kernel of `occupancy` waves per SIMD:
-// `reserve` leaves one slot per SIMD free (occupancy - 1) -- the sharded
-// 'per-frame' launch that runs while the transport's halo kernels are in
-// flight (shard_abi.hip), so that they start beside the persistent grid
-// instead of after it; DIPS_SERIES_WAVES_PER_SIMD caps every launch below
-// that (a deployment knob).
-uint64_t waves_per_simd(uint64_t occupancy, bool reserve) {
-    uint64_t w = occupancy;
-    if (reserve && w > 1) w -= 1;
-    if (const char* cap = std::getenv("DIPS_SERIES_WAVES_PER_SIMD")) {
-        const unsigned long c = std::strtoul(cap, nullptr, 10);
-        if (c >= 1 && c < w) w = c;
+// Resident waves per SIMD for a kernel of `occupancy` waves per SIMD, capped
+// by DIPS_SERIES_WAVES_PER_SIMD where `env_cap` (a deployment knob; every
+// launch applies it, dips_shard_plan also reports the uncapped count).  No
+// launch caps itself: leaving a slot per SIMD free for the halo's RCCL
+// kernels beside the sharded 'per-frame' launch cost 2-5 ms per 2,000-5,000
+// 4K frames, where the full grid lets the exchange through at +0.03-0.07 ms
+// (profiles/r06/halo_contention/).
+uint64_t waves_per_simd(uint64_t occupancy, bool env_cap) {
+    if (env_cap) {
+        if (const char* cap = std::getenv("DIPS_SERIES_WAVES_PER_SIMD")) {
+            const unsigned long c = std::strtoul(cap, nullptr, 10);
+            if (c >= 1 && c < occupancy) return c;
+        }
     }
-    return w;
+    return occupancy;
 }
 
 // The part-major schedule of the series kernels (series_v2.hip,
@@ -88,7 +89,7 @@ void part_geometry(FastGeom& g, uint64_t n_frames, uint64_t resident) {
 }
 
 FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, int C, bool pf,
-                       bool map, bool align = false, int isi = 0, bool reserve = false) {
+                       bool map, bool align = false, int isi = 0, bool env_cap = true) {
     FastGeom g;
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t fb = npx * (uint64_t)C;
@@ -106,7 +107,7 @@ FastGeom fast_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t
     g.items = g.n_tiles * n_frames;
     const void* k = dips::series_fast_kernel_ptr(C, C == 1 ? 0 : (int)h->p.chroma_filter, pf, map, align, isi);
     if (!k) return g;
-    const uint64_t resident = waves_per_simd((uint64_t)occupancy_blocks(h, k), reserve) * (uint64_t)h->cu_count * 4u;
+    const uint64_t resident = waves_per_simd((uint64_t)occupancy_blocks(h, k), env_cap) * (uint64_t)h->cu_count * 4u;
     g.n_waves = g.items < resident ? g.items : resident;
     g.blocks = (g.n_waves + 3) / 4;
     if (C == 3 || C == 4) part_geometry(g, n_frames, resident);
@@ -135,7 +136,7 @@ constexpr int kGrayLayout = 4;
 
 bool gray_lut_enabled(const dips_handle* h) { return !h->crosscheck(); }
 
-FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool reserve = false) {
+FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool env_cap = true) {
     FastGeom g;
     const uint64_t npx = (uint64_t)width * height;
     const uint64_t nvec = npx / 16u;
@@ -147,7 +148,7 @@ FastGeom gray_lut_geometry(dips_handle* h, uint32_t width, uint32_t height, uint
     g.n_tiles = (nvec + 64 * U - 1) / (64 * U);
     g.items = g.n_tiles * n_frames;
     // one group per CU (the tables fill its LDS): 4 waves per SIMD
-    const uint64_t resident = waves_per_simd(gw / 4u, reserve) * 4u * (uint64_t)h->cu_count;
+    const uint64_t resident = waves_per_simd(gw / 4u, env_cap) * 4u * (uint64_t)h->cu_count;
     g.n_waves = g.items < resident ? g.items : resident;
     // 'per-frame' batches: the part-major schedule, as for RGB8 (part_geometry)
     if (h->p.mode == DIPS_MODE_PER_FRAME) part_geometry(g, n_frames, resident);
@@ -179,11 +180,10 @@ int series_isi_form(const dips_handle* h) {
 
 namespace dips_internal {
 
-// Run the series on device pointers, asynchronously on `s` (`reserve`: see
-// waves_per_simd).
+// Run the series on device pointers, asynchronously on `s`.
 dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
                               uint32_t n_frames, const uint8_t* ref0, dips_series_entry* series, uint8_t* map,
-                              hipStream_t s, bool reserve) {
+                              hipStream_t s) {
     const int C = (int)h->p.format;
     const bool pf = h->p.mode == DIPS_MODE_PER_FRAME;
     const uint64_t npx = (uint64_t)width * height;
@@ -196,8 +196,8 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
     const bool align = (C == 3 || C == 4) && ((((uintptr_t)frames | (uintptr_t)fb | (uintptr_t)ref0) & 3u) != 0u);
     const int isi = series_isi_form(h);
     if (!(h->p.flags & DIPS_FLAG_FORCE_GENERIC))
-        g = glut ? gray_lut_geometry(h, width, height, n_frames, reserve)
-                 : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr, align, isi, reserve);
+        g = glut ? gray_lut_geometry(h, width, height, n_frames)
+                 : fast_geometry(h, width, height, n_frames, C, pf, map != nullptr, align, isi);
     // the series starts at zero: the table and RGB(A) kernels clear it
     // themselves (SeriesArgs::zero), saving a fill launch; the others after a
     // fill
@@ -309,13 +309,14 @@ dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, c
 }
 
 // Waves of the series launch an aligned batch of this shape runs (0 if the
-// shape is not eligible for the fast kernels).
-uint64_t series_waves(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool reserve) {
+// shape is not eligible for the fast kernels), with or without the
+// DIPS_SERIES_WAVES_PER_SIMD cap.
+uint64_t series_waves(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool env_cap) {
     const int C = (int)h->p.format;
     FastGeom g = C == 1 && gray_lut_enabled(h)
-                     ? gray_lut_geometry(h, width, height, n_frames, reserve)
+                     ? gray_lut_geometry(h, width, height, n_frames, env_cap)
                      : fast_geometry(h, width, height, n_frames, C, h->p.mode == DIPS_MODE_PER_FRAME, false, false,
-                                     series_isi_form(h), reserve);
+                                     series_isi_form(h), env_cap);
     return g.ok ? g.n_waves : 0;
 }
 

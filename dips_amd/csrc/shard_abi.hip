@@ -11,11 +11,13 @@
 //                DIPS_SHARD_REF_RESIDENT), the series launch over the rank's
 //                frames;
 //   'per-frame': rank r sends its last frame to r+1 and receives r-1's
-//                (ncclSend / ncclRecv in one group) on a side stream, while
-//                the series launch over its frames 1..n-1 (each against its
-//                own predecessor) runs with one wave slot per SIMD left free
-//                for the transfer's kernels; frame 0 against the halo once it
-//                has landed;
+//                (ncclSend / ncclRecv in one group) on a side stream, posted
+//                before the series launch over its frames 1..n-1 (each
+//                against its own predecessor), so the transfer's kernels are
+//                resident first and the full persistent grid fills the rest
+//                (a grid capped to leave them room measured worse:
+//                profiles/r06/halo_contention/); frame 0 against the halo
+//                once it has landed;
 //   both:        one ncclGather of the padded per-rank series (32 B a frame)
 //                onto rank 0, trimmed into place there.
 // Everything is stream-ordered on the handle's stream: the call returns
@@ -739,7 +741,7 @@ dips_status dips_diff_series_sharded(dips_handle* h, dips_comm* comm, uint32_t w
             const uint32_t n_main = halo_in ? n - 1 : n;
             if (n_main > 0) {
                 st = run_series_device(h, width, height, halo_in ? fr + fb : fr, n_main, halo_in ? fr : (rf ? rf : fr),
-                                       halo_in ? sl + 1 : sl, nullptr, s, G > 1 && !sync);
+                                       halo_in ? sl + 1 : sl, nullptr, s);
                 if (st != DIPS_OK) return st;
             }
             if (sync) {  // completes on this thread while the launch runs
@@ -810,14 +812,13 @@ dips_status dips_shard_plan(dips_handle* h, const dips_comm* comm, uint32_t widt
         ShardArgs a;
         st = check_shard(h, comm, width, height, n_total, &a);
         if (st != DIPS_OK) return st;
+        // the launch the halo transfer overlaps ('per-frame'): frames 1..n-1
+        // on ranks > 0, all frames on rank 0
         const bool pf = h->p.mode == DIPS_MODE_PER_FRAME;
-        const bool concurrent = pf && comm->nranks > 1 && !comm->host_synchronous();
-        // the launch the halo transfer overlaps: frames 1..n-1 on ranks > 0,
-        // all frames on rank 0
         const uint32_t n_main = (uint32_t)(pf && comm->rank > 0 ? a.count - 1 : a.count);
         if (first) *first = a.first;
         if (count) *count = (uint32_t)a.count;
-        if (waves) *waves = n_main ? series_waves(h, width, height, n_main, concurrent) : 0;
+        if (waves) *waves = n_main ? series_waves(h, width, height, n_main, true) : 0;
         if (waves_uncapped) *waves_uncapped = n_main ? series_waves(h, width, height, n_main, false) : 0;
         return DIPS_OK;
     });

@@ -420,10 +420,12 @@ dips_status dips_diff_series_sharded(dips_handle *h, dips_comm *comm, uint32_t w
                                      const uint8_t *ref, uint32_t shard_flags, dips_series_entry *series_local,
                                      dips_series_entry *series_all);
 
-/* The plan of that call on this rank, without running it: its frame range,
- * the waves of the series launch over its frames 1..n-1 and of the same
- * launch uncapped ('per-frame' at nranks > 1 leaves one wave slot per SIMD
- * free for the transport's halo kernels; equal otherwise). */
+/* The plan of that call on this rank, without running it: its frame range
+ * and the waves of its main series launch (the one the halo transfer
+ * overlaps: frames 1..n-1 on ranks > 0 in 'per-frame' mode, all frames
+ * otherwise), with the DIPS_SERIES_WAVES_PER_SIMD deployment cap applied
+ * (`waves`) and without it (`waves_uncapped`).  The launch itself runs the
+ * full persistent grid: the halo's kernels are posted before it. */
 dips_status dips_shard_plan(dips_handle *h, const dips_comm *comm, uint32_t width, uint32_t height,
                             uint64_t n_total, uint64_t *first, uint32_t *count, uint64_t *waves,
                             uint64_t *waves_uncapped);

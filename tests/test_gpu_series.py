@@ -267,8 +267,9 @@ def test_long_batch_segments_match_oracle(c, mode):
 
 
 def test_wave_cap_same_series(monkeypatch):
-    """DIPS_SERIES_WAVES_PER_SIMD (set by bench.py at N > 1) only changes how
-    the (tile, frame) items are split over waves: same series, fewer waves."""
+    """DIPS_SERIES_WAVES_PER_SIMD (a deployment cap; nothing sets it by
+    default) only changes how the (tile, frame) items are split over waves:
+    same series, fewer waves."""
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     w, h, n = 640, 360, 300

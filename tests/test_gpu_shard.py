@@ -3,9 +3,8 @@ the per-rank compute: two processes on the one GPU of the box, gloo as the
 process group (RCCL refuses two ranks on one device, "Duplicate GPU
 detected"), the halo frame and the series staged through host tensors since
 gloo has no device send/recv.  Each rank runs DiffSeriesOperator.run_device
-on its shard under the torch path's N > 1 wave cap (DIPS_SERIES_WAVES_PER_SIMD=3,
-one slot per SIMD below the RGB8 kernel's occupancy); the gathered series must
-equal one single-process launch over all frames.  The last test runs the
+on its shard; the gathered series must equal one single-process launch over
+all frames.  The last test runs the
 native sharded call (dips_diff_series_sharded) in the same two processes over
 the DIPS_COMM_HOST transport backed by the gloo group."""
 import os
@@ -48,7 +47,6 @@ def _hip_compute(op):
 def _worker(rank, world, port, n_total, mode, overlapped, result_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    os.environ["DIPS_SERIES_WAVES_PER_SIMD"] = "3"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     op = None
     try:
@@ -119,7 +117,6 @@ def _verify_worker(rank, world, port, n_total, mode, corrupt, result_q):
     on the device; `corrupt` = "halo" damages rank 1's received halo."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    os.environ["DIPS_SERIES_WAVES_PER_SIMD"] = "3"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     op = None
     try:

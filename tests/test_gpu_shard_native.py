@@ -11,8 +11,9 @@ shard_abi.hip) through the C ABI, on the one GPU of the box:
   every rank's first-frame reference (the halo it received, the broadcast
   reference) equals the frame it must be; ragged shards (n_total not a
   multiple of the world size) take the trimmed gather;
-* the plan: the 'per-frame' launch beside the halo leaves one wave slot per
-  SIMD free (fewer waves than uncapped), the other launches are uncapped;
+* the plan: the launch beside the halo runs the full persistent grid; the
+  DIPS_SERIES_WAVES_PER_SIMD deployment cap, when set, gives fewer waves than
+  the uncapped grid (both reported by dips_shard_plan);
 * argument errors return on the rank that has them, with the message.
 
 The reference is single-device (dips/src/gpu/mod.rs:71-78); the sharding is
@@ -155,13 +156,10 @@ def test_loopback_equals_single_launch_and_oracle(world, n_total, mode):
     for r, (s, _) in enumerate(ranges):
         want_ref = frames[s - 1] if (mode == 1 and r > 0) else frames[0]
         assert np.array_equal(first_refs[r], want_ref), r
-    # the launch beside the halo leaves wave slots free ('per-frame', world > 1)
+    # the plan: this rank's range; the full grid (no cap set)
     for r, p in enumerate(plans):
         assert (p["first"], p["first"] + p["count"]) == ranges[r]
-        if mode == 1:
-            assert 0 < p["waves"] <= p["waves_uncapped"]
-        else:
-            assert p["waves"] == p["waves_uncapped"]
+        assert 0 < p["waves"] == p["waves_uncapped"]
 
 
 @pytest.mark.parametrize("fmt_name", ["GRAY8", "RGBA8"])
@@ -184,15 +182,21 @@ def test_loopback_host_pointers_and_resident_reference():
             assert np.array_equal(local[r], want[s:e]), (mode, resident, r)
 
 
-def test_loopback_part_major_shards_4k():
+def test_loopback_part_major_shards_4k(monkeypatch):
     """The bench's shape on 2 loopback ranks: 4K RGB8, 'per-frame', 600
-    frames (300 a rank: the part-major schedule, and on rank 1 the 299-frame
-    launch beside the halo runs it with the wave reserve)."""
+    frames (300 a rank: the part-major schedule; on rank 1 the 299-frame
+    launch beside the halo), once on the full grid and once under the
+    DIPS_SERIES_WAVES_PER_SIMD=3 deployment cap, which the plan reports as
+    fewer waves than the uncapped grid."""
     W, H, n_total = 3840, 2160, 600
-    full, _, _, plans, _ = _run_loopback(2, n_total, "RGB8", 1, W, H)
     want, _ = _single_launch("RGB8", 1, n_total, W, H)
+    full, _, _, plans, _ = _run_loopback(2, n_total, "RGB8", 1, W, H)
     assert np.array_equal(full, want)
-    assert plans[1]["waves"] < plans[1]["waves_uncapped"], plans
+    assert plans[1]["waves"] == plans[1]["waves_uncapped"], plans
+    monkeypatch.setenv("DIPS_SERIES_WAVES_PER_SIMD", "3")
+    full, _, _, plans, _ = _run_loopback(2, n_total, "RGB8", 1, W, H)
+    assert np.array_equal(full, want)
+    assert 0 < plans[1]["waves"] < plans[1]["waves_uncapped"], plans
 
 
 # -- RCCL at world size 1 ------------------------------------------------------

@@ -11,7 +11,12 @@ library's own geometry, then every one of the 520 series entries must equal
 the oracle's (get_intensity, dips/src/gpu/shaders/dips_shader.wgsl:64-82).
 Also at 4K: 'overall' (configs[3]'s mode, part-major since round 4) and
 RGBA8 frames at a +2-byte offset (the aligned-load form a caller's ring
-buffer lands on)."""
+buffer lands on).
+
+BASELINE.json configs[4] (7680x4320 RGB8, tau = 8/255: ISI = 1) on the
+schedule its 1,250-frame-per-GPU batch runs: 260 frames take the part-major
+schedule with 2 parts (asserted through the library's geometry, both modes),
+and every series entry must equal the oracle's."""
 import numpy as np
 import pytest
 
@@ -23,7 +28,7 @@ pytestmark = pytest.mark.gpu
 W, H, SEED, TAU = 3840, 2160, 0xD1B5, 8.0 / 255.0
 
 
-def _series_vs_oracle(fmt_name, mode, n, offset=0, t0=0):
+def _series_vs_oracle(fmt_name, mode, n, offset=0, t0=0, W=W, H=H, schedule=None):
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
     fmt = getattr(PixelFormat, fmt_name)
@@ -31,7 +36,9 @@ def _series_vs_oracle(fmt_name, mode, n, offset=0, t0=0):
     fb = W * H * c
     op = DiffSeriesOperator(fmt, Mode(mode), TAU, 0)
     try:
-        sch = library_schedule(op, W, H, n) if (mode == 1 and offset == 0) else None
+        if schedule is None:
+            schedule = mode == 1 and offset == 0
+        sch = library_schedule(op, W, H, n) if schedule else None
         buf = torch.empty(n * fb + 16, dtype=torch.uint8, device="cuda")
         dev = buf[offset:offset + n * fb].view(n, H, W, c)
         op.synth_device(dev, W, H, SEED, t0)
@@ -65,3 +72,14 @@ def test_timed_config_overall_every_frame():
 @pytest.mark.timeout(600)
 def test_timed_config_rgba8_offset2_every_frame():
     _series_vs_oracle("RGBA8", 1, 300, offset=2, t0=5)
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("mode", [0, 1])
+def test_configs4_8k_part_major_every_frame(monkeypatch, mode):
+    """configs[4]: 7680x4320 RGB8, tau 8/255, 260 frames on the part-major
+    schedule (>= 2 parts), every entry against the oracle (the bench's
+    1,250-frame batch takes 3 parts of the same tiles)."""
+    monkeypatch.delenv("DIPS_SERIES_WAVES_PER_SIMD", raising=False)
+    sch = _series_vs_oracle("RGB8", mode, 260, t0=1000, W=7680, H=4320, schedule=True)
+    assert sch is not None and sch[1] >= 2, sch

@@ -281,3 +281,71 @@ def test_rust_calls_only_declared_ffi():
 def _read(path):
     with open(path) as f:
         return f.read()
+
+
+# Every method of the crate: the C entry point it calls, the status handling
+# it implements (a token its body must contain) and the rows of
+# tests/rust_contract.cpp that execute the same sequence
+# (tests/test_rust_contract.py: CPU rows without a device, all rows on the GPU).
+METHOD_TABLE = [
+    # (signature prefix in lib.rs, C entry point, handling token, contract rows)
+    ("fn check_abi(", "dips_abi_version", "ffi::DIPS_ERR_STATE", ["check_abi"]),
+    ("fn create(", "dips_create", "check(unsafe { ffi::dips_create(p, device, &mut h) }, ptr::null())?",
+     ["new", "diff_series_new"]),
+    ("pub fn on_device(colorize", "dips_create", "create(&p, device)?", ["new"]),
+    ("pub fn try_add_texture(", "dips_add_texture", "check(st, self.h.as_ptr())?", ["try_add_texture_error"]),
+    ("pub fn add_texture(", "dips_add_texture", "let _ = self.try_add_texture", ["try_add_texture_error"]),
+    ("pub fn try_dispatch(", "dips_dispatch", "check(r, self.h.as_ptr())?",
+     ["try_dispatch_warmup", "try_dispatch_some", "try_dispatch_error"]),
+    ("pub fn dispatch(&mut self)", "dips_dispatch", "panic!", ["dispatch_panics"]),
+    ("pub fn frame_callback_into(", "dips_frame_callback", "check(r, self.h.as_ptr())?",
+     ["frame_callback_into_size_change", "frame_callback_into_ok"]),
+    ("pub fn frame_callback_batch(", "dips_frame_callback_batch", "check(st, self.h.as_ptr())?",
+     ["frame_callback_batch"]),
+    ("pub fn callback_phases(", "dips_callback_phases", "if st == ffi::DIPS_OK { Some(v) } else { None }",
+     ["callback_phases", "callback_phases_after_call"]),
+    ("pub fn try_start_texture(", "dips_start_texture", "check(r, self.h.as_ptr())?", ["try_start_texture"]),
+    ("pub fn start_texture(", "dips_start_texture", "panic!", ["start_texture"]),
+    ("pub fn resume(", "dips_compat_resume", "check(st, self.h.as_ptr())?", ["resume"]),
+    ("pub fn frame_callback(width: u32", "dips_frame_callback", "panic!", ["frame_callback_panics"]),
+    ("pub fn run(&mut self, width: u32", "dips_diff_series", "check(st, self.h.as_ptr())?",
+     ["diff_series_run", "diff_series_refusals"]),
+    ("pub fn run_streamed(", "dips_diff_series_streamed", "check(st, self.h.as_ptr())?",
+     ["diff_series_run_streamed"]),
+    ("pub fn run_sharded(", "dips_diff_series_sharded", "check(st, self.h.as_ptr())?",
+     ["diff_series_run_sharded", "diff_series_run_sharded_error"]),
+    ("pub fn unique_id(", "dips_comm_unique_id", "check_comm(", ["comm_rccl"]),
+    ("pub fn rccl(", "dips_comm_create", "check_comm(", ["comm_rccl", "comm_rccl_error"]),
+    ("pub fn loopback(", "dips_comm_create_loopback", "check_comm(", ["comm_loopback"]),
+    ("pub fn shard_range(", "dips_shard_range", "if st == ffi::DIPS_OK", ["shard_range"]),
+    ("pub fn series_si(", "dips_series_si", "ffi::dips_series_si(e)", ["series_si"]),
+    ("pub fn abi_version(", "dips_abi_version", "ffi::dips_abi_version()", ["series_si"]),
+    ("pub fn new(num_textures", "dips_alt_create", "check_alt(", ["dips_compute_new"]),
+    ("pub fn send_frame(", "dips_alt_send_frame", "check_alt(st, self.h.as_ptr())?", ["dips_compute_send_frame"]),
+    ("pub fn run(&mut self, frames: &[u8], refresh_markers", "dips_alt_run", "check_alt(st, self.h.as_ptr())?",
+     ["dips_compute_run"]),
+]
+
+
+def test_crate_method_table():
+    """each crate method calls the C entry point the
+    table names (directly or, for on_device / add_texture / dispatch /
+    start_texture / frame_callback, through the method that does), carries
+    the status handling named, and has rows in tests/rust_contract.cpp."""
+    from test_rust_contract import contract_rows
+    lib = open(os.path.join(CRATE, "src", "lib.rs")).read()
+    rows = contract_rows()
+    indirect = {"pub fn on_device(colorize": "create(", "pub fn add_texture(": "self.try_add_texture",
+                "pub fn dispatch(&mut self)": "self.try_dispatch()", "pub fn start_texture(": "self.try_start_texture()",
+                "pub fn frame_callback(width: u32": "compute.frame_callback_into("}
+    for sig, entry, token, want_rows in METHOD_TABLE:
+        body = _fn_body(lib, sig)
+        via = indirect.get(sig)
+        assert (f"ffi::{entry}(" in body) or (via and via in body), (sig, entry)
+        assert token in body, (sig, token)
+        for r in want_rows:
+            assert r in rows, (sig, r)
+    # every pub fn of the crate has a row (methods and free functions)
+    pub = set(re.findall(r"pub fn (\w+)\(", lib))
+    covered = {re.match(r"(?:pub )?fn (\w+)\(", sig).group(1) for sig, *_ in METHOD_TABLE}
+    assert pub <= covered | {"code", "channels", "new"}, pub - covered
