@@ -44,11 +44,11 @@ def main():
                     help="GRAY8: the table kernel with its per-workgroup layout choice (auto, the library "
                          "default), the band-keyed or the pair-keyed table pinned, or the f32 kernel")
     ap.add_argument("--no-placement-probe", action="store_true",
-                    help="one plain allocation per config (dips_amd.placement.resident_frames probe=False)")
+                    help="one plain allocation per config (tools/placement.py resident_frames probe=False)")
     args = ap.parse_args()
     import torch
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    from dips_amd.placement import resident_frames
+    from tools.placement import resident_frames
     from oracle import oracle
 
     import bench  # the power legs: energy counter / PPT residency / gfx clock around a leg
