@@ -45,12 +45,13 @@ def _port():
     return p
 
 
-def _run(mode, corrupt, dump=None, frames=F, width=W, height=H, extra=(), env_extra=None, path="native"):
+def _run(mode, corrupt, dump=None, frames=F, width=W, height=H, extra=(), env_extra=None, path="native",
+         world=WORLD):
     env = dict(os.environ, DIPS_BENCH_BACKEND="gloo", DIPS_BENCH_ONE_DEVICE="1", DIPS_BENCH_SHARD=path,
                DIPS_BENCH_CORRUPT_HALO="1" if corrupt else "0", **(env_extra or {}))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(WORLD),
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", str(WORLD), "--steps", "2", "--warmup", "1", "--frames-per-gpu", str(frames),
+           "--gpus", str(world), "--steps", "2", "--warmup", "1", "--frames-per-gpu", str(frames),
            "--width", str(width), "--height", str(height), "--mode", mode,
            "--leg-steps", "1", "--no-cpu-baseline", "--no-pcie", "--no-map", "--no-per-frame-call",
            "--dist-timeout", "120", *extra]
@@ -144,3 +145,18 @@ def test_bench_rank_failure_exits_nonzero_with_device():
     assert rc != 0
     assert line is None
     assert "FAILED on rank 1" in err and "PCI" in err, err
+
+
+@pytest.mark.timeout(600)
+def test_bench_three_ranks_native(tmp_path):
+    """Three ranks: the middle one both receives and sends a halo; the
+    gathered series against the oracle at both shard boundaries."""
+    dump = str(tmp_path / "s3.npy")
+    w, h, f = 640, 360, 40
+    rc, line, err = _run("per-frame", corrupt=False, dump=dump, frames=f, width=w, height=h, world=3,
+                         extra=("--check", "--no-legs"))
+    assert rc == 0, err
+    assert line["n_gpus"] == 3 and line["check"]["equal"] is True and line["shard_path"]["path"] == "native"
+    got = np.load(dump)
+    picks = _picks(3 * f, 3)
+    assert np.array_equal(got[picks], _oracle_rows(picks, 3 * f, True, w, h))

@@ -215,10 +215,11 @@ def _native_worker(rank, world, port, n_total, mode, host_ptrs, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,host_ptrs", [(0, False), (1, False), (1, True)])
-def test_native_sharded_over_host_transport(mode, host_ptrs):
+@pytest.mark.parametrize("world,mode,host_ptrs", [(2, 0, False), (2, 1, False), (2, 1, True), (3, 1, False),
+                                                   (3, 0, True)])
+def test_native_sharded_over_host_transport(world, mode, host_ptrs):
     from dips_amd import DiffSeriesOperator, Mode, PixelFormat
-    world, n_total = 2, 33
+    n_total = 33
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
