@@ -188,6 +188,7 @@ def load() -> ctypes.CDLL:
             "dips_series_geometry": ([_vp, u32, u32, u32, P(u64), P(u64), P(u64)], st),
             "dips_comm_unique_id": ([_vp], st),
             "dips_comm_create": ([_vp, st, st, st, P(_vp)], st),
+            "dips_comm_create_all": ([st, _vp, _vp], st),
             "dips_comm_create_loopback": ([st, st, _vp], st),
             "dips_comm_create_host": ([P(DipsCommOps), _vp, st, st, st, P(_vp)], st),
             "dips_comm_destroy": ([_vp], None),

@@ -10,6 +10,8 @@ only creates the communicator it runs over:
                                          handed to the others out of band --
                                          rccl_from_process_group does that over
                                          an initialised torch process group);
+  Comm.rccl_all(devices)                 every rank in this process, one
+                                         thread per rank (ncclCommInitAll);
   Comm.loopback(nranks, device)          ranks as threads of this process on
                                          one device (tests);
   Comm.host(transport, nranks, rank, device)
@@ -70,6 +72,18 @@ class Comm:
         c = ctypes.c_void_p()
         check_comm(lib.dips_comm_create(buf, int(nranks), int(rank), int(device), ctypes.byref(c)), None)
         return cls(c)
+
+    @classmethod
+    def rccl_all(cls, devices: List[int]) -> List["Comm"]:
+        """Every rank of an RCCL communicator in THIS process
+        (ncclCommInitAll), rank r on devices[r]; drive each from its own
+        thread."""
+        lib = _lib.load()
+        n = len(devices)
+        devs = (ctypes.c_int * n)(*[int(d) for d in devices])
+        arr = (ctypes.c_void_p * n)()
+        check_comm(lib.dips_comm_create_all(n, devs, arr), None)
+        return [cls(ctypes.c_void_p(p)) for p in arr]
 
     @classmethod
     def loopback(cls, nranks: int, device: int = 0) -> List["Comm"]:

@@ -520,6 +520,45 @@ dips_status dips_comm_create(const uint8_t* id, int nranks, int rank, int device
     });
 }
 
+dips_status dips_comm_create_all(int nranks, const int* devices, dips_comm** comms) {
+    return guard(dips_abi::CommCreateTag{}, [&]() -> dips_status {
+        if (!comms || nranks < 1 || nranks > 1024) {
+            set_comm_create_err("comm_create_all: null output or nranks outside [1, 1024]");
+            return DIPS_ERR_INVALID;
+        }
+        for (int r = 0; r < nranks; ++r) comms[r] = nullptr;
+        std::vector<int> devs(nranks);
+        for (int r = 0; r < nranks; ++r) {
+            devs[r] = devices ? devices[r] : r;
+            std::string why;
+            if (device_ok(devs[r], &why) != DIPS_OK) {
+                set_comm_create_err(why);
+                return DIPS_ERR_NODEVICE;
+            }
+        }
+        std::vector<ncclComm_t> raw(nranks, nullptr);
+        const ncclResult_t res = ncclCommInitAll(raw.data(), nranks, devs.data());
+        if (res != ncclSuccess) {
+            const char* last = ncclGetLastError(nullptr);
+            set_comm_create_err(std::string("ncclCommInitAll: ") + ncclGetErrorString(res) +
+                                (last && *last ? std::string(" (") + last + ")" : std::string()));
+            return DIPS_ERR_COMM;
+        }
+        std::vector<std::unique_ptr<RcclComm>> made;
+        for (int r = 0; r < nranks; ++r) {
+            std::unique_ptr<RcclComm> c(new RcclComm());
+            c->kind = DIPS_COMM_RCCL;
+            c->nranks = nranks;
+            c->rank = r;
+            c->device = devs[r];
+            c->c = raw[r];
+            made.push_back(std::move(c));
+        }
+        for (int r = 0; r < nranks; ++r) comms[r] = made[r].release();
+        return DIPS_OK;
+    });
+}
+
 dips_status dips_comm_create_loopback(int nranks, int device, dips_comm** comms) {
     return guard(dips_abi::CommCreateTag{}, [&]() -> dips_status {
         if (!comms || nranks < 1 || nranks > 1024) {

@@ -367,7 +367,13 @@ dips_status dips_comm_unique_id(uint8_t *id);
  * `device` (ncclCommInitRank; blocks until every rank has joined). */
 dips_status dips_comm_create(const uint8_t *id, int nranks, int rank, int device, dips_comm **out);
 
-/* `nranks` loopback communicators on `device`, comms[r] = rank r; each must
+/* All `nranks` RCCL communicators of ONE process (ncclCommInitAll): rank r
+ * on HIP device devices[r] (NULL: device r), comms[r] = rank r.  The host
+ * that drives every GPU from one process -- the reference's single decoder
+ * feeding a node -- runs each rank's calls on its own thread. */
+dips_status dips_comm_create_all(int nranks, const int *devices, dips_comm **comms);
+
+/* `nranks` loopback communicators on `device`; comms[r] = rank r; each must
  * be driven by its own thread (the collectives meet on the host). */
 dips_status dips_comm_create_loopback(int nranks, int device, dips_comm **comms);
 

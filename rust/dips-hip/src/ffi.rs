@@ -192,6 +192,7 @@ extern "C" {
     pub fn dips_comm_unique_id(id: *mut u8) -> DipsStatus;
     pub fn dips_comm_create(id: *const u8, nranks: c_int, rank: c_int, device: c_int, out: *mut *mut DipsComm)
                             -> DipsStatus;
+    pub fn dips_comm_create_all(nranks: c_int, devices: *const c_int, comms: *mut *mut DipsComm) -> DipsStatus;
     pub fn dips_comm_create_loopback(nranks: c_int, device: c_int, comms: *mut *mut DipsComm) -> DipsStatus;
     pub fn dips_comm_create_host(ops: *const DipsCommOps, ctx: *mut c_void, nranks: c_int, rank: c_int,
                                  device: c_int, out: *mut *mut DipsComm) -> DipsStatus;

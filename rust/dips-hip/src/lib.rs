@@ -521,6 +521,19 @@ impl Comm {
         Self::wrap(c)
     }
 
+    /// Every rank of an RCCL communicator in this process (ncclCommInitAll),
+    /// rank r on `devices[r]`: one process driving every GPU of the node, one
+    /// thread per rank.
+    pub fn rccl_all(devices: &[i32]) -> Result<Vec<Self>, DipsError> {
+        check_abi()?;
+        let n = i32::try_from(devices.len())
+            .map_err(|_| DipsError { status: ffi::DIPS_ERR_INVALID, message: "too many devices".into() })?;
+        let mut cs = vec![ptr::null_mut(); devices.len()];
+        // SAFETY: devices and cs both have n entries.
+        check_comm(unsafe { ffi::dips_comm_create_all(n, devices.as_ptr(), cs.as_mut_ptr()) }, ptr::null())?;
+        cs.into_iter().map(Self::wrap).collect()
+    }
+
     /// `nranks` loopback ranks on `device`; each must be driven by its own
     /// thread (their collectives meet on the host).
     pub fn loopback(nranks: i32, device: i32) -> Result<Vec<Self>, DipsError> {

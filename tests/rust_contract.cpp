@@ -236,6 +236,24 @@ struct Comm {
         }
         return Result<Comm*>::Ok(w);
     }
+    static Result<std::vector<Comm*>> rccl_all(const std::vector<int>& devices) {
+        using R = Result<std::vector<Comm*>>;
+        auto a = check_abi();
+        if (!a.ok) return R::Err(a.err);
+        std::vector<dips_comm*> cs(devices.size(), nullptr);
+        auto r = check_comm(dips_comm_create_all((int)devices.size(), devices.data(), cs.data()), nullptr);
+        if (!r.ok) return R::Err(r.err);
+        std::vector<Comm*> out;
+        for (auto* c : cs) {
+            auto* w = new Comm();
+            w->c = c;
+            int kind = 0;
+            auto i = check_comm(dips_comm_info(c, &kind, &w->nranks, &w->rank), c);
+            if (!i.ok) return R::Err(i.err);
+            out.push_back(w);
+        }
+        return R::Ok(out);
+    }
     static Result<std::vector<Comm*>> loopback(int nranks, int device) {
         using R = Result<std::vector<Comm*>>;
         auto a = check_abi();
@@ -640,6 +658,10 @@ void device_rows() {
     if (rc.ok) delete rc.value;
     auto bad_rank = id.ok ? Comm::rccl(id.value, 1, 1, 0) : Result<Comm*>::Err(id.err);
     row("comm_rccl_error", !bad_rank.ok && bad_rank.err.status == DIPS_ERR_INVALID);
+    auto all = Comm::rccl_all({0});
+    row("comm_rccl_all", all.ok && all.value.size() == 1 && all.value[0]->nranks == 1, all.ok ? "" : all.err.message);
+    if (all.ok)
+        for (auto* c : all.value) delete c;
 
     // abi_version / series_si
     dips_series_entry e{1, 2, 3, 1ull << 32};

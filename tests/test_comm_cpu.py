@@ -53,6 +53,8 @@ def test_comm_constructors_check_arguments_first():
     assert lib.dips_comm_create(uid, 1, 0, 0, None) == _lib.DIPS_ERR_INVALID
     arr = (ctypes.c_void_p * 2)()
     assert lib.dips_comm_create_loopback(0, 0, arr) == _lib.DIPS_ERR_INVALID
+    assert lib.dips_comm_create_all(0, None, arr) == _lib.DIPS_ERR_INVALID
+    assert lib.dips_comm_create_all(2, None, None) == _lib.DIPS_ERR_INVALID
     assert lib.dips_comm_create_loopback(2, 0, None) == _lib.DIPS_ERR_INVALID
     ops = _lib.DipsCommOps()  # no callbacks
     assert lib.dips_comm_create_host(ctypes.byref(ops), None, 2, 0, 0, ctypes.byref(out)) == _lib.DIPS_ERR_INVALID

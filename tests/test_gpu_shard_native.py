@@ -243,6 +243,31 @@ def test_rccl_world1_equals_diff_series(fmt_name, mode):
         comm.close()
 
 
+def test_rccl_all_in_process():
+    """dips_comm_create_all (ncclCommInitAll): every rank of one process, at
+    one device here; the sharded call over it equals dips_diff_series."""
+    import torch
+    from dips_amd import DiffSeriesOperator, Mode, PixelFormat
+    from dips_amd.comm import Comm
+    comms = Comm.rccl_all([0])
+    assert len(comms) == 1 and (comms[0].nranks, comms[0].rank) == (1, 0) and "rccl" in repr(comms[0])
+    W, H, n = 320, 96, 19
+    op = DiffSeriesOperator(PixelFormat.RGB8, Mode.PerFrame, TAU)
+    try:
+        fr = torch.empty((n, H, W, 3), dtype=torch.uint8, device="cuda")
+        op.synth_device(fr, W, H, SEED, 0)
+        one = torch.zeros((n, 4), dtype=torch.int64, device="cuda")
+        op.run_device(fr, one)
+        full = torch.zeros_like(one)
+        op.run_sharded(comms[0], fr, n, full, full)
+        torch.cuda.synchronize()
+        assert torch.equal(full, one)
+    finally:
+        op.close()
+        for c in comms:
+            c.close()
+
+
 def test_rccl_world1_bench_shape():
     """4K RGB8 'per-frame' at the bench's part-major size (600 frames) over
     RCCL at world size 1 equals dips_diff_series."""

@@ -317,6 +317,7 @@ METHOD_TABLE = [
     ("pub fn unique_id(", "dips_comm_unique_id", "check_comm(", ["comm_rccl"]),
     ("pub fn rccl(", "dips_comm_create", "check_comm(", ["comm_rccl", "comm_rccl_error"]),
     ("pub fn loopback(", "dips_comm_create_loopback", "check_comm(", ["comm_loopback"]),
+    ("pub fn rccl_all(", "dips_comm_create_all", "check_comm(", ["comm_rccl_all"]),
     ("pub fn shard_range(", "dips_shard_range", "if st == ffi::DIPS_OK", ["shard_range"]),
     ("pub fn series_si(", "dips_series_si", "ffi::dips_series_si(e)", ["series_si"]),
     ("pub fn abi_version(", "dips_abi_version", "ffi::dips_abi_version()", ["series_si"]),
