@@ -226,6 +226,7 @@ void dips_destroy(dips_handle* h) {
         h->shard_halo.release();
         h->shard_send.release();
         h->shard_recv.release();
+        h->shard_send_frame.release();
         if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
         if (h->shard_ev_in) (void)hipEventDestroy(h->shard_ev_in);
         if (h->shard_ev_halo) (void)hipEventDestroy(h->shard_ev_halo);

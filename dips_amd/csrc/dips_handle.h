@@ -107,6 +107,7 @@ struct dips_handle {
     // received halo frame, the padded send / gather buffers of the series,
     // the stream the halo exchange runs on beside the series launch
     dips_host::DevBuf shard_ref, shard_halo, shard_send, shard_recv;
+    dips_host::DevBuf shard_send_frame;  // host-pointer calls: the last frame, sent as the next rank's halo
     hipStream_t comm_stream = nullptr;
     hipEvent_t shard_ev_in = nullptr, shard_ev_halo = nullptr;
     const uint8_t* shard_last_ref = nullptr;  // the reference of the last sharded call's first frame
@@ -131,6 +132,11 @@ dips_status flush_pending(dips_handle* h);
 dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
                               uint32_t n_frames, const uint8_t* ref0, dips_series_entry* series, uint8_t* map,
                               hipStream_t s);
+// the series of HOST frames through the pinned, side-stream feed
+// (series_abi.hip); `ref_dev` a device reference of the first frame or NULL
+dips_status run_series_streamed(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* host_frames,
+                                uint32_t n_frames, const uint8_t* ref_dev, dips_series_entry* series_dev,
+                                uint32_t chunk_frames);
 // waves of that launch for an aligned batch of this shape (0: not eligible),
 // with or without the DIPS_SERIES_WAVES_PER_SIMD cap
 uint64_t series_waves(dips_handle* h, uint32_t width, uint32_t height, uint32_t n_frames, bool env_cap);

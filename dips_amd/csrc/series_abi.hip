@@ -320,6 +320,66 @@ uint64_t series_waves(dips_handle* h, uint32_t width, uint32_t height, uint32_t 
     return g.ok ? g.n_waves : 0;
 }
 
+// The series of `n_frames` HOST frames staged through pooled pinned buffers
+// and copied to a triple-buffered HBM ring on the side stream, each chunk's
+// copy overlapping the previous chunk's series launch (next-1 of SURVEY.md
+// s8f); `ref_dev` = the DEVICE reference of the first frame (NULL: overall
+// -> the first frame, per-frame -> the first frame itself).  Series into
+// the device array `series_dev`, asynchronously on the handle's stream once
+// the last chunk is queued (the host frames are all read when it returns).
+dips_status run_series_streamed(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* host_frames,
+                                uint32_t n_frames, const uint8_t* ref_dev, dips_series_entry* series_dev,
+                                uint32_t chunk_frames) {
+    if (n_frames == 0) return DIPS_OK;
+    const bool pf = h->p.mode == DIPS_MODE_PER_FRAME;
+    const size_t fb = (size_t)width * height * (size_t)h->p.format;
+    uint32_t chunk = chunk_frames;
+    if (chunk == 0) {
+        const size_t target = 256u << 20;  // ~256 MiB per DMA chunk
+        chunk = (uint32_t)(target / fb);
+        if (chunk < 1) chunk = 1;
+    }
+    if (chunk > n_frames) chunk = n_frames;
+    const size_t cbytes = fb * chunk;
+    for (auto& r : h->ring) DIPS_HIP(h, r.ensure(cbytes));
+    DIPS_HIP(h, h->ring_ref.ensure(fb));
+    for (auto& pn : h->pinned) DIPS_HIP(h, pn.ensure(cbytes));
+    DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
+    // the ring and the pinned buffers are free once the stream's earlier
+    // work (a previous streamed call's kernels) is done
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    const uint32_t n_chunks = (n_frames + chunk - 1) / chunk;
+    for (uint32_t k = 0; k < n_chunks; ++k) {
+        const uint32_t b = k % 3u, hb = k % 2u;
+        const uint32_t f0 = k * chunk;
+        const uint32_t nk = (f0 + chunk <= n_frames) ? chunk : n_frames - f0;
+        // pinned[hb] was last read by the DMA of chunk k-2
+        if (k >= 2) DIPS_HIP(h, hipEventSynchronize(h->copy_done[(k - 2) % 3u]));
+        dips_host::staged_copy(static_cast<uint8_t*>(h->pinned[hb].p), host_frames + (size_t)f0 * fb,
+                               (size_t)nk * fb);
+        // ring[b] was read by kernel k-3 (frames) and kernel k-2 (per-frame ref)
+        if (k >= 2) DIPS_HIP(h, hipStreamWaitEvent(h->copy_stream, h->kernel_done[(k - 2) % 3u], 0));
+        // the upload by a copy kernel (1.00-1.15x the DMA engine's rate here)
+        DIPS_HIP(h, dips_host::pipe_h2d(h->ring[b].p, h->pinned[hb].p, (size_t)nk * fb, h->copy_stream, true));
+        DIPS_HIP(h, hipEventRecord(h->copy_done[b], h->copy_stream));
+        DIPS_HIP(h, hipStreamWaitEvent(h->stream, h->copy_done[b], 0));
+        const uint8_t* frames_dev = h->ring[b].as<uint8_t>();
+        const uint8_t* ref;
+        if (pf) {
+            if (k == 0) ref = ref_dev ? ref_dev : frames_dev;
+            else ref = h->ring[(k - 1) % 3u].as<uint8_t>() + (size_t)(chunk - 1) * fb;
+        } else {
+            if (k == 0 && !ref_dev)
+                DIPS_HIP(h, hipMemcpyAsync(h->ring_ref.p, frames_dev, fb, hipMemcpyDeviceToDevice, h->stream));
+            ref = ref_dev ? ref_dev : h->ring_ref.as<uint8_t>();
+        }
+        dips_status st = run_series_device(h, width, height, frames_dev, nk, ref, series_dev + f0, nullptr, h->stream);
+        if (st != DIPS_OK) return st;
+        DIPS_HIP(h, hipEventRecord(h->kernel_done[b], h->stream));
+    }
+    return DIPS_OK;
+}
+
 }  // namespace dips_internal
 
 namespace {
@@ -395,60 +455,22 @@ dips_status dips_diff_series_streamed(dips_handle* h, uint32_t width, uint32_t h
         if (n_frames == 0) return DIPS_OK;
         if (!host_frames || !series || width == 0 || height == 0)
             return fail(h, DIPS_ERR_INVALID, "diff_series_streamed: null or empty argument");
-        const int C = (int)h->p.format;
-        const bool pf = h->p.mode == DIPS_MODE_PER_FRAME;
-        const size_t fb = (size_t)width * height * (size_t)C;
-        uint32_t chunk = chunk_frames;
-        if (chunk == 0) {
-            const size_t target = 256u << 20;  // ~256 MiB per DMA chunk
-            chunk = (uint32_t)(target / fb);
-            if (chunk < 1) chunk = 1;
-        }
-        if (chunk > n_frames) chunk = n_frames;
-        const size_t cbytes = fb * chunk;
-        for (auto& r : h->ring) DIPS_HIP(h, r.ensure(cbytes));
-        DIPS_HIP(h, h->ring_ref.ensure(fb));
-        for (auto& pn : h->pinned) DIPS_HIP(h, pn.ensure(cbytes));
+        const size_t fb = (size_t)width * height * (size_t)h->p.format;
         DIPS_HIP(h, h->stage_series.ensure(sizeof(dips_series_entry) * (size_t)n_frames));
         dips_series_entry* series_dev = h->stage_series.as<dips_series_entry>();
-        DIPS_HIP(h, hipStreamSynchronize(h->stream));
-        DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
+        const uint8_t* ref_dev = nullptr;
         if (host_ref) {
+            DIPS_HIP(h, hipStreamSynchronize(h->stream));  // ring_ref may still be read by earlier work
+            DIPS_HIP(h, h->ring_ref.ensure(fb));
+            DIPS_HIP(h, h->pinned[1].ensure(fb));
+            DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
             std::memcpy(h->pinned[1].p, host_ref, fb);
             DIPS_HIP(h, hipMemcpyAsync(h->ring_ref.p, h->pinned[1].p, fb, hipMemcpyHostToDevice, h->copy_stream));
             DIPS_HIP(h, hipStreamSynchronize(h->copy_stream));
+            ref_dev = h->ring_ref.as<uint8_t>();
         }
-        const uint32_t n_chunks = (n_frames + chunk - 1) / chunk;
-        for (uint32_t k = 0; k < n_chunks; ++k) {
-            const uint32_t b = k % 3u, hb = k % 2u;
-            const uint32_t f0 = k * chunk;
-            const uint32_t nk = (f0 + chunk <= n_frames) ? chunk : n_frames - f0;
-            // pinned[hb] was last read by the DMA of chunk k-2
-            if (k >= 2) DIPS_HIP(h, hipEventSynchronize(h->copy_done[(k - 2) % 3u]));
-            dips_host::staged_copy(static_cast<uint8_t*>(h->pinned[hb].p), host_frames + (size_t)f0 * fb,
-                                   (size_t)nk * fb);
-            // ring[b] was read by kernel k-3 (frames) and kernel k-2 (per-frame ref)
-            if (k >= 2) DIPS_HIP(h, hipStreamWaitEvent(h->copy_stream, h->kernel_done[(k - 2) % 3u], 0));
-            // the upload by a copy kernel (1.00-1.15x the DMA engine's rate here,
-            // profiles/r02_pipe_kernel_copy_ab_boxA.jsonl)
-            DIPS_HIP(h, dips_host::pipe_h2d(h->ring[b].p, h->pinned[hb].p, (size_t)nk * fb, h->copy_stream, true));
-            DIPS_HIP(h, hipEventRecord(h->copy_done[b], h->copy_stream));
-            DIPS_HIP(h, hipStreamWaitEvent(h->stream, h->copy_done[b], 0));
-            const uint8_t* frames_dev = h->ring[b].as<uint8_t>();
-            const uint8_t* ref_dev;
-            if (pf) {
-                if (k == 0) ref_dev = host_ref ? h->ring_ref.as<uint8_t>() : frames_dev;
-                else ref_dev = h->ring[(k - 1) % 3u].as<uint8_t>() + (size_t)(chunk - 1) * fb;
-            } else {
-                if (k == 0 && !host_ref) {
-                    DIPS_HIP(h, hipMemcpyAsync(h->ring_ref.p, frames_dev, fb, hipMemcpyDeviceToDevice, h->stream));
-                }
-                ref_dev = h->ring_ref.as<uint8_t>();
-            }
-            st = run_series_device(h, width, height, frames_dev, nk, ref_dev, series_dev + f0, nullptr, h->stream);
-            if (st != DIPS_OK) return st;
-            DIPS_HIP(h, hipEventRecord(h->kernel_done[b], h->stream));
-        }
+        st = run_series_streamed(h, width, height, host_frames, n_frames, ref_dev, series_dev, chunk_frames);
+        if (st != DIPS_OK) return st;
         DIPS_HIP(h, hipMemcpyAsync(series, series_dev, sizeof(dips_series_entry) * (size_t)n_frames,
                                    hipMemcpyDeviceToHost, h->stream));
         DIPS_HIP(h, hipStreamSynchronize(h->stream));

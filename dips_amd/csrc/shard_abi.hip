@@ -713,15 +713,13 @@ dips_status dips_diff_series_sharded(dips_handle* h, dips_comm* comm, uint32_t w
         const bool dev = (h->p.flags & DIPS_FLAG_DEVICE_PTRS) != 0;
         hipStream_t s = h->stream;
 
-        // device views of the inputs and outputs (host pointers: staged)
+        // device views of the reference and the outputs (host pointers: the
+        // series in HBM until the end, the frames through the streamed feed)
         const uint8_t* fr = frames;
         const uint8_t* rf = ref;
         dips_series_entry* sl = series_local;
         dips_series_entry* sa = series_all;
         if (!dev) {
-            DIPS_HIP(h, h->stage_frames.ensure(fb * n));
-            DIPS_HIP(h, hipMemcpyAsync(h->stage_frames.p, frames, fb * n, hipMemcpyHostToDevice, s));
-            fr = h->stage_frames.as<uint8_t>();
             if (ref && (resident || r == 0)) {
                 DIPS_HIP(h, h->stage_ref.ensure(fb));
                 DIPS_HIP(h, hipMemcpyAsync(h->stage_ref.p, ref, fb, hipMemcpyHostToDevice, s));
@@ -734,71 +732,123 @@ dips_status dips_diff_series_sharded(dips_handle* h, dips_comm* comm, uint32_t w
             sa = r == 0 ? sl + n : nullptr;
         }
 
-        // 1. the series of this rank's frames
-        const uint8_t* r0 = nullptr;  // the reference of the rank's first frame
-        if (!pf) {
-            if (resident) {
-                r0 = rf;
+        if (!dev) {
+            // 1h. host frames: the reference / halo exchange first, then the
+            // rank's frames through the pinned side-stream feed
+            // (run_series_streamed: PCIe-bound, ~55 GB/s per GPU, no batch-sized
+            // HBM staging)
+            const uint8_t* r0 = nullptr;
+            if (!pf) {
+                if (resident) {
+                    r0 = rf;
+                } else {
+                    DIPS_HIP(h, h->shard_ref.ensure(fb));
+                    if (r == 0)
+                        DIPS_HIP(h, hipMemcpyAsync(h->shard_ref.p, rf ? rf : frames, fb,
+                                                   rf ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+                    DIPS_COMM(h, comm, comm->broadcast(h->shard_ref.p, h->shard_ref.p, fb, 0, s));
+                    r0 = h->shard_ref.as<uint8_t>();
+                }
             } else {
-                DIPS_HIP(h, h->shard_ref.ensure(fb));
-                const uint8_t* src = r == 0 ? (rf ? rf : fr) : nullptr;
-                DIPS_COMM(h, comm, comm->broadcast(src, h->shard_ref.p, fb, 0, s));
-                r0 = h->shard_ref.as<uint8_t>();
+                const bool halo_in = r > 0, send_out = r + 1 < G;
+                if (G > 1) {
+                    st = ensure_comm_stream(h);
+                    if (st != DIPS_OK) return st;
+                    if (send_out) {
+                        DIPS_HIP(h, h->shard_send_frame.ensure(fb));
+                        DIPS_HIP(h, hipMemcpyAsync(h->shard_send_frame.p, frames + (size_t)(n - 1) * fb, fb,
+                                                   hipMemcpyHostToDevice, s));
+                    }
+                    if (halo_in) DIPS_HIP(h, h->shard_halo.ensure(fb));
+                    DIPS_HIP(h, hipEventRecord(h->shard_ev_in, s));
+                    DIPS_HIP(h, hipStreamWaitEvent(h->comm_stream, h->shard_ev_in, 0));
+                    DIPS_COMM(h, comm, comm->exchange(send_out ? h->shard_send_frame.p : nullptr, send_out ? r + 1 : -1,
+                                                      halo_in ? h->shard_halo.p : nullptr, halo_in ? r - 1 : -1, fb,
+                                                      h->comm_stream));
+                    DIPS_HIP(h, hipEventRecord(h->shard_ev_halo, h->comm_stream));
+                    DIPS_HIP(h, hipStreamWaitEvent(s, h->shard_ev_halo, 0));
+                }
+                if (halo_in) {
+                    r0 = h->shard_halo.as<uint8_t>();
+                } else if (rf) {
+                    r0 = rf;
+                } else {  // frame 0 against itself; staged so that dips_shard_reference can return it
+                    DIPS_HIP(h, h->stage_ref.ensure(fb));
+                    DIPS_HIP(h, hipMemcpyAsync(h->stage_ref.p, frames, fb, hipMemcpyHostToDevice, s));
+                    r0 = h->stage_ref.as<uint8_t>();
+                }
             }
-            st = run_series_device(h, width, height, fr, n, r0, sl, nullptr, s);
+            st = run_series_streamed(h, width, height, frames, n, r0, sl, 0);
             if (st != DIPS_OK) return st;
+            h->shard_last_ref = r0;
+            h->shard_last_bytes = fb;
         } else {
-            // 'per-frame': the halo (global frame first-1) from rank r-1 and
-            // this rank's last frame to rank r+1, on the side stream, beside
-            // the launch that needs no halo -- every frame on rank 0, frames
-            // 1..n-1 (each against its predecessor) elsewhere; then frame 0
-            // against the halo once it has landed
-            const bool halo_in = r > 0, send_out = r + 1 < G;
-            const bool sync = G > 1 && comm->host_synchronous();
-            uint8_t* halo = nullptr;
-            if (G > 1) {
-                st = ensure_comm_stream(h);
+            // 1d. device frames
+            const uint8_t* r0 = nullptr;  // the reference of the rank's first frame
+            if (!pf) {
+                if (resident) {
+                    r0 = rf;
+                } else {
+                    DIPS_HIP(h, h->shard_ref.ensure(fb));
+                    const uint8_t* src = r == 0 ? (rf ? rf : fr) : nullptr;
+                    DIPS_COMM(h, comm, comm->broadcast(src, h->shard_ref.p, fb, 0, s));
+                    r0 = h->shard_ref.as<uint8_t>();
+                }
+                st = run_series_device(h, width, height, fr, n, r0, sl, nullptr, s);
                 if (st != DIPS_OK) return st;
-                // the frames are ready once the work issued before this call is
-                DIPS_HIP(h, hipEventRecord(h->shard_ev_in, s));
-                DIPS_HIP(h, hipStreamWaitEvent(h->comm_stream, h->shard_ev_in, 0));
-            }
-            if (halo_in) {
-                DIPS_HIP(h, h->shard_halo.ensure(fb));
-                halo = h->shard_halo.as<uint8_t>();
-            }
-            auto post = [&]() -> dips_status {
-                DIPS_COMM(h, comm, comm->exchange(fr + (size_t)(n - 1) * fb, send_out ? r + 1 : -1, halo,
-                                                  halo_in ? r - 1 : -1, fb, h->comm_stream));
-                DIPS_HIP(h, hipEventRecord(h->shard_ev_halo, h->comm_stream));
-                return DIPS_OK;
-            };
-            if (G > 1 && !sync) {  // stream-ordered: its kernels start first
-                st = post();
-                if (st != DIPS_OK) return st;
-            }
-            const uint32_t n_main = halo_in ? n - 1 : n;
-            if (n_main > 0) {
-                st = run_series_device(h, width, height, halo_in ? fr + fb : fr, n_main, halo_in ? fr : (rf ? rf : fr),
-                                       halo_in ? sl + 1 : sl, nullptr, s);
-                if (st != DIPS_OK) return st;
-            }
-            if (sync) {  // completes on this thread while the launch runs
-                st = post();
-                if (st != DIPS_OK) return st;
-            }
-            // the halo has landed, and the frame sent may change again
-            if (G > 1) DIPS_HIP(h, hipStreamWaitEvent(s, h->shard_ev_halo, 0));
-            if (halo_in) {
-                st = run_series_device(h, width, height, fr, 1, halo, sl, nullptr, s);
-                if (st != DIPS_OK) return st;
-                r0 = halo;
             } else {
-                r0 = rf ? rf : fr;
+                // 'per-frame': the halo (global frame first-1) from rank r-1 and
+                // this rank's last frame to rank r+1, on the side stream, beside
+                // the launch that needs no halo -- every frame on rank 0, frames
+                // 1..n-1 (each against its predecessor) elsewhere; then frame 0
+                // against the halo once it has landed
+                const bool halo_in = r > 0, send_out = r + 1 < G;
+                const bool sync = G > 1 && comm->host_synchronous();
+                uint8_t* halo = nullptr;
+                if (G > 1) {
+                    st = ensure_comm_stream(h);
+                    if (st != DIPS_OK) return st;
+                    // the frames are ready once the work issued before this call is
+                    DIPS_HIP(h, hipEventRecord(h->shard_ev_in, s));
+                    DIPS_HIP(h, hipStreamWaitEvent(h->comm_stream, h->shard_ev_in, 0));
+                }
+                if (halo_in) {
+                    DIPS_HIP(h, h->shard_halo.ensure(fb));
+                    halo = h->shard_halo.as<uint8_t>();
+                }
+                auto post = [&]() -> dips_status {
+                    DIPS_COMM(h, comm, comm->exchange(fr + (size_t)(n - 1) * fb, send_out ? r + 1 : -1, halo,
+                                                      halo_in ? r - 1 : -1, fb, h->comm_stream));
+                    DIPS_HIP(h, hipEventRecord(h->shard_ev_halo, h->comm_stream));
+                    return DIPS_OK;
+                };
+                if (G > 1 && !sync) {  // stream-ordered: its kernels start first
+                    st = post();
+                    if (st != DIPS_OK) return st;
+                }
+                const uint32_t n_main = halo_in ? n - 1 : n;
+                if (n_main > 0) {
+                    st = run_series_device(h, width, height, halo_in ? fr + fb : fr, n_main, halo_in ? fr : (rf ? rf : fr),
+                                           halo_in ? sl + 1 : sl, nullptr, s);
+                    if (st != DIPS_OK) return st;
+                }
+                if (sync) {  // completes on this thread while the launch runs
+                    st = post();
+                    if (st != DIPS_OK) return st;
+                }
+                // the halo has landed, and the frame sent may change again
+                if (G > 1) DIPS_HIP(h, hipStreamWaitEvent(s, h->shard_ev_halo, 0));
+                if (halo_in) {
+                    st = run_series_device(h, width, height, fr, 1, halo, sl, nullptr, s);
+                    if (st != DIPS_OK) return st;
+                    r0 = halo;
+                } else {
+                    r0 = rf ? rf : fr;
+                }
             }
+            h->shard_last_ref = r0;
+            h->shard_last_bytes = fb;
         }
-        h->shard_last_ref = r0;
-        h->shard_last_bytes = fb;
 
         // 2. one gather of the series onto rank 0 (padded to the largest
         // shard; trimmed into place unless every shard has max_n frames)
