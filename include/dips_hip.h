@@ -419,8 +419,10 @@ dips_status dips_shard_broadcast(dips_handle *h, dips_comm *comm, uint32_t width
  *                 may begin at series_local); other ranks: ignored.
  * With DIPS_FLAG_DEVICE_PTRS every pointer is a device pointer and the call
  * is asynchronous on the handle's stream (RCCL / loopback); otherwise host
- * pointers, staged through HBM, and the call returns with the results in
- * host memory.  h's device must be the communicator's. */
+ * pointers: the exchange runs first, then the rank's frames go through the
+ * pinned side-stream feed of dips_diff_series_streamed (no batch-sized HBM
+ * staging), and the call returns with the results in host memory.  h's
+ * device must be the communicator's. */
 dips_status dips_diff_series_sharded(dips_handle *h, dips_comm *comm, uint32_t width, uint32_t height,
                                      const uint8_t *frames, uint32_t n_local, uint64_t n_total,
                                      const uint8_t *ref, uint32_t shard_flags, dips_series_entry *series_local,
