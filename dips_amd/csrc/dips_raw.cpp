@@ -12,12 +12,14 @@
 //   dips_raw series IN.raw W H rgb8|rgba8|gray8 [--mode overall|per-frame]
 //            [--tau T] [--chunk N]        -> CSV frame,sad,sj,count,si
 //   dips_raw sharded IN.raw W H rgb8|rgba8|gray8 --ranks N [--mode ...]
-//            [--tau T]                    -> the same CSV, computed by N
-//            ranks (one thread and one handle each) over a loopback
-//            communicator with dips_diff_series_sharded: each rank hands its
-//            frame range of the file to the library, rank 0 prints the
-//            gathered series (the frame-range sharding a multi-GPU host
-//            drives the same way over dips_comm_create's RCCL)
+//            [--tau T] [--transport loopback|rccl]
+//                                         -> the same CSV, computed by N
+//            ranks (one thread and one handle each) with
+//            dips_diff_series_sharded: each rank hands its frame range of the
+//            file to the library, rank 0 prints the gathered series.
+//            loopback: every rank on device 0; rccl: rank r on device r, all
+//            ranks of this process from dips_comm_create_all -- one process
+//            that decodes once and feeds every GPU of a node
 //
 // Input files are memory-mapped and handed over as host pointers: the
 // library stages them through pinned memory and overlaps the PCIe transfers
@@ -71,7 +73,7 @@ int usage() {
                  "       dips_raw series IN.raw W H rgb8|rgba8|gray8 [--mode overall|per-frame] [--tau T]\n"
                  "                [--chunk N]\n"
                  "       dips_raw sharded IN.raw W H rgb8|rgba8|gray8 --ranks N [--mode overall|per-frame]\n"
-                 "                [--tau T]\n");
+                 "                [--tau T] [--transport loopback|rccl]\n");
     return 1;
 }
 
@@ -177,6 +179,7 @@ void print_series(const dips_series_entry* series, uint64_t n) {
 int run_sharded(int argc, char** argv) {
     if (argc < 6) return usage();
     uint32_t w = 0, h = 0, ranks = 0;
+    std::string transport = "loopback";
     if (!parse_u32(argv[3], &w) || !parse_u32(argv[4], &h)) return usage();
     dips_params p;
     dips_params_default(&p);
@@ -194,6 +197,9 @@ int run_sharded(int argc, char** argv) {
             p.tau = std::strtof(argv[++i], nullptr);
         } else if (a == "--ranks" && has) {
             if (!parse_u32(argv[++i], &ranks) || ranks > 64) return usage();
+        } else if (a == "--transport" && has) {
+            transport = argv[++i];
+            if (transport != "loopback" && transport != "rccl") return usage();
         } else {
             return usage();
         }
@@ -210,10 +216,13 @@ int run_sharded(int argc, char** argv) {
         return 1;
     }
     const uint64_t n_total = in.n / fb;
+    const bool rccl = transport == "rccl";
     std::vector<dips_comm*> comms(ranks, nullptr);
-    int st = dips_comm_create_loopback((int)ranks, 0, comms.data());
+    int st = rccl ? dips_comm_create_all((int)ranks, nullptr, comms.data())  // rank r on device r
+                  : dips_comm_create_loopback((int)ranks, 0, comms.data());
     if (st != DIPS_OK) {
-        std::fprintf(stderr, "dips_raw: dips_comm_create_loopback failed (%d): %s\n", st, dips_comm_last_error(nullptr));
+        std::fprintf(stderr, "dips_raw: %s failed (%d): %s\n", rccl ? "dips_comm_create_all" : "dips_comm_create_loopback",
+                     st, dips_comm_last_error(nullptr));
         return 2;
     }
     std::vector<dips_series_entry> all(n_total);
@@ -230,7 +239,7 @@ int run_sharded(int argc, char** argv) {
                 return;
             }
             dips_handle* hd = nullptr;
-            int s2 = dips_create(&p, 0, &hd);
+            int s2 = dips_create(&p, rccl ? (int)r : 0, &hd);
             if (s2 != DIPS_OK) {
                 rc[r] = s2;
                 why[r] = dips_last_error(nullptr);

@@ -100,3 +100,19 @@ def test_sharded_csv_equals_series_csv(tmp_path, ranks, n, mode):
 def test_sharded_usage():
     r = _run(["sharded", "x", "8", "4", "rgb8"])
     assert r.returncode == 1 and "usage" in r.stderr  # --ranks is required
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["overall", "per-frame"])
+def test_sharded_csv_over_rccl_in_one_process(tmp_path, mode):
+    """`dips_raw sharded --transport rccl`: the ranks of one process from
+    dips_comm_create_all (ncclCommInitAll), rank r on device r -- one rank on
+    the one-GPU box -- give the single-handle series."""
+    w, h, n = 96, 40, 13
+    frames = oracle.synth(3, w, h, 9, 0, n)
+    src = tmp_path / "in.raw"
+    frames.tofile(src)
+    r1 = _run(["series", src, w, h, "rgb8", "--mode", mode])
+    rn = _run(["sharded", src, w, h, "rgb8", "--ranks", 1, "--mode", mode, "--transport", "rccl"])
+    assert r1.returncode == 0 and rn.returncode == 0, r1.stderr + rn.stderr
+    assert rn.stdout == r1.stdout
