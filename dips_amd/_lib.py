@@ -197,6 +197,7 @@ def load() -> ctypes.CDLL:
             "dips_shard_range": ([u64, st, st, P(u64), P(u32)], st),
             "dips_shard_broadcast": ([_vp, _vp, u32, u32, _u8p, _u8p], st),
             "dips_diff_series_sharded": ([_vp, _vp, u32, u32, _u8p, u32, u64, _u8p, u32, _vp, _vp], st),
+            "dips_frame_callback_batch_sharded": ([_vp, _vp, u32, u32, _u8p, u32, u64, _u8p], st),
             "dips_shard_plan": ([_vp, _vp, u32, u32, u64, P(u64), P(u32), P(u64), P(u64)], st),
             "dips_shard_reference": ([_vp, _u8p, ctypes.c_size_t], st),
             "dips_alt_params_default": ([P(DipsAltParams)], st),

@@ -255,6 +255,36 @@ class ComputeState:
         return self._dev
 
     # -- frame-range sharding (3-frame halo + start texture) --
+    def frame_callback_batch_sharded(self, comm, width: int, height: int, frames, n_total: int) -> np.ndarray:
+        """dips_frame_callback_batch_sharded on host arrays: this rank's
+        frames [n_local, H, W, 4] (its shard_range of n_total) through a
+        fresh ComputeState, the outputs one ComputeState over all frames
+        gives them; the library exchanges the 3-frame halo and broadcasts the
+        start texture."""
+        a = _as_u8(frames)
+        if a.size % (width * height * 4) != 0:
+            raise ValueError("frames must be [N, height, width, 4] RGBA8")
+        n = a.size // (width * height * 4)
+        out = np.empty((n, height, width, 4), dtype=np.uint8)
+        self._hd.check(self._hd._lib.dips_frame_callback_batch_sharded(
+            self._hd.ptr, comm.ptr, width, height, a.ctypes.data, n, int(n_total), out.ctypes.data))
+        self._w, self._h = width, height
+        return out
+
+    def frame_callback_batch_sharded_device(self, comm, frames, out, n_total: int, stream=None) -> None:
+        """The same on uint8 HIP tensors [n_local, H, W, 4] (the device
+        handle, asynchronous on the tensor's current stream)."""
+        n, h, w = int(frames.shape[0]), int(frames.shape[1]), int(frames.shape[2])
+        if tuple(frames.shape) != (n, h, w, 4) or tuple(out.shape) != tuple(frames.shape):
+            raise ValueError("frames/out must be [N, H, W, 4] uint8 tensors")
+        for t in (frames, out):
+            if not t.is_cuda or not t.is_contiguous():
+                raise ValueError("device path needs contiguous HIP tensors")
+        dv = self._device_handle()
+        with _stream_of(dv, frames, stream):
+            dv.check(dv._lib.dips_frame_callback_batch_sharded(dv.ptr, comm.ptr, w, h, frames.data_ptr(), n,
+                                                               int(n_total), out.data_ptr()))
+
     def resume(self, width: int, height: int, start, halo, t0: int) -> None:
         """Continue as if frame_callback had seen global frames 0..t0-1
         (t0 >= 7, any window): `start` is the start texture of the handle that

@@ -490,6 +490,58 @@ int frame_callback_striped(dips_handle* h, const uint8_t* frame, uint8_t* out) {
 
 }  // namespace
 
+namespace dips_internal {
+
+dips_status compat_resume_impl(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* start_rgba,
+                               const uint8_t* halo, uint64_t t0, bool dev) {
+    if (!start_rgba || !halo || width == 0 || height == 0)
+        return fail(h, DIPS_ERR_INVALID, "compat_resume: null or empty argument");
+    if (t0 < 7) return fail(h, DIPS_ERR_INVALID, "compat_resume: t0 must be >= 7 (steady state of the ring)");
+    // a deferred frame's speculative kernels (odd stripes on copy_stream)
+    // must land before the slots are rewritten below on h->stream
+    dips_status st = flush_pending(h);
+    if (st != DIPS_OK) return st;
+    const size_t fb = (size_t)width * height * 4u;
+
+    for (auto& sl : h->slots) DIPS_HIP(h, sl.ensure(fb));
+    DIPS_HIP(h, h->raw.ensure(fb));
+    DIPS_HIP(h, h->start.ensure(fb));
+    DIPS_HIP(h, h->out.ensure(fb));
+    DIPS_HIP(h, h->io.ensure(fb));
+    DIPS_HIP(h, hipStreamSynchronize(h->stream));
+    const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    DIPS_HIP(h, hipMemcpyAsync(h->start.p, start_rgba, fb, kind, h->stream));
+    // slot (t0-1-j) mod 4 <- ring texel of frame t0-1-j (halo[2-j]); the
+    // raw frame goes through h->raw when it comes from the host
+    for (int j = 0; j < 3; ++j) {
+        const uint8_t* src = halo + (size_t)(2 - j) * fb;
+        if (!dev) {
+            DIPS_HIP(h, hipMemcpyAsync(h->raw.p, src, fb, hipMemcpyHostToDevice, h->stream));
+            src = h->raw.as<uint8_t>();
+        }
+        uint8_t* slot = h->slots[(t0 - 1 - (uint64_t)j) % 4u].as<uint8_t>();
+        if (h->p.spatial_window_size == 1)
+            DIPS_HIP(h, dips::launch_compat_gray(src, slot, (uint64_t)width * height, h->p.chroma_filter,
+                                                 h->stream));
+        else  // the filtered texel compute_main stored (dips_shader.wgsl:120-170, 187)
+            DIPS_HIP(h, dips::launch_compat_filter_frames(src, slot, width, height, 1, h->p.spatial_window_size,
+                                                          h->p.chroma_filter, h->stream));
+    }
+    DIPS_HIP(h, hipMemsetAsync(h->slots[t0 % 4u].p, 0, fb, h->stream));
+    if (!dev) DIPS_HIP(h, hipStreamSynchronize(h->stream));  // host buffers are borrowed for the call only
+    h->width = width;
+    h->height = height;
+    h->n_queued = 4;
+    h->main_init = true;
+    for (auto& r : h->slot_raw) r = false;  // gray texels, as the ring of a continuous run
+    h->ring_idx = (uint32_t)(t0 % 4u);
+    h->uniform_idx = (uint32_t)((t0 - 1) % 4u);
+    h->added = t0;
+    return DIPS_OK;
+}
+
+}  // namespace dips_internal
+
 extern "C" {
 
 dips_status dips_add_texture(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frame, size_t len) {
@@ -534,50 +586,7 @@ dips_status dips_compat_resume(dips_handle* h, uint32_t width, uint32_t height, 
     return guard(h, [&]() -> dips_status {
         dips_status st = bind(h);
         if (st != DIPS_OK) return st;
-        if (!start_rgba || !halo || width == 0 || height == 0)
-            return fail(h, DIPS_ERR_INVALID, "compat_resume: null or empty argument");
-        if (t0 < 7) return fail(h, DIPS_ERR_INVALID, "compat_resume: t0 must be >= 7 (steady state of the ring)");
-        // a deferred frame's speculative kernels (odd stripes on copy_stream)
-        // must land before the slots are rewritten below on h->stream
-        st = flush_pending(h);
-        if (st != DIPS_OK) return st;
-        const size_t fb = (size_t)width * height * 4u;
-        const bool dev = (h->p.flags & DIPS_FLAG_DEVICE_PTRS) != 0;
-        for (auto& sl : h->slots) DIPS_HIP(h, sl.ensure(fb));
-        DIPS_HIP(h, h->raw.ensure(fb));
-        DIPS_HIP(h, h->start.ensure(fb));
-        DIPS_HIP(h, h->out.ensure(fb));
-        DIPS_HIP(h, h->io.ensure(fb));
-        DIPS_HIP(h, hipStreamSynchronize(h->stream));
-        const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-        DIPS_HIP(h, hipMemcpyAsync(h->start.p, start_rgba, fb, kind, h->stream));
-        // slot (t0-1-j) mod 4 <- ring texel of frame t0-1-j (halo[2-j]); the
-        // raw frame goes through h->raw when it comes from the host
-        for (int j = 0; j < 3; ++j) {
-            const uint8_t* src = halo + (size_t)(2 - j) * fb;
-            if (!dev) {
-                DIPS_HIP(h, hipMemcpyAsync(h->raw.p, src, fb, hipMemcpyHostToDevice, h->stream));
-                src = h->raw.as<uint8_t>();
-            }
-            uint8_t* slot = h->slots[(t0 - 1 - (uint64_t)j) % 4u].as<uint8_t>();
-            if (h->p.spatial_window_size == 1)
-                DIPS_HIP(h, dips::launch_compat_gray(src, slot, (uint64_t)width * height, h->p.chroma_filter,
-                                                     h->stream));
-            else  // the filtered texel compute_main stored (dips_shader.wgsl:120-170, 187)
-                DIPS_HIP(h, dips::launch_compat_filter_frames(src, slot, width, height, 1, h->p.spatial_window_size,
-                                                              h->p.chroma_filter, h->stream));
-        }
-        DIPS_HIP(h, hipMemsetAsync(h->slots[t0 % 4u].p, 0, fb, h->stream));
-        if (!dev) DIPS_HIP(h, hipStreamSynchronize(h->stream));  // host buffers are borrowed for the call only
-        h->width = width;
-        h->height = height;
-        h->n_queued = 4;
-        h->main_init = true;
-        for (auto& r : h->slot_raw) r = false;  // gray texels, as the ring of a continuous run
-        h->ring_idx = (uint32_t)(t0 % 4u);
-        h->uniform_idx = (uint32_t)((t0 - 1) % 4u);
-        h->added = t0;
-        return DIPS_OK;
+        return compat_resume_impl(h, width, height, start_rgba, halo, t0, (h->p.flags & DIPS_FLAG_DEVICE_PTRS) != 0);
     });
 }
 

@@ -132,6 +132,9 @@ dips_status flush_pending(dips_handle* h);
 dips_status run_series_device(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* frames,
                               uint32_t n_frames, const uint8_t* ref0, dips_series_entry* series, uint8_t* map,
                               hipStream_t s);
+// dips_compat_resume with the pointer kind given (compat_abi.hip)
+dips_status compat_resume_impl(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* start_rgba,
+                               const uint8_t* halo, uint64_t t0, bool dev);
 // the series of HOST frames through the pinned, side-stream feed
 // (series_abi.hip); `ref_dev` a device reference of the first frame or NULL
 dips_status run_series_streamed(dips_handle* h, uint32_t width, uint32_t height, const uint8_t* host_frames,

@@ -892,6 +892,87 @@ dips_status dips_diff_series_sharded(dips_handle* h, dips_comm* comm, uint32_t w
     });
 }
 
+dips_status dips_frame_callback_batch_sharded(dips_handle* h, dips_comm* comm, uint32_t width, uint32_t height,
+                                              const uint8_t* frames, uint32_t n_local, uint64_t n_total,
+                                              uint8_t* out) {
+    return guard(h, [&]() -> dips_status {
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        if (!comm) return fail(h, DIPS_ERR_INVALID, "compat sharded: null communicator");
+        if (comm->device != h->device) return fail(h, DIPS_ERR_INVALID, "compat sharded: device mismatch");
+        if (width == 0 || height == 0) return fail(h, DIPS_ERR_INVALID, "compat sharded: empty frame shape");
+        const int G = comm->nranks, r = comm->rank;
+        // the layout rule, checked for every rank on every rank (the same
+        // answer everywhere: no rank is left in a collective)
+        for (int k = 0; k < G; ++k) {
+            uint64_t f = 0, c = 0;
+            shard_range(n_total, G, k, &f, &c);
+            if (k > 0 && f < 7)
+                return fail(h, DIPS_ERR_INVALID, "compat sharded: rank " + std::to_string(k) + " would start at frame " +
+                                                     std::to_string(f) + " (< 7; n_total >= 7 * nranks suffices)");
+            if (k + 1 < G && c < 3) return fail(h, DIPS_ERR_INVALID, "compat sharded: every rank but the last needs >= 3 frames");
+        }
+        uint64_t first = 0, count = 0;
+        shard_range(n_total, G, r, &first, &count);
+        if ((uint64_t)n_local != count)
+            return fail(h, DIPS_ERR_INVALID, "compat sharded: rank " + std::to_string(r) + " owns " +
+                                                 std::to_string(count) + " frames, n_local is " + std::to_string(n_local));
+        if (n_local == 0) return DIPS_OK;
+        if (!frames || !out) return fail(h, DIPS_ERR_INVALID, "compat sharded: null frames or output");
+        if (h->added != 0 || h->main_init)
+            return fail(h, DIPS_ERR_STATE, "compat sharded: the handle must be fresh (no frame added yet)");
+        if (G == 1) return dips_frame_callback_batch(h, width, height, frames, n_local, out);
+        const size_t fb = (size_t)width * height * 4u;
+        const uint32_t n = n_local;
+        const bool dev = (h->p.flags & DIPS_FLAG_DEVICE_PTRS) != 0;
+        const bool halo_in = r > 0, send_out = r + 1 < G;
+        hipStream_t s = h->stream;
+        st = ensure_comm_stream(h);
+        if (st != DIPS_OK) return st;
+
+        // 1. the 3-frame halo: this rank's last three frames to r+1, r-1's
+        // into shard_halo, on the side stream
+        const uint8_t* send3 = nullptr;
+        if (send_out) {
+            send3 = frames + (size_t)(n - 3) * fb;
+            if (!dev) {
+                DIPS_HIP(h, h->shard_send_frame.ensure(3 * fb));
+                DIPS_HIP(h, hipMemcpyAsync(h->shard_send_frame.p, send3, 3 * fb, hipMemcpyHostToDevice, s));
+                send3 = h->shard_send_frame.as<uint8_t>();
+            }
+        }
+        if (halo_in) DIPS_HIP(h, h->shard_halo.ensure(3 * fb));
+        DIPS_HIP(h, hipEventRecord(h->shard_ev_in, s));
+        DIPS_HIP(h, hipStreamWaitEvent(h->comm_stream, h->shard_ev_in, 0));
+        DIPS_COMM(h, comm, comm->exchange(send3, send_out ? r + 1 : -1, halo_in ? h->shard_halo.p : nullptr,
+                                          halo_in ? r - 1 : -1, 3 * fb, h->comm_stream));
+        DIPS_HIP(h, hipEventRecord(h->shard_ev_halo, h->comm_stream));
+        // the communicator's next operation (the broadcast) after this one on
+        // every rank, and the sent frames unchanged until it is done
+        DIPS_HIP(h, hipStreamWaitEvent(s, h->shard_ev_halo, 0));
+
+        // 2. the start texture from rank 0, which builds it on frames 0..3
+        if (r == 0) {
+            st = dips_frame_callback_batch(h, width, height, frames, n < 4 ? n : 4u, out);
+            if (st != DIPS_OK) return st;
+        } else {
+            DIPS_HIP(h, h->shard_ref.ensure(fb));
+        }
+        DIPS_HIP(h, h->start.ensure(fb));
+        DIPS_COMM(h, comm, comm->broadcast(r == 0 ? h->start.p : nullptr, r == 0 ? h->start.p : h->shard_ref.p, fb, 0, s));
+
+        // 3. the rank's frames: rank 0 goes on from frame 4, the others
+        // resume at their first frame from S and the halo
+        if (r == 0) {
+            if (n > 4) return dips_frame_callback_batch(h, width, height, frames + 4 * fb, n - 4, out + 4 * fb);
+            return DIPS_OK;
+        }
+        st = compat_resume_impl(h, width, height, h->shard_ref.as<uint8_t>(), h->shard_halo.as<uint8_t>(), first, true);
+        if (st != DIPS_OK) return st;
+        return dips_frame_callback_batch(h, width, height, frames, n, out);
+    });
+}
+
 dips_status dips_shard_plan(dips_handle* h, const dips_comm* comm, uint32_t width, uint32_t height,
                             uint64_t n_total, uint64_t* first, uint32_t* count, uint64_t* waves,
                             uint64_t* waves_uncapped) {

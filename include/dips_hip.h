@@ -438,6 +438,23 @@ dips_status dips_shard_plan(dips_handle *h, const dips_comm *comm, uint32_t widt
                             uint64_t n_total, uint64_t *first, uint32_t *count, uint64_t *waves,
                             uint64_t *waves_uncapped);
 
+/* The dips-compat ComputeState over frame ranges ("dips-compat
+ * T=4 needs a 3-frame halo"): consecutive frame_callback calls of global
+ * frames [first, first + n_local) (this rank's dips_shard_range of n_total)
+ * on a FRESH handle of every rank, the outputs those frames get from one
+ * ComputeState that saw every frame (dips/src/lib.rs:233-246,
+ * dips/src/gpu/mod.rs:170-397).  Rank 0 runs frames 0..3 (passthrough, then
+ * the start texture) and broadcasts the start texture; rank r sends its last
+ * three frames to rank r+1 and resumes (dips_compat_resume) from the start
+ * texture and the three frames it receives.  Every rank after the first must
+ * start at global frame >= 7 and every rank but the last own >= 3 frames
+ * (n_total >= 7 * nranks suffices); the check is the same on every rank.
+ * out: n_local RGBA8 frames on this rank (no gather: the outputs are frames,
+ * each rank's muxer takes its own).  Pointers as dips_frame_callback_batch. */
+dips_status dips_frame_callback_batch_sharded(dips_handle *h, dips_comm *comm, uint32_t width, uint32_t height,
+                                              const uint8_t *frames, uint32_t n_local, uint64_t n_total,
+                                              uint8_t *out);
+
 /* Copy the reference the last sharded call used for this rank's first frame
  * (the received halo, the broadcast reference, or rank 0's own) into `out`
  * (width*height*C bytes; device pointer with DIPS_FLAG_DEVICE_PTRS).

@@ -208,6 +208,9 @@ extern "C" {
                                     frames: *const u8, n_local: u32, n_total: u64, reference: *const u8,
                                     shard_flags: u32, series_local: *mut DipsSeriesEntry,
                                     series_all: *mut DipsSeriesEntry) -> DipsStatus;
+    pub fn dips_frame_callback_batch_sharded(h: *mut DipsHandle, comm: *mut DipsComm, width: u32, height: u32,
+                                             frames: *const u8, n_local: u32, n_total: u64, out: *mut u8)
+                                             -> DipsStatus;
     pub fn dips_shard_plan(h: *mut DipsHandle, comm: *const DipsComm, width: u32, height: u32, n_total: u64,
                            first: *mut u64, count: *mut u32, waves: *mut u64, waves_uncapped: *mut u64)
                            -> DipsStatus;

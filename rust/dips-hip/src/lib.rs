@@ -286,6 +286,29 @@ impl ComputeState {
         }
     }
 
+    /// `frame_callback` over this rank's frames of a video sharded by frame
+    /// range over `comm` (a fresh ComputeState on every rank): the outputs
+    /// one ComputeState over all `n_total` frames gives them; the library
+    /// broadcasts the start texture and passes each rank's last three frames
+    /// to the next (every rank after the first starts at frame >= 7).
+    pub fn frame_callback_batch_sharded(&mut self, comm: &mut Comm, width: u32, height: u32, frames: &[u8],
+                                        n_total: u64, out: &mut [u8]) -> Result<(), DipsError> {
+        let fb = width as usize * height as usize * 4;
+        if fb == 0 || frames.len() % fb != 0 || out.len() < frames.len() {
+            return Err(DipsError { status: ffi::DIPS_ERR_INVALID, message: "frames/out not n RGBA8 frames".into() });
+        }
+        let n = frame_count(frames.len() / fb)?;
+        // SAFETY: sizes checked above; the call is collective over `comm`.
+        let st = unsafe {
+            ffi::dips_frame_callback_batch_sharded(self.h.as_ptr(), comm.c.as_ptr(), width, height, frames.as_ptr(),
+                                                   n, n_total, out.as_mut_ptr())
+        };
+        check(st, self.h.as_ptr())?;
+        self.width = width;
+        self.height = height;
+        Ok(())
+    }
+
     /// Continue as if frame_callback had seen frames 0..t0-1 (t0 >= 7): the
     /// start texture of the process that saw frames 0..3 and the raw frames
     /// t0-3..t0-1 (frame-range sharding, one decoder per GPU).

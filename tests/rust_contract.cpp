@@ -161,6 +161,10 @@ struct ComputeState {
         return Result<int>::Ok(0);
     }
 
+    Result<int> frame_callback_batch_sharded(struct Comm& comm, uint32_t w, uint32_t hh,
+                                             const std::vector<uint8_t>& frames, uint64_t n_total,
+                                             std::vector<uint8_t>& out);
+
     std::optional<std::vector<double>> callback_phases() const {
         std::vector<double> v(DIPS_CALLBACK_PHASES);
         uint32_t n = 0;
@@ -274,6 +278,22 @@ struct Comm {
         return R::Ok(out);
     }
 };
+
+// lib.rs `ComputeState::frame_callback_batch_sharded`
+Result<int> ComputeState::frame_callback_batch_sharded(Comm& comm, uint32_t w, uint32_t hh,
+                                                       const std::vector<uint8_t>& frames, uint64_t n_total,
+                                                       std::vector<uint8_t>& out) {
+    const size_t fb = (size_t)w * hh * 4;
+    if (fb == 0 || frames.size() % fb != 0 || out.size() < frames.size())
+        return Result<int>::Err({DIPS_ERR_INVALID, "frames/out not n RGBA8 frames"});
+    auto c = check(dips_frame_callback_batch_sharded(h, comm.c, w, hh, frames.data(), (uint32_t)(frames.size() / fb),
+                                                     n_total, out.data()),
+                   h);
+    if (!c.ok) return c;
+    width = w;
+    height = hh;
+    return Result<int>::Ok(0);
+}
 
 // lib.rs `shard_range`
 Result<std::pair<uint64_t, uint32_t>> shard_range(uint64_t n_total, int nranks, int rank) {
@@ -629,6 +649,55 @@ void device_rows() {
         }
     }
     delete ds.value;
+
+    {
+        // ComputeState::frame_callback_batch_sharded over 2 loopback ranks
+        // (fresh handles) == one ComputeState's frame_callback_batch; a
+        // layout with a rank starting before frame 7 is refused on every rank
+        const uint32_t n_total = 16;
+        std::vector<uint8_t> all;
+        for (uint32_t t = 0; t < n_total; ++t) {
+            auto f = frame_rgba(W, H, 200 + t);
+            all.insert(all.end(), f.begin(), f.end());
+        }
+        const size_t fb = (size_t)W * H * 4;
+        auto one = ComputeState::on_device(true, 1, 5.0f, DIPS_FILTER_SIGMOID, DIPS_CHROMA_NONE, 0);
+        std::vector<uint8_t> want(all.size());
+        bool ok = one.ok && one.value->frame_callback_batch(W, H, all, want).ok;
+        if (one.ok) delete one.value;
+        auto comms = Comm::loopback(2, 0);
+        ok = ok && comms.ok;
+        std::vector<std::vector<uint8_t>> outs(2);
+        std::vector<int> good(2, 0);
+        if (ok) {
+            std::vector<std::thread> th;
+            for (int r = 0; r < 2; ++r)
+                th.emplace_back([&, r]() {
+                    auto cs = ComputeState::on_device(true, 1, 5.0f, DIPS_FILTER_SIGMOID, DIPS_CHROMA_NONE, 0);
+                    if (!cs.ok) return;
+                    auto range = shard_range(n_total, 2, r);
+                    std::vector<uint8_t> mine(all.begin() + range.value.first * fb,
+                                              all.begin() + (range.value.first + range.value.second) * fb);
+                    outs[r].resize(mine.size());
+                    good[r] = cs.value->frame_callback_batch_sharded(*comms.value[r], W, H, mine, n_total, outs[r]).ok;
+                    delete cs.value;
+                });
+            for (auto& t : th) t.join();
+        }
+        std::vector<uint8_t> got = outs[0];
+        got.insert(got.end(), outs[1].begin(), outs[1].end());
+        row("frame_callback_batch_sharded", ok && good[0] && good[1] && got == want);
+        if (comms.ok) {
+            auto cs = ComputeState::on_device(false, 1, 5.0f, DIPS_FILTER_UNFILTERED, DIPS_CHROMA_NONE, 0);
+            std::vector<uint8_t> few(all.begin(), all.begin() + 6 * fb), o(few.size());
+            auto bad = cs.ok ? cs.value->frame_callback_batch_sharded(*comms.value[0], W, H, few, 12, o)
+                             : Result<int>::Err({0, ""});
+            row("frame_callback_batch_sharded_layout", !bad.ok && bad.err.status == DIPS_ERR_INVALID &&
+                                                           has(bad.err.message, "< 7"));
+            if (cs.ok) delete cs.value;
+            for (auto* c : comms.value) delete c;
+        }
+    }
 
     // DiPsCompute: (rows, cols) -> dips_alt_create(cols, rows); a wrong frame
     // length is an error, not a panic inside the library

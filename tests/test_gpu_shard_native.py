@@ -326,3 +326,88 @@ def test_sharded_argument_errors():
         op.close()
         for c in comms:
             c.close()
+
+
+# -- the dips-compat ComputeState over frame ranges ----------
+def _compat_loopback(world, n_total, w, h, props, device_ptrs):
+    import torch
+    from dips_amd import ComputeState
+    from dips_amd.comm import Comm, shard_range
+    frames = np.random.default_rng(world * 100 + n_total).integers(0, 256, (n_total, h, w, 4), dtype=np.uint8)
+    comms = Comm.loopback(world, 0)
+    states = [ComputeState(*props) for _ in range(world)]
+    outs, errors = [None] * world, []
+    try:
+        ranges = [shard_range(n_total, world, r) for r in range(world)]
+        if device_ptrs:
+            dev_in = [torch.from_numpy(frames[s:e].copy()).cuda() for s, e in ranges]
+            dev_out = [torch.empty_like(t) for t in dev_in]
+            torch.cuda.synchronize()
+
+        def rank(r):
+            try:
+                s, e = ranges[r]
+                if device_ptrs:
+                    states[r].frame_callback_batch_sharded_device(comms[r], dev_in[r], dev_out[r], n_total)
+                else:
+                    outs[r] = states[r].frame_callback_batch_sharded(comms[r], w, h, frames[s:e], n_total)
+            except Exception as ex:  # reported below
+                errors.append((r, repr(ex)))
+
+        threads = [threading.Thread(target=rank, args=(r,)) for r in range(world)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=180)
+        assert not any(t.is_alive() for t in threads) and not errors, errors
+        if device_ptrs:
+            torch.cuda.synchronize()
+            outs = [o.cpu().numpy() for o in dev_out]
+        return frames, np.concatenate(outs)
+    finally:
+        for c in states:
+            c.close()
+        for c in comms:
+            c.close()
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 19), (3, 31)])
+@pytest.mark.parametrize("window", [1, 3])
+@pytest.mark.parametrize("device_ptrs", [False, True])
+def test_compat_sharded_equals_one_compute_state(world, n_total, window, device_ptrs):
+    """dips_frame_callback_batch_sharded over loopback ranks (fresh
+    ComputeStates) gives every frame the output one ComputeState over the
+    whole clip gives it, which the oracle's frame_callback pins."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+    w, h = 48, 32
+    props = (True, window, 5.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+    frames, got = _compat_loopback(world, n_total, w, h, props, device_ptrs)
+    one = ComputeState(*props)
+    try:
+        want = one.frame_callback_batch(w, h, frames)
+    finally:
+        one.close()
+    assert np.array_equal(got, want)
+    cs = oracle.ComputeState(True, window, 5.0, 0, 0)
+    ref = np.stack([oracle.frame_callback(w, h, f, cs) for f in frames])
+    assert np.array_equal(got, ref)
+
+
+def test_compat_sharded_layout_refused_everywhere():
+    """A layout where a rank would start before frame 7 is refused on every
+    rank with the same message (no rank is left in a collective)."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter, DipsError
+    from dips_amd.comm import Comm
+    comms = Comm.loopback(2, 0)
+    states = [ComputeState(False, 1, 5.0, DiPsFilter.Unfiltered, ChromaFilter.None_) for _ in range(2)]
+    try:
+        fr = np.zeros((6, 16, 16, 4), dtype=np.uint8)
+        for r in range(2):
+            with pytest.raises(DipsError) as ei:
+                states[r].frame_callback_batch_sharded(comms[r], 16, 16, fr, 12)
+            assert "< 7" in str(ei.value)
+    finally:
+        for c in states:
+            c.close()
+        for c in comms:
+            c.close()

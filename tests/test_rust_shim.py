@@ -307,6 +307,8 @@ METHOD_TABLE = [
     ("pub fn try_start_texture(", "dips_start_texture", "check(r, self.h.as_ptr())?", ["try_start_texture"]),
     ("pub fn start_texture(", "dips_start_texture", "panic!", ["start_texture"]),
     ("pub fn resume(", "dips_compat_resume", "check(st, self.h.as_ptr())?", ["resume"]),
+    ("pub fn frame_callback_batch_sharded(", "dips_frame_callback_batch_sharded", "check(st, self.h.as_ptr())?",
+     ["frame_callback_batch_sharded"]),
     ("pub fn frame_callback(width: u32", "dips_frame_callback", "panic!", ["frame_callback_panics"]),
     ("pub fn run(&mut self, width: u32", "dips_diff_series", "check(st, self.h.as_ptr())?",
      ["diff_series_run", "diff_series_refusals"]),
