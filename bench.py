@@ -769,12 +769,30 @@ def _per_frame_call(torch, n_timed: int, warm: int = 8):
 _WHO = {"rank": os.environ.get("RANK", "0"), "local": os.environ.get("LOCAL_RANK", "0"), "bus": None}
 
 
+# The JSON line goes to the process's real stdout; everything else written to
+# fd 1 -- RCCL prints its version banner there when a communicator is made --
+# goes to stderr, so that rank 0's stdout holds the one line and nothing else.
+_LINE_FD = None
+
+
+def _stdout_for_the_line_only():
+    global _LINE_FD
+    sys.stdout.flush()
+    _LINE_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def _emit_line(text: str) -> None:
+    os.write(_LINE_FD if _LINE_FD is not None else 1, (text + "\n").encode())
+
+
 def main():
     """Run the bench; any exception on any rank ends THIS process with a
     non-zero status after naming the rank and its device's PCI bus id (a rank
     left waiting in a collective fails at the process group's timeout,
     --dist-timeout, instead of hanging until the driver's limit)."""
     args = parse()
+    _stdout_for_the_line_only()
     try:
         _main(args)
     except SystemExit:
@@ -1162,7 +1180,7 @@ def _main(args):
             "per_frame_call": pfc,
             **legs,
         }
-        print(json.dumps(out), flush=True)
+        _emit_line(json.dumps(out))
     if op is not None:
         op.close()
     if comm is not None:

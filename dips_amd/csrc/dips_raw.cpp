@@ -218,8 +218,16 @@ int run_sharded(int argc, char** argv) {
     const uint64_t n_total = in.n / fb;
     const bool rccl = transport == "rccl";
     std::vector<dips_comm*> comms(ranks, nullptr);
+    // RCCL prints its version banner to stdout when a communicator is made:
+    // send it to stderr, stdout carries the CSV only
+    std::fflush(stdout);
+    const int saved_stdout = dup(1);
+    dup2(2, 1);
     int st = rccl ? dips_comm_create_all((int)ranks, nullptr, comms.data())  // rank r on device r
                   : dips_comm_create_loopback((int)ranks, 0, comms.data());
+    std::fflush(stdout);
+    dup2(saved_stdout, 1);
+    close(saved_stdout);
     if (st != DIPS_OK) {
         std::fprintf(stderr, "dips_raw: %s failed (%d): %s\n", rccl ? "dips_comm_create_all" : "dips_comm_create_loopback",
                      st, dips_comm_last_error(nullptr));
