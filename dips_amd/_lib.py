@@ -209,6 +209,7 @@ def load() -> ctypes.CDLL:
             "dips_alt_send_frame": ([_vp, _u8p, ctypes.c_size_t, st, _u8p, ctypes.c_size_t], st),
             "dips_alt_send_frames": ([_vp, _u8p, u32, _u8p, _u8p], st),
             "dips_alt_run": ([_vp, _u8p, u32, _vp, u32, _u8p], st),
+            "dips_alt_run_sharded": ([_vp, _vp, _u8p, u32, u64, _vp, u32, _u8p], st),
             "dips_alt_snapshot_texture": ([_vp, _u8p, ctypes.c_size_t], st),
             "dips_alt_kernel_time": ([_vp, P(ctypes.c_double), P(u64)], st),
             "dips_alt_kernel_time_reset": ([_vp], st),

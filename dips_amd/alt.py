@@ -263,6 +263,41 @@ class DiPsRunner:
                                     int(self.markers.size), out.ctypes.data))
         return out
 
+    def run_sharded(self, comm, frames, n_total: int) -> np.ndarray:
+        """This rank's part of one loop over an `n_total`-frame video split
+        by frame range over `comm` (a dips_amd.comm.Comm; dips_alt_run_sharded):
+        `frames` are the rank's frames [first, first + count) of
+        comm.shard_range, the result is what the single loop gives them.  The
+        runner must be fresh (no frame sent yet) on every rank."""
+        c = self.compute
+        a = _frames_u8(frames, c.rows, c.cols)
+        out = np.empty_like(a)
+        h = c._host
+        h.check(h._lib.dips_alt_run_sharded(h.ptr, comm.ptr, a.ctypes.data, a.shape[0], int(n_total),
+                                            self.markers.ctypes.data if self.markers.size else None,
+                                            int(self.markers.size), out.ctypes.data))
+        return out
+
+    def run_sharded_device(self, comm, frames, out, n_total: int, stream=None) -> None:
+        """run_sharded on HBM-resident frames (torch uint8 [count, rows,
+        cols, 4] on the communicator's device), on the tensor's current
+        stream; returns once `out` is written."""
+        c = self.compute
+        n = int(frames.shape[0])
+        if tuple(frames.shape) != (n, c.rows, c.cols, 4) or tuple(out.shape) != tuple(frames.shape):
+            raise ValueError("frames/out must be [N, rows, cols, 4] uint8 tensors")
+        for t in (frames, out):
+            if not t.is_cuda or not t.is_contiguous():
+                raise ValueError("device path needs contiguous HIP tensors")
+        hd = c._device_handle()
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(frames.device).cuda_stream
+        with _lib.on_stream(hd._lib.dips_alt_set_stream, hd.ptr, hd.check, stream):
+            hd.check(hd._lib.dips_alt_run_sharded(hd.ptr, comm.ptr, frames.data_ptr(), n, int(n_total),
+                                                  self.markers.ctypes.data if self.markers.size else None,
+                                                  int(self.markers.size), out.data_ptr()))
+
     def close(self) -> None:
         self.compute.close()
 

@@ -19,6 +19,7 @@
 
 #include "../../include/dips_hip.h"
 #include "abi_guard.h"
+#include "comm.h"
 #include "alt_lut.h"
 #include "dips_kernels.h"
 #include "host_buffers.h"
@@ -162,6 +163,10 @@ struct dips_alt_handle {
     uint32_t lut_filter = 0, lut_col = 0;
     float lut_k = 0.0f;
     DevBuf filtered;        // W > 1 batch: filtered f32 intensities of a chunk of frames (+ the one before)
+    // the sharded run loop (dips_alt_run_sharded): frames received from
+    // other ranks, the replay sequence built from them, its discarded
+    // outputs, and the staging of a host frame this rank sends
+    DevBuf shard_recv, shard_replay, shard_scratch, shard_stage;
 
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
     std::vector<hipEvent_t> ev_free;
@@ -628,6 +633,10 @@ void dips_alt_destroy(dips_alt_handle* h) {
         h->io_out.release();
         h->meta.release();
         h->io.release();
+        h->shard_recv.release();
+        h->shard_replay.release();
+        h->shard_scratch.release();
+        h->shard_stage.release();
         if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
         delete h;
     });
@@ -813,6 +822,160 @@ dips_status dips_alt_run(dips_alt_handle* h, const uint8_t* frames, uint32_t n, 
                 }
         }
         return dips_alt_send_frames(h, frames, n, flags.data(), out);
+    });
+}
+
+dips_status dips_alt_run_sharded(dips_alt_handle* h, dips_comm* comm, const uint8_t* frames, uint32_t n_local,
+                                 uint64_t n_total, const uint64_t* markers, uint32_t n_markers, uint8_t* out) {
+    return guard(h, [&]() -> dips_status {
+        dips_status st = bind(h);
+        if (st != DIPS_OK) return st;
+        if (!comm) return fail(h, DIPS_ERR_INVALID, "alt sharded: null communicator");
+        if (comm->device != h->device) return fail(h, DIPS_ERR_INVALID, "alt sharded: device mismatch");
+        if (n_markers && !markers) return fail(h, DIPS_ERR_INVALID, "alt sharded: null refresh markers");
+        if (n_total >= (1ull << 32)) return fail(h, DIPS_ERR_INVALID, "alt sharded: 2^32 frames or more");
+        const int G = comm->nranks, r = comm->rank;
+        const uint64_t N = h->p.num_textures;
+        auto range = [&](int k, uint64_t* f, uint64_t* c) {
+            const unsigned __int128 nt = n_total;
+            *f = (uint64_t)(nt * (unsigned)k / (unsigned)G);
+            *c = (uint64_t)(nt * (unsigned)(k + 1) / (unsigned)G) - *f;
+        };
+        uint64_t first = 0, count = 0;
+        range(r, &first, &count);
+        if ((uint64_t)n_local != count)
+            return fail(h, DIPS_ERR_INVALID, "alt sharded: rank " + std::to_string(r) + " owns " +
+                                                 std::to_string(count) + " frames, n_local is " + std::to_string(n_local));
+        if (count && (!frames || !out)) return fail(h, DIPS_ERR_INVALID, "alt sharded: null frames or output");
+        if (h->sent != 0 || h->overall != 0)
+            return fail(h, DIPS_ERR_STATE, "alt sharded: the handle must be fresh (no frame sent yet)");
+
+        // the run_dips_on_file loop over every frame (lib.rs:588-683, as
+        // dips_alt_run): the snapshot flags, and the loop state after this
+        // rank's last frame
+        std::vector<uint8_t> flags((size_t)n_total);
+        uint64_t index = 0, overall = 0, end_index = 0, end_overall = 0;
+        for (uint64_t t = 0; t < n_total; ++t) {
+            flags[t] = index == kFrameCount ? 1 : 0;
+            if (index <= kFrameCount) index += 1;
+            overall += 1;
+            for (uint32_t k = 0; k < n_markers; ++k)
+                if (markers[k] == overall) {
+                    index = 0;
+                    break;
+                }
+            if (t + 1 == first + count) {
+                end_index = index;
+                end_overall = overall;
+            }
+        }
+        // what rank k replays through its fresh operator before its own
+        // frames: the source frames of the last snapshot before its first
+        // frame t0 (that one flagged), then its halo, the min(N, t0) frames
+        // before t0 -- the slots and the snapshot texture as the single loop
+        // has them at frame t0.  With t0 < N the single loop still holds
+        // N - t0 never-written (zero) slots, the oldest; after a snapshot
+        // replay that many zero frames (kZeroFrame) go before the halo.
+        constexpr uint64_t kZeroFrame = ~0ull;
+        auto replay_of = [&](int k) {
+            std::vector<std::pair<uint64_t, uint8_t>> rp;
+            uint64_t t0 = 0, c = 0;
+            range(k, &t0, &c);
+            if (t0 == 0 || c == 0) return rp;
+            for (uint64_t sf = t0; sf-- > 0;) {
+                if (flags[sf]) {
+                    for (uint64_t g = sf + 1 > N ? sf + 1 - N : 0; g <= sf; ++g) rp.emplace_back(g, g == sf ? 1 : 0);
+                    break;
+                }
+            }
+            const uint64_t halo = std::min<uint64_t>(N, t0);
+            if (!rp.empty())
+                for (uint64_t z = halo; z < N; ++z) rp.emplace_back(kZeroFrame, 0);
+            for (uint64_t g = t0 - halo; g < t0; ++g) rp.emplace_back(g, 0);
+            return rp;
+        };
+        auto distinct = [&](const std::vector<std::pair<uint64_t, uint8_t>>& rp) {
+            std::vector<uint64_t> v;
+            for (auto& e : rp)
+                if (e.first != kZeroFrame) v.push_back(e.first);
+            std::sort(v.begin(), v.end());
+            v.erase(std::unique(v.begin(), v.end()), v.end());
+            return v;
+        };
+        auto owner = [&](uint64_t g) {
+            int k = (int)((unsigned __int128)g * (unsigned)G / n_total);  // first guess, then adjust
+            uint64_t f = 0, c = 0;
+            for (;;) {
+                range(k, &f, &c);
+                if (g < f) --k;
+                else if (g >= f + c) ++k;
+                else return k;
+            }
+        };
+        const size_t fb = h->frame_bytes();
+        const bool dev = (h->p.flags & DIPS_FLAG_DEVICE_PTRS) != 0;
+        hipStream_t s = h->stream;
+
+        // every (frame, owner, destination) transfer, in one order on every
+        // rank; each rank takes part in each exchange (the loopback meets
+        // all ranks), passing -1 where it neither sends nor receives
+        const auto mine = replay_of(r);
+        const std::vector<uint64_t> want = distinct(mine);  // the frames this rank receives
+        if (!want.empty()) ALT_HIP(h, h->shard_recv.ensure(want.size() * fb));
+        if (!dev) ALT_HIP(h, h->shard_stage.ensure(fb));
+        for (int k = 1; k < G; ++k) {
+            for (uint64_t g : distinct(replay_of(k))) {
+                const int o = owner(g);
+                if (o == k) continue;  // (never: replayed frames precede the rank's own)
+                const void* send = nullptr;
+                void* recv = nullptr;
+                if (r == o) {
+                    const uint8_t* src = frames + (size_t)(g - first) * fb;
+                    if (!dev) {
+                        ALT_HIP(h, hipMemcpyAsync(h->shard_stage.p, src, fb, hipMemcpyHostToDevice, s));
+                        src = static_cast<const uint8_t*>(h->shard_stage.p);
+                    }
+                    send = src;
+                }
+                if (r == k)
+                    recv = h->shard_recv.as<uint8_t>() +
+                           (size_t)(std::lower_bound(want.begin(), want.end(), g) - want.begin()) * fb;
+                const dips_status cs = comm->exchange(send, r == o ? k : -1, recv, r == k ? o : -1, fb, s);
+                if (cs != DIPS_OK)
+                    return fail(h, cs, "alt sharded: communicator (rank " + std::to_string(r) + "): " + comm->err);
+            }
+        }
+
+        // replay (outputs discarded), then this rank's frames with its flags
+        if (!mine.empty()) {
+            ALT_HIP(h, h->shard_replay.ensure(mine.size() * fb));
+            ALT_HIP(h, h->shard_scratch.ensure(mine.size() * fb));
+            std::vector<uint8_t> rflags(mine.size());
+            for (size_t i = 0; i < mine.size(); ++i) {
+                uint8_t* dst = h->shard_replay.as<uint8_t>() + i * fb;
+                if (mine[i].first == kZeroFrame) {
+                    ALT_HIP(h, hipMemsetAsync(dst, 0, fb, s));
+                } else {
+                    const size_t at =
+                        (size_t)(std::lower_bound(want.begin(), want.end(), mine[i].first) - want.begin());
+                    ALT_HIP(h, hipMemcpyAsync(dst, h->shard_recv.as<uint8_t>() + at * fb, fb,
+                                              hipMemcpyDeviceToDevice, s));
+                }
+                rflags[i] = mine[i].second;
+            }
+            st = send_frames_device(h, h->shard_replay.as<uint8_t>(), (uint32_t)mine.size(), rflags.data(),
+                                    h->shard_scratch.as<uint8_t>(), s);
+            if (st != DIPS_OK) return st;
+        }
+        if (count) {
+            st = dev ? send_frames_device(h, frames, (uint32_t)count, flags.data() + first, out, s)
+                     : dips_alt_send_frames(h, frames, (uint32_t)count, flags.data() + first, out);
+            if (st != DIPS_OK) return st;
+        }
+        h->index = end_index;  // the loop state of the single loop after this rank's last frame
+        h->overall = end_overall;
+        if (dev) ALT_HIP(h, hipStreamSynchronize(s));  // synchronous in both pointer modes
+        return DIPS_OK;
     });
 }
 

@@ -538,6 +538,18 @@ dips_status dips_alt_send_frames(dips_alt_handle *h, const uint8_t *frames, uint
 dips_status dips_alt_run(dips_alt_handle *h, const uint8_t *frames, uint32_t n_frames,
                          const uint64_t *refresh_markers, uint32_t n_markers, uint8_t *out);
 
+/* The dips_alt run loop over frame ranges: this rank's frames [first,
+ * first + n_local) of an n_total-frame video (its dips_shard_range), on a
+ * FRESH handle of every rank, with the outputs one run_dips_on_file loop over
+ * every frame gives them (the same refresh markers on every rank).  Rank r
+ * replays, outputs discarded, the source frames of the last snapshot before
+ * its first frame and the num_textures frames before it (fewer, after zero
+ * frames, near the start), fetched point to point from the ranks that own
+ * them, then runs its own frames; any split, ranks with no frame included.
+ * Pointers as dips_alt_send_frames; synchronous. */
+dips_status dips_alt_run_sharded(dips_alt_handle *h, dips_comm *comm, const uint8_t *frames, uint32_t n_local,
+                                 uint64_t n_total, const uint64_t *refresh_markers, uint32_t n_markers, uint8_t *out);
+
 /* Copy the snapshot texture's .r channel (width*height bytes, host). */
 dips_status dips_alt_snapshot_texture(dips_alt_handle *h, uint8_t *out_gray, size_t cap);
 

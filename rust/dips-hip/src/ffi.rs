@@ -230,6 +230,9 @@ extern "C" {
                                 snapshot_flags: *const u8, out: *mut u8) -> DipsStatus;
     pub fn dips_alt_run(h: *mut DipsAltHandle, frames: *const u8, n_frames: u32, refresh_markers: *const u64,
                         n_markers: u32, out: *mut u8) -> DipsStatus;
+    pub fn dips_alt_run_sharded(h: *mut DipsAltHandle, comm: *mut DipsComm, frames: *const u8, n_local: u32,
+                                n_total: u64, refresh_markers: *const u64, n_markers: u32, out: *mut u8)
+                                -> DipsStatus;
     pub fn dips_alt_snapshot_texture(h: *mut DipsAltHandle, out_gray: *mut u8, cap: usize) -> DipsStatus;
     pub fn dips_alt_kernel_time(h: *mut DipsAltHandle, total_ms: *mut f64, launches: *mut u64) -> DipsStatus;
     pub fn dips_alt_kernel_time_reset(h: *mut DipsAltHandle) -> DipsStatus;

@@ -682,6 +682,27 @@ impl DiPsCompute {
         check_alt(st, self.h.as_ptr())?;
         Ok(())
     }
+
+    /// This rank's frames of one run_dips_on_file loop over an n_total-frame
+    /// video split by frame range over `comm` (shard_range); collective, on
+    /// a fresh DiPsCompute of every rank.
+    pub fn run_sharded(&mut self, comm: &mut Comm, frames: &[u8], n_total: u64, refresh_markers: &[u64],
+                       out: &mut [u8]) -> Result<(), DipsError> {
+        if self.bytes == 0 || frames.len() % self.bytes != 0 || out.len() < frames.len() {
+            return Err(DipsError { status: ffi::DIPS_ERR_INVALID, message: "frames/out not n frames".into() });
+        }
+        let n = frame_count(frames.len() / self.bytes)?;
+        let n_markers = u32::try_from(refresh_markers.len())
+            .map_err(|_| DipsError { status: ffi::DIPS_ERR_INVALID, message: "too many refresh markers".into() })?;
+        // SAFETY: sizes checked above; the call is collective over `comm`.
+        let st = unsafe {
+            ffi::dips_alt_run_sharded(self.h.as_ptr(), comm.c.as_ptr(), frames.as_ptr(), n, n_total,
+                                      if refresh_markers.is_empty() { ptr::null() } else { refresh_markers.as_ptr() },
+                                      n_markers, out.as_mut_ptr())
+        };
+        check_alt(st, self.h.as_ptr())?;
+        Ok(())
+    }
 }
 
 impl Drop for DiPsCompute {

@@ -411,7 +411,20 @@ struct DiPsCompute {
                                       out.data()),
                          h);
     }
+    // lib.rs `DiPsCompute::run_sharded`
+    Result<int> run_sharded(struct Comm& comm, const std::vector<uint8_t>& frames, uint64_t n_total,
+                            const std::vector<uint64_t>& markers, std::vector<uint8_t>& out);
 };
+
+Result<int> DiPsCompute::run_sharded(Comm& comm, const std::vector<uint8_t>& frames, uint64_t n_total,
+                                     const std::vector<uint64_t>& markers, std::vector<uint8_t>& out) {
+    if (bytes == 0 || frames.size() % bytes != 0 || out.size() < frames.size())
+        return Result<int>::Err({DIPS_ERR_INVALID, "frames/out not n frames"});
+    return check_alt(dips_alt_run_sharded(h, comm.c, frames.data(), (uint32_t)(frames.size() / bytes), n_total,
+                                          markers.empty() ? nullptr : markers.data(), (uint32_t)markers.size(),
+                                          out.data()),
+                     h);
+}
 
 // ---------------------------------------------------------------------------
 int failures = 0;
@@ -718,6 +731,58 @@ void device_rows() {
         auto refused = alt.value->run(fr, {}, small);
         row("dips_compute_run", r.ok && !refused.ok && refused.err.status == DIPS_ERR_INVALID);
         delete alt.value;
+    }
+
+    {
+        // DiPsCompute::run_sharded over 3 loopback ranks (fresh operators,
+        // refresh markers on and across the range edges) == one DiPsCompute's
+        // run over every frame; a wrong frame count is refused
+        const uint32_t n_total = 15, rows = 16, cols = 24;
+        std::vector<uint8_t> all;
+        for (uint32_t t = 0; t < n_total; ++t) {
+            auto f = frame_rgba(cols, rows, 90 + t);
+            all.insert(all.end(), f.begin(), f.end());
+        }
+        const size_t fb = (size_t)rows * cols * 4;
+        const std::vector<uint64_t> markers = {5, 6, 11};
+        auto one = DiPsCompute::create_(2, rows, cols);
+        std::vector<uint8_t> want(all.size());
+        bool ok = one.ok && one.value->run(all, markers, want).ok;
+        if (one.ok) delete one.value;
+        auto comms = Comm::loopback(3, 0);
+        ok = ok && comms.ok;
+        std::vector<std::vector<uint8_t>> outs(3);
+        std::vector<int> good(3, 0);
+        if (ok) {
+            std::vector<std::thread> th;
+            for (int r = 0; r < 3; ++r)
+                th.emplace_back([&, r]() {
+                    auto d = DiPsCompute::create_(2, rows, cols);
+                    if (!d.ok) return;
+                    auto range = shard_range(n_total, 3, r);
+                    std::vector<uint8_t> mine(all.begin() + range.value.first * fb,
+                                              all.begin() + (range.value.first + range.value.second) * fb);
+                    outs[r].resize(mine.size());
+                    good[r] = d.value->run_sharded(*comms.value[r], mine, n_total, markers, outs[r]).ok;
+                    delete d.value;
+                });
+            for (auto& t : th) t.join();
+        }
+        std::vector<uint8_t> got;
+        for (auto& o : outs) got.insert(got.end(), o.begin(), o.end());
+        row("dips_compute_run_sharded", ok && good[0] && good[1] && good[2] && got == want);
+        if (comms.ok) {
+            // rank 0 owns 5 of 15 frames: one frame is refused on that rank
+            // alone, before any exchange
+            auto d = DiPsCompute::create_(2, rows, cols);
+            std::vector<uint8_t> few(all.begin(), all.begin() + fb), o(few.size());
+            auto bad = d.ok ? d.value->run_sharded(*comms.value[0], few, n_total, {}, o) : Result<int>::Err({0, ""});
+            row("dips_compute_run_sharded_error", !bad.ok && bad.err.status == DIPS_ERR_INVALID &&
+                                                      has(bad.err.message, "owns 5 frames, n_local is 1"),
+                bad.ok ? "accepted" : bad.err.message);
+            if (d.ok) delete d.value;
+            for (auto* c : comms.value) delete c;
+        }
     }
 
     // Comm::unique_id + Comm::rccl at one rank (ncclCommInitRank)

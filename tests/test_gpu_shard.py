@@ -243,3 +243,68 @@ def test_native_sharded_over_host_transport(world, mode, host_ptrs):
     finally:
         op.close()
     assert np.array_equal(got, one.cpu().numpy().view(np.uint64))
+
+
+def _alt_frames(n):
+    rng = np.random.default_rng(505)
+    return rng.integers(0, 256, (n, 24, 40, 4), dtype=np.uint8)
+
+
+ALT_MARKERS = [6, 11, 12, 20]
+
+
+def _native_alt_worker(rank, world, port, n_total, host_ptrs, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    runner = comm = None
+    try:
+        from dips_amd.alt import DiPsRunner
+        from dips_amd.comm import Comm, TorchHostTransport, shard_range
+        torch.cuda.set_device(0)
+        s, e = shard_range(n_total, world, rank)
+        frames = _alt_frames(n_total)[s:e]
+        runner = DiPsRunner(24, 40, refresh_markers=ALT_MARKERS)
+        comm = Comm.host(TorchHostTransport(), world, rank, 0)
+        if host_ptrs:
+            out = runner.run_sharded(comm, frames, n_total)
+        else:
+            dev = torch.from_numpy(frames).cuda()
+            o = torch.empty_like(dev)
+            runner.run_sharded_device(comm, dev, o, n_total)
+            out = o.cpu().numpy()
+        result_q.put((rank, out))
+    finally:
+        if runner is not None:
+            runner.close()
+        if comm is not None:
+            comm.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,host_ptrs", [(2, True), (3, False)])
+def test_native_alt_sharded_over_host_transport(world, host_ptrs):
+    """dips_alt_run_sharded in `world` processes over DIPS_COMM_HOST (gloo):
+    the ranks' outputs equal one run_dips_on_file loop over every frame."""
+    from dips_amd.alt import DiPsRunner
+    n_total = 26
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_alt_worker, args=(r, world, port, n_total, host_ptrs, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        parts = dict(q.get(timeout=300) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    frames = _alt_frames(n_total)
+    r = DiPsRunner(24, 40, refresh_markers=ALT_MARKERS)
+    try:
+        want = r(frames)
+    finally:
+        r.close()
+    assert np.array_equal(np.concatenate([parts[k] for k in range(world)]), want)

@@ -327,6 +327,8 @@ METHOD_TABLE = [
     ("pub fn send_frame(", "dips_alt_send_frame", "check_alt(st, self.h.as_ptr())?", ["dips_compute_send_frame"]),
     ("pub fn run(&mut self, frames: &[u8], refresh_markers", "dips_alt_run", "check_alt(st, self.h.as_ptr())?",
      ["dips_compute_run"]),
+    ("pub fn run_sharded(&mut self, comm: &mut Comm, frames", "dips_alt_run_sharded",
+     "check_alt(st, self.h.as_ptr())?", ["dips_compute_run_sharded", "dips_compute_run_sharded_error"]),
 ]
 
 
