@@ -116,3 +116,59 @@ def test_sharded_csv_over_rccl_in_one_process(tmp_path, mode):
     rn = _run(["sharded", src, w, h, "rgb8", "--ranks", 1, "--mode", mode, "--transport", "rccl"])
     assert r1.returncode == 0 and rn.returncode == 0, r1.stderr + rn.stderr
     assert rn.stdout == r1.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,transport", [(2, "loopback"), (3, "loopback"), (1, "rccl")])
+def test_callback_ranks_equal_one_compute_state(tmp_path, ranks, transport):
+    """`dips_raw callback --ranks N`: fresh ComputeStates per rank through
+    dips_frame_callback_batch_sharded write the file one ComputeState writes
+    (and the oracle's frame_callback)."""
+    w, h, n = 48, 32, 23
+    frames = np.random.default_rng(40 + ranks).integers(0, 256, (n, h, w, 4), dtype=np.uint8)
+    src, one, many = tmp_path / "in.rgba", tmp_path / "one.rgba", tmp_path / "many.rgba"
+    frames.tofile(src)
+    common = ["--colorize", "--filter", "sigmoid"]
+    r1 = _run(["callback", src, w, h, one, "--batch", 5] + common)
+    rn = _run(["callback", src, w, h, many, "--ranks", ranks, "--transport", transport] + common)
+    assert r1.returncode == 0 and rn.returncode == 0, r1.stderr + rn.stderr
+    assert one.read_bytes() == many.read_bytes()
+    cs = oracle.ComputeState(True, 1, 5.0, 0, 0)
+    want = np.stack([oracle.frame_callback(w, h, f, cs) for f in frames])
+    assert np.array_equal(np.fromfile(many, dtype=np.uint8).reshape(n, h, w, 4), want)
+
+
+@pytest.mark.gpu
+def test_callback_ranks_layout_refused(tmp_path):
+    w, h, n = 16, 8, 10  # 3 ranks start at 0, 3, 6: before frame 7
+    src = tmp_path / "in.rgba"
+    np.zeros((n, h, w, 4), dtype=np.uint8).tofile(src)
+    r = _run(["callback", src, w, h, tmp_path / "o.rgba", "--ranks", 3])
+    assert r.returncode == 2 and "< 7" in r.stderr, r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,transport", [(0, None), (3, "loopback"), (8, "loopback"), (1, "rccl")])
+def test_alt_file_matches_oracle(tmp_path, ranks, transport):
+    """`dips_raw alt`: the dips_alt run_dips_on_file loop over a raw RGBA8
+    file with refresh markers, on one handle or sharded over N ranks
+    (dips_alt_run_sharded), equals the oracle's loop."""
+    w, h, n, markers = 40, 24, 30, [4, 11, 12, 25]
+    frames = np.random.default_rng(3).integers(0, 256, (n, h, w, 4), dtype=np.uint8)
+    src, dst = tmp_path / "in.rgba", tmp_path / "out.rgba"
+    frames.tofile(src)
+    args = ["alt", src, w, h, dst, "--markers", ",".join(map(str, markers))]
+    if ranks:
+        args += ["--ranks", ranks, "--transport", transport]
+    r = _run(args)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(dst, dtype=np.uint8).reshape(n, h, w, 4)
+    want = oracle.AltCompute(2, w, h, True, 1, 5.0, 0, 0).run(frames, markers)
+    assert np.array_equal(got, want)
+
+
+def test_alt_usage():
+    for bad in (["alt", "x", "8", "4"], ["alt", "x", "8", "4", "o", "--markers", "1,,2"],
+                ["alt", "x", "8", "4", "o", "--transport", "mpi"]):
+        r = _run(bad)
+        assert r.returncode == 1 and "usage" in r.stderr, bad
