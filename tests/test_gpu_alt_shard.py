@@ -49,7 +49,7 @@ def _one_loop(frames, props, markers, n_tex):
         r.close()
 
 
-def _sharded(world, frames, props, markers, n_tex, device_ptrs, keep_last=False):
+def _sharded(world, frames, props, markers, n_tex, device_ptrs, keep_last=False, crosscheck=False):
     """dips_alt_run_sharded on `world` loopback ranks, one thread each;
     returns the concatenated outputs (and the last rank's runner if asked)."""
     import torch
@@ -57,7 +57,7 @@ def _sharded(world, frames, props, markers, n_tex, device_ptrs, keep_last=False)
     from dips_amd.comm import Comm, shard_range
     n, h, w = frames.shape[:3]
     comms = Comm.loopback(world, 0)
-    runners = [DiPsRunner(h, w, props, markers, num_textures=n_tex) for _ in range(world)]
+    runners = [DiPsRunner(h, w, props, markers, num_textures=n_tex, crosscheck=crosscheck) for _ in range(world)]
     outs, errs = [None] * world, [None] * world
 
     def rank(r):
@@ -83,7 +83,7 @@ def _sharded(world, frames, props, markers, n_tex, device_ptrs, keep_last=False)
     try:
         assert not any(t.is_alive() for t in th), "a rank did not return"
         assert errs == [None] * world, errs
-        got = np.concatenate(outs)
+        got = np.concatenate(outs) if n else np.empty((0, h, w, 4), dtype=np.uint8)
         if keep_last:
             last = runners.pop()
             return got, last
@@ -117,6 +117,25 @@ def test_alt_sharded_equals_one_loop(world, n, n_tex, window, markers, device_pt
     assert got.shape == want.shape
     bad = np.argwhere(np.any(got != want, axis=(1, 2, 3)))
     assert bad.size == 0, f"frames differing from the single loop: {bad.ravel()[:8]}"
+
+
+@pytest.mark.parametrize("device_ptrs", [False, True])
+def test_alt_sharded_crosscheck_kernels(device_ptrs):
+    """DIPS_FLAG_CROSSCHECK (the arithmetic epilogue instead of the table,
+    host frames through the pinned buffer) under the sharded call."""
+    w, h, n, markers = 40, 24, 33, [9, 10, 21]
+    frames = _frames(w, h, n, 123)
+    props = _props(1, 1, True, 3)
+    want = _one_loop(frames, props, markers, 2)
+    got = _sharded(3, frames, props, markers, 2, device_ptrs, crosscheck=True)
+    assert np.array_equal(got, want)
+
+
+def test_alt_sharded_no_frames():
+    """n_total = 0: every rank owns nothing and returns at once."""
+    frames = np.zeros((0, 8, 16, 4), dtype=np.uint8)
+    got = _sharded(3, frames, _props(), [], 2, False)
+    assert got.shape == (0, 8, 16, 4)
 
 
 @pytest.mark.parametrize("world", [2, 3])
