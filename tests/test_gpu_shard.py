@@ -308,3 +308,61 @@ def test_native_alt_sharded_over_host_transport(world, host_ptrs):
     finally:
         r.close()
     assert np.array_equal(np.concatenate([parts[k] for k in range(world)]), want)
+
+
+def _native_compat_worker(rank, world, port, n_total, host_ptrs, result_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cs = comm = None
+    try:
+        from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+        from dips_amd.comm import Comm, TorchHostTransport, shard_range
+        torch.cuda.set_device(0)
+        s, e = shard_range(n_total, world, rank)
+        frames = _alt_frames(n_total)[s:e]
+        cs = ComputeState(True, 3, 4.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+        comm = Comm.host(TorchHostTransport(), world, rank, 0)
+        if host_ptrs:
+            out = cs.frame_callback_batch_sharded(comm, 40, 24, frames, n_total)
+        else:
+            dev = torch.from_numpy(frames).cuda()
+            o = torch.empty_like(dev)
+            cs.frame_callback_batch_sharded_device(comm, dev, o, n_total)
+            torch.cuda.synchronize()
+            out = o.cpu().numpy()
+        result_q.put((rank, out))
+    finally:
+        if cs is not None:
+            cs.close()
+        if comm is not None:
+            comm.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,host_ptrs", [(2, False), (3, True)])
+def test_native_compat_sharded_over_host_transport(world, host_ptrs):
+    """dips_frame_callback_batch_sharded in `world` processes over
+    DIPS_COMM_HOST (gloo), window 3: the ranks' outputs equal one
+    ComputeState's frame_callback_batch over every frame."""
+    from dips_amd import ChromaFilter, ComputeState, DiPsFilter
+    n_total = 26
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_compat_worker, args=(r, world, port, n_total, host_ptrs, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        parts = dict(q.get(timeout=300) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    cs = ComputeState(True, 3, 4.0, DiPsFilter.Sigmoid, ChromaFilter.None_)
+    try:
+        want = cs.frame_callback_batch(40, 24, _alt_frames(n_total))
+    finally:
+        cs.close()
+    assert np.array_equal(np.concatenate([parts[k] for k in range(world)]), want)
