@@ -65,9 +65,29 @@ R on_exception(dips_status st) noexcept {
     }
 }
 
+// The calling thread's current HIP device, put back on exit: an entry point
+// binds its handle's device (hipSetDevice) and must not leave the caller --
+// torch, another library, the rank thread of another GPU -- on it.  Host-only
+// functions (guard(nullptr, ...)) skip it and never touch the HIP runtime.
+// current_device / set_device are the HIP calls (dips_abi.hip); -1 = none.
+int current_device() noexcept;
+void set_device(int dev) noexcept;
+struct DeviceRestore {
+    int dev;
+    DeviceRestore() noexcept : dev(current_device()) {}
+    ~DeviceRestore() {
+        if (dev >= 0 && current_device() != dev) set_device(dev);
+    }
+    DeviceRestore(const DeviceRestore&) = delete;
+    DeviceRestore& operator=(const DeviceRestore&) = delete;
+};
+struct NoRestore {};
+
 template <typename Where, typename Body>
 auto guard(Where where, Body&& body) noexcept -> decltype(body()) {
     using R = decltype(body());
+    [[maybe_unused]] std::conditional_t<std::is_same_v<std::decay_t<Where>, std::nullptr_t>, NoRestore, DeviceRestore>
+        restore;
     try {
         return body();
     } catch (const std::bad_alloc&) {

@@ -117,6 +117,14 @@ int occupancy_blocks(dips_handle* h, const void* kernel) {
 using dips_abi::guard;
 using namespace dips_internal;
 
+namespace dips_abi {
+int current_device() noexcept {
+    int d = -1;
+    return hipGetDevice(&d) == hipSuccess ? d : -1;
+}
+void set_device(int dev) noexcept { (void)hipSetDevice(dev); }
+}  // namespace dips_abi
+
 extern "C" {
 
 int dips_abi_version(void) {

@@ -12,7 +12,9 @@
  *
  * Threading: a handle is not internally synchronised (the reference uses
  * ComputeState under an RwLock write guard, dips/src/frame_extractor.rs:232);
- * a handle may move between threads.  The caller owns every buffer.
+ * a handle may move between threads.  The caller owns every buffer.  Every
+ * entry point leaves the calling thread's current HIP device as it found it
+ * (work runs on the handle's device).
  */
 #ifndef DIPS_HIP_H
 #define DIPS_HIP_H

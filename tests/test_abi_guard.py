@@ -136,6 +136,10 @@ void note_error(dips_alt_handle* h, const char* m) noexcept { if (h) h->err = m;
 static std::string g_create;
 void note_error(CreateTag, const char* m) noexcept { g_create = m; }
 void note_error(AltCreateTag, const char* m) noexcept { g_create = m; }
+// the HIP device of the calling thread, simulated
+static int g_dev = 1, g_dev_reads = 0;
+int current_device() noexcept { ++g_dev_reads; return g_dev; }
+void set_device(int d) noexcept { g_dev = d; }
 }
 using dips_abi::guard;
 int main() {
@@ -157,6 +161,16 @@ int main() {
     guard(&h, [&]() -> void { ran = true; throw std::runtime_error("void"); });
     bad += !ran || h.err != "void";
     bad += guard(&h, [&]() -> int { return 7; }) != 7;
+    // the caller's device is put back, also when the body throws; host-only
+    // functions (nullptr) never read it
+    dips_abi::g_dev = 1;
+    bad += guard(&h, [&]() -> int { dips_abi::g_dev = 3; return 0; }) != 0;
+    bad += dips_abi::g_dev != 1;
+    guard(&h, [&]() -> void { dips_abi::g_dev = 2; throw std::runtime_error("x"); });
+    bad += dips_abi::g_dev != 1;
+    const int reads = dips_abi::g_dev_reads;
+    (void)guard(nullptr, [&]() -> int { return 0; });
+    bad += dips_abi::g_dev_reads != reads;
     std::printf("bad %d\n", bad);
     return bad != 0;
 }
