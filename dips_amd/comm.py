@@ -197,11 +197,20 @@ class TorchHostTransport:
 
 def rccl_from_process_group(device: int, group=None) -> Comm:
     """The RCCL communicator of an initialised torch process group's ranks:
-    rank 0's unique id travels over the group (broadcast_object_list)."""
+    rank 0's unique id travels over the group (broadcast_object_list).  If
+    rank 0 cannot make one, every rank raises (none is left waiting in the
+    broadcast or in ncclCommInitRank)."""
     import torch.distributed as dist
-    uid: List[Optional[bytes]] = [Comm.unique_id() if dist.get_rank(group) == 0 else None]
-    dist.broadcast_object_list(uid, src=0, group=group)
-    return Comm.rccl(uid[0], dist.get_world_size(group), dist.get_rank(group), device)
+    msg: List[Optional[object]] = [None, None]  # [unique id, rank 0's error]
+    if dist.get_rank(group) == 0:
+        try:
+            msg[0] = Comm.unique_id()
+        except Exception as e:  # travels to every rank, raised there
+            msg[1] = f"{type(e).__name__}: {e}"
+    dist.broadcast_object_list(msg, src=0, group=group)
+    if msg[0] is None:
+        raise _lib.DipsError(_lib.DIPS_ERR_COMM, f"rank 0 made no RCCL unique id ({msg[1]})")
+    return Comm.rccl(msg[0], dist.get_world_size(group), dist.get_rank(group), device)
 
 
 __all__ = ["Comm", "TorchHostTransport", "rccl_from_process_group", "shard_range"]

@@ -88,3 +88,45 @@ def test_error_code_and_abi():
     hdr = open(_lib.HEADER_PATH).read()
     assert "DIPS_ERR_COMM = -8" in hdr and "#define DIPS_COMM_ID_BYTES 128u" in hdr
     assert _lib.COMM_ID_BYTES == 128
+
+
+def _uid_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    from dips_amd import comm as comm_mod
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def no_uid():
+            raise _lib.DipsError(_lib.DIPS_ERR_COMM, "bootstrap unavailable")
+        comm_mod.Comm.unique_id = staticmethod(no_uid)  # rank 0 cannot make the id
+        try:
+            comm_mod.rccl_from_process_group(0)
+            q.put((rank, "returned"))
+        except _lib.DipsError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_from_process_group_fails_on_every_rank():
+    """Rank 0 failing to make the unique id raises on every rank instead of
+    leaving the others in the broadcast (gloo, 2 processes, no device)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_uid_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        got = dict(q.get(timeout=120) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all("no RCCL unique id" in got[r] and "bootstrap unavailable" in got[r] for r in range(2)), got
